@@ -1,0 +1,89 @@
+"""Packaged assets and their bootstrap.
+
+* ``m2kassets/`` - containerizer detector directories (``dockerfiles/*`` with
+  ``m2kdfdetect.sh`` + ``Dockerfile`` template, ``s2i/*`` with
+  ``m2ks2idetect.sh`` + ``.s2i/environment``).  Copied at start-up into a fresh
+  temp dir exactly like the reference unpacks its embedded tar
+  (``internal/common/utils.go:550-582``), so plans keep the portable
+  ``m2kassets/...`` relative paths.
+* ``templates/`` - output/build-script Go templates.
+* ``clusters.json`` - the 7 built-in target-cluster profiles.
+* ``cfbuildpacks.json`` - built-in CF buildpack containerization map.
+"""
+
+import json
+import os
+import shutil
+import tempfile
+
+from ..utils import log
+from ..utils.constants import ASSETS_DIR, TEMP_DIR_PREFIX, settings
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ASSETS_SRC = os.path.join(HERE, "m2kassets")
+TEMPLATES_DIR = os.path.join(HERE, "templates")
+
+_templates = {}
+_clusters = None
+
+
+def template(name):
+    t = _templates.get(name)
+    if t is None:
+        with open(os.path.join(TEMPLATES_DIR, name)) as f:
+            t = f.read()
+        _templates[name] = t
+    return t
+
+
+def builtin_clusters():
+    """{name: {"storageClasses": [...], "apiKindVersionMap": {...}}}"""
+    global _clusters
+    if _clusters is None:
+        with open(os.path.join(HERE, "clusters.json")) as f:
+            _clusters = json.load(f)
+    return _clusters
+
+
+def builtin_cf_buildpacks():
+    with open(os.path.join(HERE, "cfbuildpacks.json")) as f:
+        return json.load(f)["buildpackContainerizers"]
+
+
+def _copy_tree(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    for entry in os.scandir(src):
+        s = entry.path
+        d = os.path.join(dst, entry.name)
+        if entry.is_dir(follow_symlinks=False):
+            _copy_tree(s, d)
+        else:
+            shutil.copyfile(s, d)
+            shutil.copymode(s, d)
+
+
+def create_assets_data():
+    """Create ``<tmp>/m2kassets`` populated with the detector assets.
+
+    Returns (assets_path, temp_path)."""
+    temp_path = os.path.abspath(settings.temp_path)
+    assets_path = os.path.abspath(settings.assets_path)
+    try:
+        temp_path = tempfile.mkdtemp(prefix=TEMP_DIR_PREFIX)
+        assets_path = os.path.join(temp_path, ASSETS_DIR)
+    except OSError:
+        log.error("Unable to create temp dir. Defaulting to local path.")
+    _copy_tree(ASSETS_SRC, assets_path)
+    return assets_path, temp_path
+
+
+def setup():
+    """Create the assets dir and point the global settings at it (cmd main)."""
+    assets_path, temp_path = create_assets_data()
+    settings.temp_path = temp_path
+    settings.assets_path = assets_path
+    return temp_path
+
+
+def cleanup(temp_path=None):
+    shutil.rmtree(temp_path or settings.temp_path, ignore_errors=True)

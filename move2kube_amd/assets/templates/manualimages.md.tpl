@@ -1,0 +1,6 @@
+Manual containers
+-----------------
+There is no known automated containerization approach for the below container requirements.
+
+{{range $image := .Images}}{{$image}}
+{{end}}

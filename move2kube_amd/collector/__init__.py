@@ -1,0 +1,76 @@
+"""Metadata collectors for ``move2kube collect`` (reference ``internal/collector/``).
+
+Each collector shells out to the platform CLI that already holds the user's
+credentials (kubectl/oc, docker, cf) and writes a move2kube metadata YAML
+under ``<out>/m2k_collect/<area>/``.  Collectors are selected by annotation
+(``-a k8s,cf``); a failing collector is logged and skipped.
+"""
+
+import subprocess
+
+from ..utils import log
+
+
+class Collector:
+    annotations = ()
+
+    def get_annotations(self):
+        return list(self.annotations)
+
+    def collect(self, input_path, output_path):
+        raise NotImplementedError
+
+    def __repr__(self):
+        return "*collector.%s" % type(self).__name__
+
+
+class CommandError(RuntimeError):
+    def __init__(self, argv, code, output=b""):
+        super().__init__("exit status %d" % code if code >= 0 else "signal: %d" % -code)
+        self.argv = argv
+        self.code = code
+        self.output = output
+
+
+def run(argv, combined=False, timeout=300):
+    """Run a command; stdout bytes (stdout+stderr with ``combined``). Raises
+    :class:`CommandError` on a non-zero exit and FileNotFoundError if missing."""
+    p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT if combined else subprocess.PIPE,
+                       stdin=subprocess.DEVNULL, timeout=timeout)
+    if p.returncode != 0:
+        raise CommandError(argv, p.returncode, p.stdout)
+    return p.stdout
+
+
+def get_collectors():
+    from .cf import CfAppsCollector, CFContainerTypesCollector
+    from .cluster import ClusterCollector
+    from .images import ImagesCollector
+    return [ClusterCollector(), ImagesCollector(), CFContainerTypesCollector(), CfAppsCollector()]
+
+
+def has_overlap(a, b):
+    return any(x.casefold() == y.casefold() for x in a for y in b)
+
+
+def collect(input_path, output_path, annotations=()):
+    import os
+    from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION
+    try:
+        os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+    except OSError as e:
+        log.fatal("Unable to create output directory at path %r Error: %r", output_path, str(e))
+    log.info("Begin collection")
+    for c in get_collectors():
+        if annotations and not has_overlap(annotations, c.get_annotations()):
+            continue
+        log.info("[%r] Begin collection", c)
+        try:
+            c.collect(input_path, output_path)
+        except Exception as e:  # noqa: BLE001
+            if isinstance(e, log.FatalError):
+                raise
+            log.warning("[%r] failed. Error: %r", c, str(e))
+            continue
+        log.info("[%r] Done", c)
+    log.info("Collection done")

@@ -1,0 +1,307 @@
+"""Target-cluster metadata (reference ``internal/collector/clustercollector.go``).
+
+Storage classes come from ``<kubectl|oc> get sc -o yaml``.  The kind ->
+group/version map is taken from the discovery API first (here: the raw
+``/api`` + ``/apis`` discovery documents fetched with ``kubectl get --raw``,
+i.e. the same kubeconfig client-go would use) and, if that fails, from the
+CLI (``api-resources -o name`` + ``explain``).  Versions are finally ordered
+by the global group policy: ``*.openshift.io``, ``*.k8s.io``, ``apps``,
+``extensions``, other named groups, then the core group.
+"""
+
+import json
+import os
+import re
+import shutil
+
+from ..k8s import scheme
+from ..models import collection
+from ..utils import common, log, yamlio
+from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
+from . import Collector, CommandError, run
+
+GLOBAL_GROUP_ORDER = [r"^.+\.openshift\.io$", r"^.+\.k8s\.io$", r"^apps$", r"^extensions$"]
+
+
+def _gv_string(group, version):
+    return version if group == "" else "%s/%s" % (group, version)
+
+
+def _parse_gv(gv):
+    g, v = common.parse_group_version(gv)
+    return g, v
+
+
+class ClusterCollector(Collector):
+    annotations = ("k8s",)
+
+    def __init__(self):
+        self.cluster_cmd = ""
+
+    # -- helpers -----------------------------------------------------------
+    def get_cluster_command(self):
+        if self.cluster_cmd:
+            return self.cluster_cmd
+        for cmd in ("kubectl", "oc"):
+            if shutil.which(cmd):
+                self.cluster_cmd = cmd
+                return cmd
+            log.warning('Unable to find the %s command. Error: %r', cmd,
+                        'exec: "%s": executable file not found in $PATH' % cmd)
+        return ""
+
+    def _run(self, *args, combined=False):
+        return run([self.get_cluster_command()] + list(args), combined=combined)
+
+    def get_cluster_context_name(self):
+        name = self._run("config", "current-context").decode("utf-8", "replace")
+        # the reference keeps kubectl's trailing newline in the name
+        return name.strip() if settings.fixed else name
+
+    def interpret_error(self, output):
+        for term in ("Unauthorized", "Username"):
+            if self.get_cluster_command() == "oc" and term in output:
+                return "Please login to cluster before running collect. (e.g. oc login <cluster url> --token=<token string>)"
+            if self.get_cluster_command() == "kubectl" and term in output:
+                return ("Please configure the cluster authentication with following instructions: "
+                        "[https://kubernetes.io/docs/reference/kubectl/cheatsheet/#kubectl-context-and-configuration]")
+        return ""
+
+    def get_storage_classes(self):
+        try:
+            out = self._run("get", "sc", "-o", "yaml", combined=True)
+        except CommandError as e:
+            desc = self.interpret_error(e.output.decode("utf-8", "replace"))
+            if desc:
+                log.warning("Error while running %s. %s", self.get_cluster_command(), desc)
+            else:
+                log.warning("Error while fetching storage classes using command [%s get sc -o yaml]",
+                            self.get_cluster_command())
+            raise
+        doc = yamlio.load(out.decode("utf-8", "replace")) or {}
+        names = []
+        for sc in doc.get("items") or []:
+            if isinstance(sc, dict):
+                names.append(str((sc.get("metadata") or {}).get("name", "")))
+            else:
+                log.warning("Unknown type detected in cluster metadata [%s]", type(sc).__name__)
+        return names
+
+    # -- discovery API -----------------------------------------------------
+    def _raw(self, path):
+        return json.loads(self._run("get", "--raw", path))
+
+    def get_server_groups(self):
+        """[(name, preferred_gv, [gv...])] like ``ServerGroups()`` (core group first)."""
+        groups = []
+        core = self._raw("/api")
+        versions = core.get("versions") or []
+        if versions:
+            groups.append(("", versions[0], list(versions)))
+        for g in self._raw("/apis").get("groups") or []:
+            gvs = [v.get("groupVersion", "") for v in g.get("versions") or []]
+            pref = (g.get("preferredVersion") or {}).get("groupVersion", gvs[0] if gvs else "")
+            groups.append((g.get("name", ""), pref, gvs))
+        return groups
+
+    def get_preferred_resources_using_api(self, groups):
+        gv_list = []
+        for name, pref, gvs in groups:
+            if pref == "":
+                continue
+            gv_list.append(pref)
+            for pgv in scheme.prioritized_versions_for_group(name):
+                if pgv == pref:
+                    continue
+                if pgv in gvs:
+                    gv_list.append(pgv)
+            for gv in gvs:
+                if gv not in gv_list:
+                    gv_list.append(gv)
+        return gv_list
+
+    def get_kinds_for_groups(self, groups):
+        kinds = {}
+        for _name, _pref, gvs in groups:
+            for gv in gvs:
+                path = "/api/" + gv if "/" not in gv else "/apis/" + gv
+                try:
+                    res = self._raw(path)
+                except (CommandError, ValueError) as e:
+                    log.warning("Ignoring group-version [%s]. %s", gv, e)
+                    continue
+                for r in res.get("resources") or []:
+                    if "/" in r.get("name", ""):
+                        continue  # subresources
+                    lst = kinds.setdefault(r.get("kind", ""), [])
+                    if gv not in lst:
+                        lst.append(gv)
+        return kinds
+
+    def sort_gv_by_preference(self, pref, kinds):
+        for kind, gvs in kinds.items():
+            ordered = [p for p in pref if p in gvs]
+            if settings.fixed:
+                # the reference's inverted parse check drops every version that is not preferred
+                rest = [p for p in gvs if p not in ordered]
+                ordered.extend(self.cluster_by_groups_and_sort_versions(rest))
+            kinds[kind] = ordered
+
+    def collect_using_api(self):
+        if not self.get_cluster_command():
+            raise RuntimeError("no cluster CLI")
+        groups = self.get_server_groups()
+        gv_list = self.get_preferred_resources_using_api(groups)
+        if not gv_list:
+            raise RuntimeError("Failed to retrieve preferred group information from cluster")
+        kinds = self.get_kinds_for_groups(groups)
+        if not kinds:
+            raise RuntimeError("Failed to retrieve <kind, group-version> information from cluster")
+        self.sort_gv_by_preference(gv_list, kinds)
+        return kinds
+
+    # -- CLI fallback ------------------------------------------------------
+    def get_gvk_using_name_cli(self, name):
+        out = self._run("explain", name).decode("utf-8", "replace")
+        lines = out.split("\n")
+        if len(lines) < 2:
+            raise ValueError("Description incomplete")
+        if "KIND" not in lines[0]:
+            raise ValueError("no KIND")
+        kind = lines[0].split(":")[1].strip()
+        group, version = "", ""
+        if "VERSION" in lines[1]:
+            parts = lines[1].split(":")[1].strip().split("/")
+            if len(parts) == 2:
+                group, version = parts
+            else:
+                version = parts[0]
+        return kind, _gv_string(group, version)
+
+    def is_supported_gv(self, kind, gv):
+        try:
+            out = self._run("explain", kind, "--api-version=" + gv, "--recursive").decode("utf-8", "replace")
+        except (CommandError, OSError):
+            return False
+        lines = out.split("\n")
+        return len(lines) >= 2 and "VERSION" in lines[1]
+
+    def get_preferred_gv_using_cli(self, kind, groups):
+        out = []
+        for group, _v in groups:
+            prio = scheme.prioritized_versions_for_group(group)
+            if prio:
+                for gv in prio:
+                    if self.is_supported_gv(kind, gv):
+                        out.append(gv)
+                    else:
+                        log.debug("Group version not found by CLI for kind [%s]", kind)
+            else:
+                try:
+                    out.append(self.get_gvk_using_name_cli(kind)[1])
+                except (CommandError, OSError, ValueError):
+                    pass
+        return out
+
+    def collect_using_cli(self):
+        out = self._run("api-resources", "-o", "name").decode("utf-8", "replace")
+        kinds = {}
+        for name in out.split("\n"):
+            parts = name.split(".")
+            try:
+                kind, gv = self.get_gvk_using_name_cli(parts[0])
+            except (CommandError, OSError, ValueError):
+                log.debug("Erroring parsing kind from CLI output")
+                continue
+            group = ".".join(p.strip() if i > 0 else p for i, p in enumerate(parts[1:]))
+            if group:
+                kinds.setdefault(kind, []).append((group, ""))
+            else:
+                kinds[kind] = [("", gv)]
+        api = {}
+        for kind in sorted(kinds):
+            groups = kinds[kind]
+            if len(groups) == 1 and groups[0][0] == "":
+                api[kind] = [groups[0][1]]
+                continue
+            api[kind] = self.get_preferred_gv_using_cli(kind, groups)
+        return api
+
+    # -- ordering ----------------------------------------------------------
+    @staticmethod
+    def _matching(group_regex, gvs):
+        rx = re.compile(group_regex)
+        out = []
+        for gv in gvs:
+            g, _ = _parse_gv(gv)
+            if g and rx.search(g):
+                out.append(gv)
+        return out
+
+    def group_order_policy(self, kinds):
+        for kind, gvs in kinds.items():
+            ordered = []
+            for rx in GLOBAL_GROUP_ORDER:
+                ordered.extend(self._matching(rx, gvs))
+            for gv in gvs:
+                g, _ = _parse_gv(gv)
+                if common.is_string_present(ordered, gv):
+                    continue
+                if g != "":
+                    ordered.append(gv)
+            for gv in gvs:
+                g, _ = _parse_gv(gv)
+                if g == "":
+                    ordered.append(gv)
+            kinds[kind] = ordered if ordered else gvs
+
+    @staticmethod
+    def _version_key(v):
+        """Kubernetes-style version priority: GA > beta > alpha, higher numbers first."""
+        m = re.match(r"^v(\d+)(?:(alpha|beta)(\d+))?$", v)
+        if not m:
+            return (0, 0, 0, v)
+        stage = {"alpha": 1, "beta": 2, None: 3}[m.group(2)]
+        return (stage, int(m.group(1)), int(m.group(3) or 0), v)
+
+    def cluster_by_groups_and_sort_versions(self, gvs):
+        by_group = {}
+        for gv in gvs:
+            g, v = _parse_gv(gv)
+            by_group.setdefault(g, []).append(v)
+        out = []
+        for g in sorted(by_group):
+            for v in sorted(by_group[g], key=self._version_key, reverse=True):
+                out.append(_gv_string(g, v))
+        return out
+
+    # -- entry point -------------------------------------------------------
+    def collect(self, input_path, output_path):
+        output_path = os.path.join(output_path, "clusters")
+        os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+        if self.get_cluster_command() == "":
+            msg = "No kubectl or oc in path. Add kubectl to path and rerun to collect data about the cluster in context."
+            log.warning(msg)
+            raise RuntimeError(msg)
+        try:
+            name = self.get_cluster_context_name()
+        except (CommandError, OSError) as e:
+            log.warning("Unable to access cluster in context : %s", e)
+            raise
+        cm = collection.ClusterMetadata(name)
+        try:
+            cm.spec.storage_classes = self.get_storage_classes()
+        except Exception:  # noqa: BLE001
+            cm.spec.storage_classes = []
+        try:
+            kinds = self.collect_using_api()
+        except Exception as e:  # noqa: BLE001
+            log.warning("Failed to collect using the API. Error: %r . Falling back to using the CLI.", str(e))
+            try:
+                kinds = self.collect_using_cli()
+            except Exception as e2:  # noqa: BLE001
+                log.warning("Failed to collect using the CLI. Error: %r", str(e2))
+                raise
+        self.group_order_policy(kinds)
+        cm.spec.api_kind_version_map = kinds
+        common.write_yaml(os.path.join(output_path, common.normalize_for_filename(cm.name) + ".yaml"), cm)

@@ -1,0 +1,132 @@
+"""Image metadata via ``docker inspect`` (reference ``internal/collector/imagescollector.go``)."""
+
+import json
+import os
+import re
+
+from ..models.collection import ImageInfo
+from ..utils import common, log
+from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
+from . import Collector, CommandError, run
+
+_NUM = re.compile(r"[0-9]+")
+
+
+def cast_to_int_e(s):
+    """spf13/cast ``ToIntE`` for strings (base prefix aware, "1.0" -> 1)."""
+    if isinstance(s, bool):
+        return int(s)
+    if isinstance(s, int):
+        return s
+    t = str(s)
+    if "." in t:
+        head, _, tail = t.partition(".")
+        if tail.strip("0") == "":
+            t = head
+    return int(t, 0)
+
+
+def get_image_info(data):
+    info = ImageInfo()
+    try:
+        images = json.loads(data)
+    except ValueError as e:
+        log.error("Unable to unmarshal image info : %s", e)
+        images = []
+    for image in images or []:
+        cfg = image.get("ContainerConfig") or {}
+        info.tags = list(image.get("RepoTags") or [])
+        try:
+            info.user_id = cast_to_int_e(cfg.get("User", ""))
+        except (ValueError, TypeError):
+            log.debug("UserID not available in image metadata for [%s]", (info.tags or [""])[0])
+            info.user_id = -1
+        info.accessed_dirs.append(cfg.get("WorkingDir", ""))
+        for key in sorted(cfg.get("ExposedPorts") or {}):
+            m = _NUM.search(key)
+            if m is None:
+                log.debug("PortNumber not available in image metadata for [%s]", (info.tags or [""])[0])
+                continue
+            info.ports.append(int(m.group(0)))
+    return info
+
+
+def get_docker_inspect_result(image):
+    try:
+        return run(["docker", "inspect", image], combined=True)
+    except FileNotFoundError as e:
+        log.warning("Error while running docker-inspect: %s", e)
+        raise
+    except CommandError as e:
+        out = e.output.decode("utf-8", "replace")
+        if "permission denied" in out:
+            log.warning("Error while running docker-inspect due to lack of permissions")
+            log.warning("Please refer to [https://docs.docker.com/engine/install/linux-postinstall/] to fix this issue")
+        elif "No such object" in out:
+            log.warning('Image [%s] not available in local image repo. Run "docker pull %s"', image, image)
+            return None
+        else:
+            log.warning("Error while running docker-inspect: %s", e)
+        raise
+
+
+def get_all_image_names():
+    try:
+        out = run(["docker", "image", "list", "--format", "{{.Repository}}:{{.Tag}}"])
+    except (OSError, CommandError) as e:
+        log.warning("Error while running docker image list : %s", e)
+        raise
+    images = []
+    for image in out.decode("utf-8", "replace").split("\n"):
+        if image.startswith("<none>") or image.endswith("<none>"):
+            log.debug("Ignore image with <none> : %s", image)
+            continue
+        if image:
+            images.append(image)
+    # the reference filters the list but never appends to its result
+    return images if settings.fixed else []
+
+
+def get_dc_image_names(directory):
+    names = []
+    for path in common.get_files_by_ext(directory, [".yml", ".yaml"]):
+        try:
+            doc = common.read_yaml(path)
+        except Exception:  # noqa: BLE001
+            continue
+        if not isinstance(doc, dict):
+            continue
+        services = doc.get("services")
+        if not isinstance(services, dict):
+            continue
+        for name in sorted(services):
+            svc = services[name]
+            names.append(str(svc.get("image", "")) if isinstance(svc, dict) else "")
+    return names
+
+
+class ImagesCollector(Collector):
+    annotations = ("k8s", "dockerswarm", "dockercompose")
+
+    def collect(self, input_path, output_path):
+        output_path = os.path.join(output_path, "images")
+        os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+        names = get_all_image_names() if input_path == "" else get_dc_image_names(input_path)
+        log.debug("Images : %s", names)
+        for name in names:
+            try:
+                data = get_docker_inspect_result(name)
+            except (OSError, CommandError):
+                continue
+            if data is None:
+                continue
+            info = get_image_info(data)
+            shortest = ""
+            for tag in info.tags:
+                if shortest == "" or len(shortest) > len(tag):
+                    shortest = tag
+            path = os.path.join(output_path, common.normalize_for_filename(shortest) + ".yaml")
+            try:
+                common.write_yaml(path, info)
+            except OSError as e:
+                log.error("Unable to write file %s : %s", path, e)

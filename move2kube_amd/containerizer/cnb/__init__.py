@@ -1,0 +1,61 @@
+"""CNB containerizer (reference ``internal/containerizer/cnbcontainerizer.go``)."""
+
+import threading
+
+from ... import assets
+from ...models import ir as irtypes
+from ...models import plan as plantypes
+from ...utils import common
+from ...utils.constants import DEFAULT_SERVICE_PORT
+from ..base import Containerizer, ContainerizerError
+from . import providers
+
+DEFAULT_BUILDERS = ["cloudfoundry/cnb:cflinuxfs3", "gcr.io/buildpacks/builder"]
+
+_cache = {}
+_cache_lock = threading.Lock()
+
+
+def reset_cache():
+    with _cache_lock:
+        _cache.clear()
+
+
+class CNBContainerizer(Containerizer):
+    build_type = plantypes.CNB
+
+    def __init__(self):
+        self.builders = list(DEFAULT_BUILDERS)
+
+    def init(self, path):
+        self.builders = list(DEFAULT_BUILDERS)
+
+    def get_target_options(self, plan, path):
+        with _cache_lock:
+            if path in _cache:
+                return list(_cache[path])
+        supported = [b for b in self.builders if providers.is_builder_supported(path, b)]
+        with _cache_lock:
+            _cache[path] = supported
+        return list(supported)
+
+    def get_container(self, plan, service):
+        container = irtypes.new_container(self.build_type, service.image, True)
+        if service.container_build_type != self.build_type:
+            raise ContainerizerError("Service %s has container build type %s . Expected %s"
+                                     % (service.service_name, service.container_build_type, self.build_type))
+        if not service.target_options:
+            raise ContainerizerError("Service %s has no containerization target options" % service.service_name)
+        builder = service.target_options[0]
+        script = common.get_string_from_template(assets.template("cnbbuild.sh.tpl"),
+                                                 {"ImageName": service.image, "Builder": builder})
+        srcs = service.source_artifacts.get(plantypes.SOURCE_DIRECTORY_ARTIFACT) or []
+        if not srcs:
+            raise ContainerizerError("Service %s has no source code directory specified" % service.service_name)
+        rel = common.go_rel(plan.root_dir, srcs[0])
+        container.add_file(common.go_join(rel, service.service_name + "-cnb-build.sh"), script)
+        container.add_exposed_port(DEFAULT_SERVICE_PORT)
+        return container
+
+    def get_all_buildpacks(self):
+        return providers.get_all_buildpacks(self.builders)

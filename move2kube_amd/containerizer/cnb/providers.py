@@ -1,0 +1,441 @@
+"""Cloud Native Buildpack detection providers (reference ``internal/containerizer/cnb/``).
+
+Fallback chain ``[docker Engine API, podman, pack, runc+skopeo+umoci]``: the
+first provider that does not error decides whether a builder image supports
+a source directory (``/cnb/lifecycle/detector`` exit status).  Buildpack lists
+come from the builder image label ``io.buildpacks.buildpack.order``.
+
+Every provider degrades gracefully when its runtime is absent (the common case
+on build hosts and on this framework's CI), and availability probes are cached
+per process so that a missing runtime costs one probe, not one per directory.
+"""
+
+import http.client
+import io
+import json
+import os
+import shutil
+import socket
+import subprocess
+import tarfile
+import threading
+import urllib.parse
+
+from ...utils import common, log
+from ...utils.constants import settings
+
+ORDER_LABEL = "io.buildpacks.buildpack.order"
+DOCKER_SOCK = "/var/run/docker.sock"
+
+_warned_not_supported = False
+_warned_long_wait = False
+_lock = threading.Lock()
+
+
+def get_builders_from_label(label):
+    try:
+        order = json.loads(label)
+    except (ValueError, TypeError) as e:
+        log.warning("Unable to read order : %s", e)
+        return []
+    out = []
+    for og in order or []:
+        for bp in (og or {}).get("group") or []:
+            out.append(bp.get("id", ""))
+    return out
+
+
+class ProviderError(RuntimeError):
+    pass
+
+
+# ---------------------------------------------------------------------------
+# Docker Engine API over the unix socket
+# ---------------------------------------------------------------------------
+
+class _UnixHTTPConnection(http.client.HTTPConnection):
+    def __init__(self, path, timeout=60):
+        super().__init__("localhost", timeout=timeout)
+        self._path = path
+
+    def connect(self):
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.settimeout(self.timeout)
+        s.connect(self._path)
+        self.sock = s
+
+
+class DockerAPIProvider:
+    """Talks to dockerd through ``DOCKER_HOST`` (unix socket) like docker's Go client."""
+
+    def __init__(self):
+        self.sock_state = None  # None unknown / True / False
+        self.available_images = set()
+        host = os.environ.get("DOCKER_HOST", "unix://" + DOCKER_SOCK)
+        self.sock_path = host[len("unix://"):] if host.startswith("unix://") else None
+
+    def _request(self, method, path, body=None, headers=None, timeout=600, raw=False):
+        if not self.sock_path or not os.path.exists(self.sock_path):
+            raise ProviderError("docker socket not available")
+        conn = _UnixHTTPConnection(self.sock_path, timeout=timeout)
+        try:
+            hdrs = dict(headers or {})
+            if body is not None and not isinstance(body, (bytes, bytearray)) and not hasattr(body, "read"):
+                body = json.dumps(body).encode()
+                hdrs.setdefault("Content-Type", "application/json")
+            conn.request(method, path, body=body, headers=hdrs)
+            resp = conn.getresponse()
+            data = resp.read()
+        except OSError as e:
+            raise ProviderError(str(e))
+        finally:
+            conn.close()
+        if resp.status >= 400:
+            raise ProviderError("docker API %s %s: %d %s" % (method, path, resp.status, data[:200]))
+        if raw:
+            return data
+        return json.loads(data.decode() or "null") if data else None
+
+    def pull_image(self, image):
+        name, tag = (image.rsplit(":", 1) + ["latest"])[:2] if ":" in image.rsplit("/", 1)[-1] else (image, "latest")
+        self._request("POST", "/images/create?" + urllib.parse.urlencode({"fromImage": name, "tag": tag}), raw=True)
+
+    def inspect_image(self, image):
+        return self._request("GET", "/images/%s/json" % urllib.parse.quote(image, safe=""))
+
+    def _copy_dir(self, cid, src, dst):
+        buf = io.BytesIO()
+        with tarfile.open(fileobj=buf, mode="w") as tw:
+            for root, dirs, files in os.walk(src):
+                dirs.sort()
+                for name in sorted(dirs) + sorted(files):
+                    full = os.path.join(root, name)
+                    rel = os.path.relpath(full, src)
+                    try:
+                        tw.add(full, arcname=os.path.join(dst.lstrip("/"), rel), recursive=False)
+                    except OSError:
+                        continue
+        self._request("PUT", "/containers/%s/archive?path=/" % cid, body=buf.getvalue(),
+                      headers={"Content-Type": "application/x-tar"}, raw=True)
+
+    def run_container(self, image, cmd="", volsrc="", voldest=""):
+        cfg = {"Image": image}
+        if cmd:
+            cfg["Cmd"] = [cmd]
+        host = {}
+        if volsrc and voldest:
+            host["Mounts"] = [{"Type": "bind", "Source": volsrc, "Target": voldest, "ReadOnly": True}]
+        try:
+            resp = self._request("POST", "/containers/create", body=dict(cfg, HostConfig=host))
+        except ProviderError:
+            resp = self._request("POST", "/containers/create", body=cfg)
+            if volsrc and voldest:
+                self._copy_dir(resp["Id"], volsrc, voldest)
+        cid = resp["Id"]
+        try:
+            self._request("POST", "/containers/%s/start" % cid, raw=True)
+            st = self._request("POST", "/containers/%s/wait?condition=not-running" % cid)
+            logs = self._request("GET", "/containers/%s/logs?stdout=1" % cid, raw=True).decode("utf-8", "replace")
+            code = (st or {}).get("StatusCode", 0)
+            if code != 0:
+                raise ProviderError("Container execution terminated with error code : %d" % code)
+            return logs
+        finally:
+            try:
+                self._request("DELETE", "/containers/%s?force=1" % cid, raw=True)
+            except ProviderError:
+                pass
+
+    def is_sock_accessible(self):
+        if self.sock_state is None:
+            try:
+                self.pull_image("hello-world")
+                self.run_container("hello-world")
+                self.sock_state = True
+            except (ProviderError, KeyError, ValueError):
+                self.sock_state = False
+        return self.sock_state
+
+    def is_builder_available(self, builder):
+        if not self.is_sock_accessible():
+            return False
+        if builder in self.available_images:
+            return True
+        try:
+            self.pull_image(builder)
+        except ProviderError as e:
+            log.warning("Error while pulling builder %s : %s", builder, e)
+            return False
+        self.available_images.add(builder)
+        return True
+
+    def is_builder_supported(self, path, builder):
+        if not self.is_builder_available(builder):
+            raise ProviderError("Builder image not available : %s" % builder)
+        try:
+            out = self.run_container(builder, "/cnb/lifecycle/detector", os.path.abspath(path), "/workspace")
+            log.debug(out)
+            return True
+        except ProviderError as e:
+            log.debug("Detect failed %s : %s", builder, e)
+            return False
+
+    def get_all_buildpacks(self, builders):
+        if not self.is_sock_accessible():
+            raise ProviderError("Container runtime not supported in this instance")
+        out = {}
+        for b in builders:
+            try:
+                info = self.inspect_image(b)
+            except ProviderError as e:
+                log.debug("Unable to inspect image %s : %s", b, e)
+                continue
+            labels = ((info or {}).get("Config") or {}).get("Labels") or {}
+            out[b] = get_builders_from_label(labels.get(ORDER_LABEL, ""))
+        return out
+
+
+# ---------------------------------------------------------------------------
+# podman CLI
+# ---------------------------------------------------------------------------
+
+def _run(cmd, timeout=600):
+    return subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                          timeout=timeout)
+
+
+class ContainerRuntimeProvider:
+    def __init__(self):
+        self.runtime = None  # "podman" | "none"
+        self.available = set()
+
+    def get_runtime(self):
+        if self.runtime is None:
+            if shutil.which("podman") is None:
+                self.runtime = "none"
+            else:
+                try:
+                    p = _run(["podman", "run", "--storage-driver=vfs", "--rm", "hello-world"])
+                    self.runtime = "podman" if p.returncode == 0 else "none"
+                except (OSError, subprocess.TimeoutExpired):
+                    self.runtime = "none"
+        return self.runtime if self.runtime != "none" else None
+
+    def is_builder_available(self, builder):
+        rt = self.get_runtime()
+        if rt is None:
+            return False
+        if builder in self.available:
+            return True
+        try:
+            p = _run([rt, "--storage-driver=vfs", "images", "-q", builder])
+            if p.returncode == 0 and p.stdout.strip():
+                self.available.add(builder)
+                return True
+            p = _run([rt, "pull", "--storage-driver=vfs", builder])
+        except (OSError, subprocess.TimeoutExpired):
+            return False
+        if p.returncode != 0:
+            log.warning("Error while pulling builder %s : %s", builder, p.stdout[:200])
+            return False
+        self.available.add(builder)
+        return True
+
+    def is_builder_supported(self, path, builder):
+        if not self.is_builder_available(builder):
+            raise ProviderError("Builder image not available : %s" % builder)
+        p = _run([self.runtime, "run", "--rm", "--storage-driver=vfs", "-v", os.path.abspath(path) + ":/workspace",
+                  builder, "/cnb/lifecycle/detector"])
+        return p.returncode == 0
+
+    def get_all_buildpacks(self, builders):
+        rt = self.get_runtime()
+        if rt is None:
+            raise ProviderError("Container runtime not supported in this instance")
+        out = {}
+        for b in builders:
+            p = _run([rt, "inspect", "--storage-driver=vfs", "--format",
+                      '{{ index .Config.Labels "' + ORDER_LABEL + '"}}', b])
+            if p.returncode != 0:
+                continue
+            out[b] = get_builders_from_label(p.stdout.decode())
+        return out
+
+
+# ---------------------------------------------------------------------------
+# pack CLI
+# ---------------------------------------------------------------------------
+
+class PackProvider:
+    def is_available(self):
+        return shutil.which("pack") is not None and os.path.exists(DOCKER_SOCK)
+
+    def is_builder_supported(self, path, builder):
+        if not self.is_available():
+            raise ProviderError("Pack not supported in this instance")
+        proc = subprocess.Popen(["pack", "build", "m2ktestcflinuxf2selector:1", "-B", builder, "-p", path],
+                                stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL)
+        try:
+            for raw in proc.stdout:
+                t = raw.decode("utf-8", "replace")
+                if "===> ANALYZING" in t:
+                    proc.kill()
+                    return True
+                if "No buildpack groups passed detection." in t:
+                    proc.kill()
+                    return False
+        finally:
+            try:
+                proc.kill()
+            except OSError:
+                pass
+            proc.wait()
+        raise ProviderError("Error while using pack")
+
+    def get_all_buildpacks(self, builders):
+        import re
+        out = {}
+        rx = re.compile(r"(?s)Group\s#\d+:[\r\n\s]+[^\s]+")
+        for b in builders:
+            try:
+                p = _run(["pack", "inspect-builder", b])
+            except (OSError, subprocess.TimeoutExpired) as e:
+                log.warning("Error while getting supported buildpacks for builder %s : %s", b, e)
+                continue
+            if p.returncode != 0:
+                continue
+            for m in rx.findall(p.stdout.decode("utf-8", "replace")):
+                out.setdefault(b, []).append(m.split()[-1])
+        return out
+
+
+# ---------------------------------------------------------------------------
+# runc + skopeo + umoci
+# ---------------------------------------------------------------------------
+
+class RuncProvider:
+    @staticmethod
+    def _paths():
+        # resolved at call time (the reference captured AssetsPath at package init - SURVEY 2.13 #11)
+        base = os.path.join(settings.assets_path, "cnb")
+        return os.path.join(base, "images"), os.path.join(base, "bundles")
+
+    def is_available(self):
+        return all(shutil.which(t) for t in ("runc", "skopeo", "umoci"))
+
+    def _init(self, builders):
+        images, bundles = self._paths()
+        os.makedirs(images, exist_ok=True)
+        os.makedirs(bundles, exist_ok=True)
+        for b in builders:
+            image, tag = common.get_image_name_and_tag(b)
+            if os.path.exists(os.path.join(images, image)):
+                continue
+            p = subprocess.run(["skopeo", "copy", "docker://" + b, "oci:" + image + ":" + tag], cwd=images,
+                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+            if p.returncode != 0:
+                continue
+            subprocess.run(["umoci", "unpack", "--image", image + ":" + tag, os.path.abspath(os.path.join(bundles, image))],
+                           cwd=images, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+
+    def is_builder_supported(self, path, builder):
+        if not self.is_available():
+            raise ProviderError("Runc Builder image not available : %s" % builder)
+        self._init([builder])
+        _, bundles = self._paths()
+        image, _ = common.get_image_name_and_tag(builder)
+        cfg_path = os.path.join(bundles, image, "config.json")
+        if not os.path.exists(os.path.dirname(cfg_path)):
+            raise ProviderError("Runc Builder image not available : %s" % builder)
+        spec = common.read_json(cfg_path)
+        mount = {"destination": "/workspace", "type": "bind", "source": os.path.abspath(path), "options": ["rbind", "ro"]}
+        mounts = spec.get("mounts") or []
+        for i, m in enumerate(mounts):
+            if m.get("destination") == "/workspace":
+                mounts[i] = mount
+                break
+        else:
+            mounts.append(mount)
+        spec["mounts"] = mounts
+        spec.setdefault("process", {})["args"] = ["/cnb/lifecycle/detector"]
+        spec["process"]["terminal"] = False
+        common.write_json(cfg_path, spec)
+        p = subprocess.run(["runc", "run", "cnbbuilder"], cwd=os.path.dirname(cfg_path),
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        if p.returncode != 0:
+            raise ProviderError("Error while executing runc")
+        return b"ERROR: No buildpack groups passed detection." not in p.stdout
+
+    def get_all_buildpacks(self, builders):
+        if not self.is_available():
+            raise ProviderError("Runc not supported in this instance")
+        out = {}
+        for b in builders:
+            p = _run(["skopeo", "inspect", "docker://" + b])
+            if p.returncode != 0:
+                continue
+            try:
+                labels = json.loads(p.stdout.decode()).get("Labels") or {}
+            except ValueError:
+                continue
+            if ORDER_LABEL in labels:
+                out[b] = get_builders_from_label(labels[ORDER_LABEL])
+        return out
+
+
+_providers = None
+
+
+def providers():
+    global _providers
+    with _lock:
+        if _providers is None:
+            _providers = [DockerAPIProvider(), ContainerRuntimeProvider(), PackProvider(), RuncProvider()]
+        return _providers
+
+
+def reset_providers():
+    global _providers
+    with _lock:
+        _providers = None
+
+
+def _log_not_supported():
+    global _warned_not_supported
+    if not _warned_not_supported:
+        log.warning("No CNB containerizer method accessible")
+        _warned_not_supported = True
+
+
+def _log_long_wait():
+    # the reference initialises its flag to true so the warning never fires
+    # (SURVEY 2.13 #14); "fixed" compat warns once.
+    global _warned_long_wait
+    if settings.fixed and not _warned_long_wait:
+        log.warning("This could take a few minutes to complete.")
+        _warned_long_wait = True
+
+
+def is_builder_supported(path, builder):
+    _log_long_wait()
+    for p in providers():
+        try:
+            return p.is_builder_supported(path, builder)
+        except (ProviderError, OSError, subprocess.SubprocessError, ValueError, KeyError) as e:
+            log.debug("CNB provider %s: %s", type(p).__name__, e)
+            continue
+    _log_not_supported()
+    return False
+
+
+def get_all_buildpacks(builders):
+    for p in providers():
+        try:
+            bps = p.get_all_buildpacks(builders)
+        except (ProviderError, OSError, subprocess.SubprocessError, ValueError, KeyError) as e:
+            log.debug("CNB provider %s: %s", type(p).__name__, e)
+            continue
+        if bps:
+            return bps
+    _log_not_supported()
+    return {}

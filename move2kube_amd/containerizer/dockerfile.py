@@ -1,0 +1,134 @@
+"""New-Dockerfile containerizer (reference ``internal/containerizer/dockerfilecontainerizer.go``).
+
+Detector protocol (the extension ABI): every directory containing an
+``m2kdfdetect.sh`` is a detector.  ``/bin/sh m2kdfdetect.sh <dir>`` is run
+with the detector directory as cwd; exit status 0 means "can containerize",
+stdout is a JSON object whose keys feed the detector's ``Dockerfile`` Go
+template.  All other files of the detector directory are copied next to the
+generated ``Dockerfile.<service>``.
+"""
+
+import json
+import os
+
+from .. import assets
+from ..models import ir as irtypes
+from ..models import plan as plantypes
+from ..parallel.detect_pool import run_detect, run_detect_jobs
+from ..utils import common, log
+from ..utils.fsindex import get_index
+from ..utils.gotemplate import TemplateError
+from .base import CONTAINERIZER_JSON_PORT, Containerizer, ContainerizerError
+
+DOCKERFILE_DETECT_SCRIPT = "m2kdfdetect.sh"
+
+
+def parse_detect_output(output):
+    """JSON object from a detect script; numbers decode as float64 like Go's encoding/json."""
+    return json.loads(output, parse_int=float)
+
+
+def _port_from(m):
+    v = m.get(CONTAINERIZER_JSON_PORT)
+    if isinstance(v, (int, float)) and not isinstance(v, bool):
+        return int(v)
+    return None
+
+
+class DockerfileContainerizer(Containerizer):
+    build_type = plantypes.NEW_DOCKERFILE
+    script = DOCKERFILE_DETECT_SCRIPT
+
+    def __init__(self):
+        self.detectors = []
+
+    def init(self, path):
+        try:
+            files = common.get_files_by_name(path, [self.script])
+        except (OSError, ValueError) as e:
+            log.warning("Unable to fetch files to recognize detect scripts : %s", e)
+            files = []
+        for f in files:
+            self.detectors.append(os.path.dirname(f))
+        log.debug("Detected %s containerization options : %s", self.build_type, self.detectors)
+
+    def get_target_options_batch(self, plan, paths):
+        jobs = [(d, self.script, p) for p in paths for d in self.detectors]
+        res = run_detect_jobs(jobs)
+        out = []
+        k = 0
+        for _ in paths:
+            opts = []
+            for d in self.detectors:
+                r = res[k]
+                k += 1
+                if r.ok:
+                    opts.append(d)
+            out.append(opts)
+        return out
+
+    def get_target_options(self, plan, path):
+        return self.get_target_options_batch(plan, [path])[0]
+
+    def get_container(self, plan, service):
+        if service.container_build_type != self.build_type or not service.target_options:
+            raise ContainerizerError("Unsupported service type for containerization or insufficient information in service")
+        container = irtypes.new_container(self.build_type, service.image, True)
+        container.repo_info = service.repo_info.copy()
+        cdir = service.target_options[0]
+        tpl_path = os.path.join(cdir, "Dockerfile")
+        try:
+            template = common.read_text(tpl_path)
+        except OSError as e:
+            log.error("Unable to read the Dockerfile template at path %r Error: %r", tpl_path, str(e))
+            raise
+        srcs = service.source_artifacts.get(plantypes.SOURCE_DIRECTORY_ARTIFACT) or []
+        if not srcs:
+            raise ContainerizerError("Service %s has no source code directory specified" % service.service_name)
+        src_dir = srcs[0]
+        r = run_detect(cdir, self.script, src_dir)
+        if not r.ok:
+            log.error("Detect using Dockerfile containerizer at path %r on the source code at path %r failed.", cdir, src_dir)
+            raise ContainerizerError("detect failed with exit status %d" % r.code)
+        contents = template
+        if r.stdout != "":
+            try:
+                m = parse_detect_output(r.stdout)
+            except ValueError as e:
+                log.error("Unable to unmarshal the output of the detect script at path %r Output: %r Error: %r",
+                          cdir, r.stdout, str(e))
+                raise
+            port = _port_from(m)
+            if port is not None:
+                container.add_exposed_port(port)
+            try:
+                contents = common.get_string_from_template(template, m)
+            except TemplateError as e:
+                log.warning("Template conversion failed : %s", e)
+                contents = ""
+        rel = common.go_rel(plan.root_dir, src_dir)
+        df_name = "Dockerfile." + service.service_name
+        df_path = common.go_join(rel, df_name)
+        container.add_file(df_path, contents)
+        try:
+            script = common.get_string_from_template(assets.template("dockerbuild.sh.tpl"), {
+                "Dockerfilename": df_name, "ImageName": service.image, "Context": "."})
+            container.add_file(common.go_join(rel, service.service_name + "-docker-build.sh"), script)
+            container.repo_info.target_path = df_path
+        except TemplateError as e:
+            log.error("Unable to translate Dockerfile build template to string Error: %r", str(e))
+        # copy every other file of the detector directory next to the Dockerfile
+        try:
+            files = get_index(cdir).files()
+        except OSError:
+            files = []
+        for f in files:
+            name = os.path.basename(f)
+            if name in ("Dockerfile", self.script):
+                continue
+            try:
+                container.add_file(common.go_join(rel, name), common.read_text(f))
+            except OSError as e:
+                log.error("Failed to read the file at path %r Error: %r", f, str(e))
+                raise
+        return container

@@ -1,0 +1,388 @@
+"""Go ``encoding/json`` marshalling rules for the Kubernetes/OpenShift/Knative/
+Tekton types the framework emits.
+
+The reference writes every object as ``json.Marshal(typedObject)`` -> YAML
+(``internal/transformer/transformer.go:162-204``).  Which empty fields appear
+is decided by the Go struct tags: non-pointer structs are always emitted
+(``resources: {}``, ``status: {}``, ``strategy: {}``), a zero ``metav1.Time``
+marshals as ``null`` (``creationTimestamp: null``), fields without
+``omitempty`` emit their zero value (``containerPort``, ``replicas`` of a
+DeploymentConfig, ``currentNumberScheduled`` of a DaemonSet ...), and unknown
+fields are dropped by the typed decode.  :func:`marshal` applies exactly those
+rules to JSON-shaped dicts using the struct tables below.
+
+Field DSL: ``"jsonName:type[,o]"`` where ``,o`` marks ``omitempty`` and type is
+one of ``string int bool map any Time Quantity IntOrString bytes ArrayOrString``,
+a struct name, ``*T`` (pointer), ``[]T`` (slice), ``map:T`` (map of T) or
+``inline:T`` (embedded struct).
+"""
+
+import base64
+
+_STRUCTS = {}
+
+
+def _def(name, spec):
+    fields = []
+    for item in spec.split():
+        o = item.endswith(",o")
+        if o:
+            item = item[:-2]
+        jname, typ = item.split(":", 1)
+        fields.append((jname, typ, o))
+    _STRUCTS[name] = fields
+
+
+# -- meta --------------------------------------------------------------------
+_def("TypeMeta", "kind:string,o apiVersion:string,o")
+_def("ObjectMeta", "name:string,o generateName:string,o namespace:string,o selfLink:string,o uid:string,o "
+     "resourceVersion:string,o generation:int,o creationTimestamp:Time deletionTimestamp:*Time,o "
+     "deletionGracePeriodSeconds:*int,o labels:map,o annotations:map,o ownerReferences:[]any,o "
+     "finalizers:[]string,o clusterName:string,o managedFields:[]any,o")
+_def("LabelSelector", "matchLabels:map,o matchExpressions:[]any,o")
+_def("ObjectReference", "kind:string,o namespace:string,o name:string,o uid:string,o apiVersion:string,o "
+     "resourceVersion:string,o fieldPath:string,o")
+_def("LocalObjectReference", "name:string,o")
+
+# -- core/v1 pod -------------------------------------------------------------
+_def("PodTemplateSpec", "metadata:ObjectMeta,o spec:PodSpec,o")
+_def("PodSpec", "volumes:[]Volume,o initContainers:[]Container,o containers:[]Container "
+     "ephemeralContainers:[]any,o restartPolicy:string,o terminationGracePeriodSeconds:*int,o "
+     "activeDeadlineSeconds:*int,o dnsPolicy:string,o nodeSelector:map,o serviceAccountName:string,o "
+     "serviceAccount:string,o automountServiceAccountToken:*bool,o nodeName:string,o hostNetwork:bool,o "
+     "hostPID:bool,o hostIPC:bool,o shareProcessNamespace:*bool,o securityContext:*PodSecurityContext,o "
+     "imagePullSecrets:[]LocalObjectReference,o hostname:string,o subdomain:string,o affinity:*any,o "
+     "schedulerName:string,o tolerations:[]any,o hostAliases:[]any,o priorityClassName:string,o "
+     "priority:*int,o dnsConfig:*any,o readinessGates:[]any,o runtimeClassName:*string,o "
+     "enableServiceLinks:*bool,o preemptionPolicy:*string,o overhead:map,o topologySpreadConstraints:[]any,o "
+     "setHostnameAsFQDN:*bool,o")
+_def("Container", "name:string image:string,o command:[]string,o args:[]string,o workingDir:string,o "
+     "ports:[]ContainerPort,o envFrom:[]any,o env:[]EnvVar,o resources:ResourceRequirements,o "
+     "volumeMounts:[]VolumeMount,o volumeDevices:[]any,o livenessProbe:*Probe,o readinessProbe:*Probe,o "
+     "startupProbe:*Probe,o lifecycle:*any,o terminationMessagePath:string,o terminationMessagePolicy:string,o "
+     "imagePullPolicy:string,o securityContext:*SecurityContext,o stdin:bool,o stdinOnce:bool,o tty:bool,o")
+_def("ContainerPort", "name:string,o hostPort:int,o containerPort:int protocol:string,o hostIP:string,o")
+_def("EnvVar", "name:string value:string,o valueFrom:*any,o")
+_def("ResourceRequirements", "limits:map:Quantity,o requests:map:Quantity,o")
+_def("VolumeMount", "name:string readOnly:bool,o mountPath:string subPath:string,o mountPropagation:*string,o "
+     "subPathExpr:string,o")
+_def("Volume", "name:string inline:VolumeSource")
+_def("VolumeSource", "hostPath:*HostPathVolumeSource,o emptyDir:*EmptyDirVolumeSource,o gcePersistentDisk:*any,o "
+     "awsElasticBlockStore:*any,o gitRepo:*any,o secret:*SecretVolumeSource,o nfs:*any,o iscsi:*any,o "
+     "glusterfs:*any,o persistentVolumeClaim:*PersistentVolumeClaimVolumeSource,o rbd:*any,o flexVolume:*any,o "
+     "cinder:*any,o cephfs:*any,o flocker:*any,o downwardAPI:*any,o fc:*any,o azureFile:*any,o "
+     "configMap:*ConfigMapVolumeSource,o vsphereVolume:*any,o quobyte:*any,o azureDisk:*any,o "
+     "photonPersistentDisk:*any,o projected:*any,o portworxVolume:*any,o scaleIO:*any,o storageos:*any,o "
+     "csi:*any,o ephemeral:*any,o")
+_def("HostPathVolumeSource", "path:string type:*string,o")
+_def("EmptyDirVolumeSource", "medium:string,o sizeLimit:*Quantity,o")
+_def("PersistentVolumeClaimVolumeSource", "claimName:string readOnly:bool,o")
+_def("SecretVolumeSource", "secretName:string,o items:[]KeyToPath,o defaultMode:*int,o optional:*bool,o")
+_def("ConfigMapVolumeSource", "name:string,o items:[]KeyToPath,o defaultMode:*int,o optional:*bool,o")
+_def("KeyToPath", "key:string path:string mode:*int,o")
+_def("SecurityContext", "capabilities:*Capabilities,o privileged:*bool,o seLinuxOptions:*any,o "
+     "windowsOptions:*any,o runAsUser:*int,o runAsGroup:*int,o runAsNonRoot:*bool,o "
+     "readOnlyRootFilesystem:*bool,o allowPrivilegeEscalation:*bool,o procMount:*string,o seccompProfile:*any,o")
+_def("Capabilities", "add:[]string,o drop:[]string,o")
+_def("PodSecurityContext", "seLinuxOptions:*any,o windowsOptions:*any,o runAsUser:*int,o runAsGroup:*int,o "
+     "runAsNonRoot:*bool,o supplementalGroups:[]int,o fsGroup:*int,o sysctls:[]any,o "
+     "fsGroupChangePolicy:*string,o seccompProfile:*any,o")
+_def("Probe", "exec:*ExecAction,o httpGet:*any,o tcpSocket:*any,o initialDelaySeconds:int,o timeoutSeconds:int,o "
+     "periodSeconds:int,o successThreshold:int,o failureThreshold:int,o")
+_def("ExecAction", "command:[]string,o")
+_def("PodStatus", "phase:string,o conditions:[]any,o message:string,o reason:string,o nominatedNodeName:string,o "
+     "hostIP:string,o podIP:string,o podIPs:[]any,o startTime:*Time,o initContainerStatuses:[]any,o "
+     "containerStatuses:[]any,o qosClass:string,o ephemeralContainerStatuses:[]any,o")
+
+# -- workloads ------------------------------------------------------------------
+_META = "inline:TypeMeta metadata:ObjectMeta,o "
+_def("Pod", _META + "spec:PodSpec,o status:PodStatus,o")
+_def("Deployment", _META + "spec:DeploymentSpec,o status:DeploymentStatus,o")
+_def("DeploymentSpec", "replicas:*int,o selector:*LabelSelector template:PodTemplateSpec strategy:DeploymentStrategy,o "
+     "minReadySeconds:int,o revisionHistoryLimit:*int,o paused:bool,o rollbackTo:*any,o progressDeadlineSeconds:*int,o")
+_def("DeploymentStrategy", "type:string,o rollingUpdate:*any,o")
+_def("DeploymentStatus", "observedGeneration:int,o replicas:int,o updatedReplicas:int,o readyReplicas:int,o "
+     "availableReplicas:int,o unavailableReplicas:int,o conditions:[]any,o collisionCount:*int,o")
+_def("DaemonSet", _META + "spec:DaemonSetSpec,o status:DaemonSetStatus,o")
+_def("DaemonSetSpec", "selector:*LabelSelector template:PodTemplateSpec updateStrategy:DaemonSetUpdateStrategy,o "
+     "minReadySeconds:int,o templateGeneration:int,o revisionHistoryLimit:*int,o")
+_def("DaemonSetUpdateStrategy", "type:string,o rollingUpdate:*any,o")
+_def("DaemonSetStatus", "currentNumberScheduled:int numberMisscheduled:int desiredNumberScheduled:int numberReady:int "
+     "observedGeneration:int,o updatedNumberScheduled:int,o numberAvailable:int,o numberUnavailable:int,o "
+     "collisionCount:*int,o conditions:[]any,o")
+_def("StatefulSet", _META + "spec:any,o status:any,o")
+_def("ReplicaSet", _META + "spec:any,o status:any,o")
+_def("Job", _META + "spec:JobSpec,o status:JobStatus,o")
+_def("JobSpec", "parallelism:*int,o completions:*int,o activeDeadlineSeconds:*int,o backoffLimit:*int,o "
+     "selector:*LabelSelector,o manualSelector:*bool,o template:PodTemplateSpec ttlSecondsAfterFinished:*int,o")
+_def("JobStatus", "conditions:[]any,o startTime:*Time,o completionTime:*Time,o active:int,o succeeded:int,o failed:int,o")
+_def("ReplicationController", _META + "spec:ReplicationControllerSpec,o status:ReplicationControllerStatus,o")
+_def("ReplicationControllerSpec", "replicas:*int,o minReadySeconds:int,o selector:map,o template:*PodTemplateSpec,o")
+_def("ReplicationControllerStatus", "replicas:int fullyLabeledReplicas:int,o readyReplicas:int,o availableReplicas:int,o "
+     "observedGeneration:int,o conditions:[]any,o")
+_def("DeploymentConfig", _META + "spec:DeploymentConfigSpec status:DeploymentConfigStatus")
+_def("DeploymentConfigSpec", "strategy:OpenShiftDeploymentStrategy minReadySeconds:int,o triggers:[]DeploymentTriggerPolicy "
+     "replicas:int revisionHistoryLimit:*int,o test:bool paused:bool,o selector:map,o template:*PodTemplateSpec,o")
+_def("OpenShiftDeploymentStrategy", "type:string,o customParams:*any,o recreateParams:*any,o rollingParams:*any,o "
+     "resources:ResourceRequirements,o labels:map,o annotations:map,o activeDeadlineSeconds:*int,o")
+_def("DeploymentTriggerPolicy", "type:string,o imageChangeParams:*DeploymentTriggerImageChangeParams,o")
+_def("DeploymentTriggerImageChangeParams", "automatic:bool,o containerNames:[]string,o from:ObjectReference "
+     "lastTriggeredImage:string,o")
+_def("DeploymentConfigStatus", "latestVersion:int observedGeneration:int replicas:int updatedReplicas:int "
+     "availableReplicas:int unavailableReplicas:int details:*any,o conditions:[]any,o readyReplicas:int,o")
+
+# -- networking ---------------------------------------------------------------
+_def("Service", _META + "spec:ServiceSpec,o status:ServiceStatus,o")
+_def("ServiceSpec", "ports:[]ServicePort,o selector:map,o clusterIP:string,o type:string,o externalIPs:[]string,o "
+     "sessionAffinity:string,o loadBalancerIP:string,o loadBalancerSourceRanges:[]string,o externalName:string,o "
+     "externalTrafficPolicy:string,o healthCheckNodePort:int,o publishNotReadyAddresses:bool,o "
+     "sessionAffinityConfig:*any,o ipFamily:*string,o topologyKeys:[]string,o")
+_def("ServicePort", "name:string,o protocol:string,o appProtocol:*string,o port:int targetPort:IntOrString,o nodePort:int,o")
+_def("ServiceStatus", "loadBalancer:LoadBalancerStatus,o")
+_def("LoadBalancerStatus", "ingress:[]any,o")
+_def("Ingress", _META + "spec:IngressSpec,o status:IngressStatus,o")
+_def("IngressSpec", "ingressClassName:*string,o defaultBackend:*IngressBackend,o tls:[]IngressTLS,o rules:[]IngressRule,o")
+_def("IngressBackend", "service:*IngressServiceBackend,o resource:*any,o")
+_def("IngressServiceBackend", "name:string port:ServiceBackendPort,o")
+_def("ServiceBackendPort", "name:string,o number:int,o")
+_def("IngressRule", "host:string,o http:*HTTPIngressRuleValue,o")
+_def("HTTPIngressRuleValue", "paths:[]HTTPIngressPath")
+_def("HTTPIngressPath", "path:string,o pathType:*string,o backend:IngressBackend")
+_def("IngressTLS", "hosts:[]string,o secretName:string,o")
+_def("IngressStatus", "loadBalancer:LoadBalancerStatus,o")
+_def("IngressV1beta1", _META + "spec:IngressSpecV1beta1,o status:IngressStatus,o")
+_def("IngressSpecV1beta1", "ingressClassName:*string,o backend:*IngressBackendV1beta1,o tls:[]IngressTLS,o "
+     "rules:[]IngressRuleV1beta1,o")
+_def("IngressBackendV1beta1", "serviceName:string,o servicePort:IntOrString,o resource:*any,o")
+_def("IngressRuleV1beta1", "host:string,o http:*HTTPIngressRuleValueV1beta1,o")
+_def("HTTPIngressRuleValueV1beta1", "paths:[]HTTPIngressPathV1beta1")
+_def("HTTPIngressPathV1beta1", "path:string,o pathType:*string,o backend:IngressBackendV1beta1")
+_def("Route", _META + "spec:RouteSpec status:RouteStatus,o")
+_def("RouteSpec", "host:string,o subdomain:string,o path:string,o to:RouteTargetReference alternateBackends:[]any,o "
+     "port:*RoutePort,o tls:*any,o wildcardPolicy:string,o")
+_def("RouteTargetReference", "kind:string name:string weight:*int")
+_def("RoutePort", "targetPort:IntOrString")
+_def("RouteStatus", "ingress:[]RouteIngress")
+_def("RouteIngress", "host:string,o routerName:string,o conditions:[]any,o wildcardPolicy:string,o "
+     "routerCanonicalHostname:string,o")
+_def("NetworkPolicy", _META + "spec:NetworkPolicySpec,o")
+_def("NetworkPolicySpec", "podSelector:LabelSelector ingress:[]NetworkPolicyIngressRule,o egress:[]any,o "
+     "policyTypes:[]string,o")
+_def("NetworkPolicyIngressRule", "ports:[]any,o from:[]NetworkPolicyPeer,o")
+_def("NetworkPolicyPeer", "podSelector:*LabelSelector,o namespaceSelector:*LabelSelector,o ipBlock:*any,o")
+
+# -- storage / config ------------------------------------------------------------
+_def("ConfigMap", _META + "immutable:*bool,o data:map,o binaryData:map:bytes,o")
+_def("Secret", _META + "immutable:*bool,o data:map:bytes,o stringData:map,o type:string,o")
+_def("PersistentVolumeClaim", _META + "spec:PersistentVolumeClaimSpec,o status:PersistentVolumeClaimStatus,o")
+_def("PersistentVolumeClaimSpec", "accessModes:[]string,o selector:*LabelSelector,o resources:ResourceRequirements,o "
+     "volumeName:string,o storageClassName:*string,o volumeMode:*string,o dataSource:*any,o")
+_def("PersistentVolumeClaimStatus", "phase:string,o accessModes:[]string,o capacity:map:Quantity,o conditions:[]any,o")
+_def("ImageStream", _META + "spec:ImageStreamSpec status:ImageStreamStatus,o")
+_def("ImageStreamSpec", "lookupPolicy:ImageLookupPolicy,o dockerImageRepository:string,o tags:[]TagReference,o")
+_def("ImageLookupPolicy", "local:bool")
+_def("TagReference", "name:string annotations:map from:*ObjectReference,o reference:bool,o generation:*int "
+     "importPolicy:TagImportPolicy,o referencePolicy:TagReferencePolicy,o")
+_def("TagImportPolicy", "insecure:bool,o scheduled:bool,o")
+_def("TagReferencePolicy", "type:string")
+_def("ImageStreamStatus", "dockerImageRepository:string publicDockerImageRepository:string,o tags:[]any,o")
+
+# -- rbac ----------------------------------------------------------------------------
+_def("Role", _META + "rules:[]PolicyRule")
+_def("PolicyRule", "verbs:[]string apiGroups:[]string,o resources:[]string,o resourceNames:[]string,o "
+     "nonResourceURLs:[]string,o")
+_def("RoleBinding", _META + "subjects:[]Subject,o roleRef:RoleRef")
+_def("Subject", "kind:string apiGroup:string,o name:string namespace:string,o")
+_def("RoleRef", "apiGroup:string kind:string name:string")
+_def("ServiceAccount", _META + "secrets:[]ObjectReference,o imagePullSecrets:[]LocalObjectReference,o "
+     "automountServiceAccountToken:*bool,o")
+
+# -- knative -------------------------------------------------------------------------
+_def("KnativeService", _META + "spec:KnativeServiceSpec,o status:KnativeServiceStatus,o")
+_def("KnativeServiceSpec", "template:RevisionTemplateSpec,o traffic:[]any,o")
+_def("RevisionTemplateSpec", "metadata:ObjectMeta,o spec:RevisionSpec,o")
+_def("RevisionSpec", "inline:PodSpec containerConcurrency:*int,o timeoutSeconds:*int,o")
+_def("KnativeServiceStatus", "observedGeneration:int,o conditions:[]any,o annotations:map,o "
+     "latestReadyRevisionName:string,o latestCreatedRevisionName:string,o url:*any,o address:*any,o traffic:[]any,o")
+
+# -- tekton ---------------------------------------------------------------------------
+_def("Pipeline", _META + "spec:PipelineSpec")
+_def("PipelineSpec", "description:string,o resources:[]any,o tasks:[]PipelineTask,o params:[]ParamSpec,o "
+     "workspaces:[]PipelineWorkspaceDeclaration,o results:[]any,o finally:[]any,o")
+_def("PipelineTask", "name:string,o taskRef:*TaskRef,o taskSpec:*any,o conditions:[]any,o when:[]any,o retries:int,o "
+     "runAfter:[]string,o resources:*any,o params:[]Param,o workspaces:[]WorkspacePipelineTaskBinding,o timeout:*any,o")
+_def("TaskRef", "name:string,o kind:string,o apiVersion:string,o bundle:string,o")
+_def("Param", "name:string value:ArrayOrString")
+_def("ParamSpec", "name:string type:string,o description:string,o default:*any,o")
+_def("PipelineWorkspaceDeclaration", "name:string description:string,o optional:bool,o")
+_def("WorkspacePipelineTaskBinding", "name:string workspace:string subPath:string,o")
+_def("PipelineRun", _META + "spec:PipelineRunSpec,o status:PipelineRunStatus,o")
+_def("PipelineRunSpec", "pipelineRef:*PipelineRef,o pipelineSpec:*any,o resources:[]any,o params:[]Param,o "
+     "serviceAccountName:string,o serviceAccountNames:[]any,o status:string,o timeout:*any,o podTemplate:*any,o "
+     "workspaces:[]WorkspaceBinding,o taskRunSpecs:[]any,o")
+_def("PipelineRef", "name:string,o apiVersion:string,o bundle:string,o")
+_def("WorkspaceBinding", "name:string subPath:string,o volumeClaimTemplate:*PersistentVolumeClaim,o "
+     "persistentVolumeClaim:*any,o emptyDir:*any,o configMap:*any,o secret:*any,o")
+_def("PipelineRunStatus", "observedGeneration:int,o conditions:[]any,o annotations:map,o podName:string,o "
+     "startTime:*Time,o completionTime:*Time,o taskRuns:map,o runs:map,o pipelineResults:[]any,o "
+     "pipelineSpec:*any,o skippedTasks:[]any,o")
+_def("EventListener", _META + "spec:EventListenerSpec status:EventListenerStatus,o")
+_def("EventListenerSpec", "serviceAccountName:string triggers:[]EventListenerTrigger serviceType:string,o "
+     "replicas:*int,o podTemplate:ELPodTemplate,o namespaceSelector:ELNamespaceSelector,o resources:ELResources,o")
+_def("ELPodTemplate", "tolerations:[]any,o nodeSelector:map,o")
+_def("ELNamespaceSelector", "matchNames:[]string,o")
+_def("ELResources", "kubernetesResource:*any,o")
+_def("EventListenerTrigger", "bindings:[]EventListenerBinding template:*EventListenerTemplate,o triggerRef:string,o "
+     "name:string,o interceptors:[]any,o serviceAccount:*any,o")
+_def("EventListenerBinding", "name:string,o kind:string,o ref:string,o spec:*any,o apiversion:string,o")
+_def("EventListenerTemplate", "name:string,o ref:*string,o apiversion:string,o")
+_def("EventListenerStatus", "observedGeneration:int,o conditions:[]any,o annotations:map,o address:*any,o "
+     "configuration:EventListenerConfig")
+_def("EventListenerConfig", "generatedName:string")
+_def("TriggerBinding", _META + "spec:TriggerBindingSpec status:EmptyStatus")
+_def("TriggerBindingSpec", "params:[]any,o")
+_def("EmptyStatus", "")
+_def("TriggerTemplate", _META + "spec:TriggerTemplateSpec status:EmptyStatus")
+_def("TriggerTemplateSpec", "params:[]ParamSpec,o resourcetemplates:[]RawExtension,o")
+
+
+# (group/version, kind) -> struct type; "*" group wildcard per kind
+KIND_TYPES = {
+    "Pod": "Pod", "Deployment": "Deployment", "DaemonSet": "DaemonSet", "Job": "Job",
+    "ReplicationController": "ReplicationController", "DeploymentConfig": "DeploymentConfig",
+    "Service": "Service", "Ingress": "Ingress", "Route": "Route", "NetworkPolicy": "NetworkPolicy",
+    "ConfigMap": "ConfigMap", "Secret": "Secret", "PersistentVolumeClaim": "PersistentVolumeClaim",
+    "ImageStream": "ImageStream", "Role": "Role", "RoleBinding": "RoleBinding", "ServiceAccount": "ServiceAccount",
+    "Pipeline": "Pipeline", "PipelineRun": "PipelineRun", "EventListener": "EventListener",
+    "TriggerBinding": "TriggerBinding", "TriggerTemplate": "TriggerTemplate",
+    "StatefulSet": "StatefulSet", "ReplicaSet": "ReplicaSet",
+}
+
+
+def type_for(obj):
+    """Struct type used to marshal ``obj`` (None = pass-through)."""
+    kind = obj.get("kind", "")
+    gv = obj.get("apiVersion", "")
+    if kind == "Service" and gv.startswith("serving.knative.dev/"):
+        return "KnativeService"
+    if kind == "Ingress" and gv in ("networking.k8s.io/v1beta1", "extensions/v1beta1"):
+        return "IngressV1beta1"
+    return KIND_TYPES.get(kind)
+
+
+def _is_empty(v, typ):
+    if v is None:
+        return True
+    if typ.startswith("*"):
+        return False
+    if typ in ("string",):
+        return v == ""
+    if typ == "int":
+        return v == 0
+    if typ == "bool":
+        return v is False
+    if typ.startswith("[]") or typ.startswith("map") or typ == "bytes":
+        return len(v) == 0
+    if typ == "any":
+        return isinstance(v, (dict, list, str)) and len(v) == 0 or v is False or v == 0
+    return False
+
+
+def _zero(typ):
+    if typ == "string":
+        return ""
+    if typ == "int":
+        return 0
+    if typ == "bool":
+        return False
+    if typ == "Time":
+        return None
+    if typ == "IntOrString":
+        return 0
+    if typ in ("ArrayOrString",):
+        return ""
+    if typ in _STRUCTS:
+        return _marshal_struct({}, typ)
+    return None
+
+
+def _marshal_value(v, typ):
+    if typ.startswith("*"):
+        return None if v is None else _marshal_value(v, typ[1:])
+    if typ.startswith("[]"):
+        if v is None:
+            return None
+        return [_marshal_value(x, typ[2:]) for x in v]
+    if typ == "map":
+        return None if v is None else dict(v)
+    if typ.startswith("map:"):
+        if v is None:
+            return None
+        return {k: _marshal_value(x, typ[4:]) for k, x in v.items()}
+    if typ == "bytes":
+        if v is None:
+            return None
+        if isinstance(v, str):
+            return v
+        return base64.b64encode(bytes(v)).decode()
+    if typ == "Time":
+        return v if v else None
+    if typ in ("string", "Quantity", "ArrayOrString"):
+        return v if isinstance(v, str) else ("" if v is None else v)
+    if typ == "int":
+        return v
+    if typ == "bool":
+        return bool(v)
+    if typ == "IntOrString":
+        return v
+    if typ == "any":
+        return v
+    if typ == "RawExtension":
+        return marshal(v) if isinstance(v, dict) else v
+    if typ in _STRUCTS:
+        return _marshal_struct(v or {}, typ)
+    return v
+
+
+def _marshal_struct(d, typ):
+    out = {}
+    for jname, ftype, omit in _STRUCTS[typ]:
+        if jname == "inline":
+            out.update(_marshal_struct(d, ftype))
+            continue
+        present = jname in d
+        v = d.get(jname)
+        if not present or v is None:
+            if ftype in _STRUCTS:
+                out[jname] = _marshal_struct({}, ftype)
+            elif ftype == "Time":
+                out[jname] = None
+            elif omit:
+                continue
+            elif ftype.startswith("*") or ftype.startswith("[]") or ftype.startswith("map") or ftype in ("any", "bytes"):
+                out[jname] = None
+            else:
+                out[jname] = _zero(ftype)
+            continue
+        if omit and _is_empty(v, ftype):
+            continue
+        out[jname] = _marshal_value(v, ftype)
+    return out
+
+
+def marshal(obj):
+    """Go json.Marshal of a typed Kubernetes object given as a JSON-shaped dict."""
+    typ = type_for(obj)
+    if typ is None:
+        out = dict(obj)
+        md = out.get("metadata")
+        if isinstance(md, dict):
+            out["metadata"] = _marshal_struct(md, "ObjectMeta")
+        elif "metadata" not in out:
+            out["metadata"] = _marshal_struct({}, "ObjectMeta")
+        return out
+    return _marshal_struct(obj, typ)
+
+
+def marshal_as(d, typ):
+    return _marshal_struct(d, typ)

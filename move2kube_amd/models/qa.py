@@ -1,0 +1,350 @@
+"""QA problems and the QA cache (``kind: QACache``).
+
+Reference: ``types/qaengine/problem.go:33-291`` and ``types/qaengine/cache.go:29-138``.
+Problem validation rules (auto-resolution of single-option selects and
+empty multi-selects, default checks), answer validation and cache matching
+(case-insensitive description equality *or* regex match) follow the reference
+so that caches written by either tool replay in the other.
+"""
+
+import re
+import threading
+
+from ..utils import common, log, yamlio
+from ..utils.constants import SCHEME_GROUP_VERSION
+from .base import as_bool, as_list, as_map, as_str, as_str_list
+
+SELECT = "Select"
+MULTISELECT = "MultiSelect"
+INPUT = "Input"
+MULTILINE = "MultiLine"
+PASSWORD = "Password"
+CONFIRM = "Confirm"
+
+QACACHE_KIND = "QACache"
+
+_id_lock = threading.Lock()
+_last_id = 0
+
+
+def _next_id():
+    global _last_id
+    with _id_lock:
+        _last_id += 1
+        return _last_id
+
+
+class ProblemError(ValueError):
+    pass
+
+
+def _parse_bool(s):
+    return common.cast_to_bool(s)
+
+
+class Problem:
+    __slots__ = ("id", "desc", "context", "type", "default", "options", "answer", "resolved")
+
+    def __init__(self, id=0, desc="", context=None, type="", default=None, options=None,
+                 answer=None, resolved=False):
+        self.id = id
+        self.desc = desc
+        self.context = context if context is not None else []
+        self.type = type
+        self.default = default if default is not None else []
+        self.options = options if options is not None else []
+        self.answer = answer
+        self.resolved = resolved
+
+    def copy(self):
+        return Problem(self.id, self.desc, list(self.context), self.type, list(self.default),
+                       list(self.options), None if self.answer is None else list(self.answer), self.resolved)
+
+    # -- answers -------------------------------------------------------------
+    def set_answer(self, answer):
+        answer = list(answer or [])
+        if self.type != MULTISELECT and len(answer) == 0:
+            raise ProblemError("The answer slice is empty")
+        if self.type != MULTISELECT and len(answer) > 1:
+            raise ProblemError("The question type is not multiselect, but there are multiple answers")
+        if self.type in (SELECT, MULTISELECT):
+            ok = True
+            self.answer = []
+            for a in answer:
+                if not common.is_string_present(self.options, a):
+                    log.warning("No matching value in options for %s. Ignoring.", a)
+                    ok = False
+                    continue
+                self.answer.append(a)
+            if not ok:
+                raise ProblemError("Unknown options selected")
+            self.resolved = True
+            return
+        if self.type == CONFIRM:
+            try:
+                _parse_bool(answer[0])
+            except ValueError as e:
+                log.warning("Error while parsing answer for confirm question type : %s", e)
+                raise ProblemError(str(e))
+        self.answer = [answer[0]]
+        self.resolved = True
+
+    def get_slice_answer(self):
+        if not self.resolved:
+            raise ProblemError("Problem yet to be resolved")
+        if self.type != MULTISELECT:
+            raise ProblemError("This question type does not support this answer type")
+        return list(self.answer or [])
+
+    def get_bool_answer(self):
+        if not self.resolved:
+            raise ProblemError("Problem yet to be resolved")
+        if self.type != CONFIRM:
+            raise ProblemError("This question type does not support this answer type")
+        if not self.answer or len(self.answer) != 1:
+            raise ProblemError("No answer available")
+        return _parse_bool(self.answer[0])
+
+    def get_string_answer(self):
+        if not self.resolved:
+            raise ProblemError("Problem yet to be resolved")
+        if self.type in (MULTISELECT, CONFIRM):
+            raise ProblemError("This question type does not support this answer type")
+        if not self.answer or len(self.answer) != 1:
+            raise ProblemError("Wrong number of answers")
+        return self.answer[0]
+
+    def matches(self, other):
+        return _match_string(self.desc, other.desc) and self.type == other.type
+
+    # -- encoding ------------------------------------------------------------
+    def to_yaml(self):
+        d = {"description": self.desc}
+        if self.context:
+            d["context"] = list(self.context)
+        sol = {"type": self.type}
+        if self.default:
+            sol["default"] = list(self.default)
+        if self.options:
+            sol["options"] = list(self.options)
+        sol["answer"] = list(self.answer) if self.answer is not None else None
+        if sol["answer"] is None:
+            sol["answer"] = []
+        d["solution"] = sol
+        if self.resolved:
+            d["resolved"] = True
+        return d
+
+    def to_json(self):
+        d = {"id": self.id, "description": self.desc}
+        if self.context:
+            d["context"] = list(self.context)
+        sol = {"type": self.type}
+        if self.default:
+            sol["default"] = list(self.default)
+        if self.options:
+            sol["options"] = list(self.options)
+        sol["answer"] = list(self.answer) if self.answer is not None else None
+        d["solution"] = sol
+        if self.resolved:
+            d["resolved"] = True
+        return d
+
+    @classmethod
+    def from_yaml(cls, d):
+        d = as_map(d)
+        sol = as_map(d.get("solution"))
+        ans = sol.get("answer")
+        return cls(0, as_str(d.get("description")), as_str_list(d.get("context")), as_str(sol.get("type")),
+                   as_str_list(sol.get("default")), as_str_list(sol.get("options")),
+                   as_str_list(ans) if ans is not None else None, as_bool(d.get("resolved")))
+
+    def __repr__(self):
+        return "Problem(%r)" % (self.to_json(),)
+
+
+def _match_string(s1, s2):
+    if s1.casefold() == s2.casefold():
+        return True
+    try:
+        return re.search(_go_regex(s1), s2) is not None
+    except re.error as e:
+        log.debug("Unable to compile string %s : %s", s1, e)
+        return False
+
+
+def _go_regex(p):
+    """Translate the few RE2-only constructs to Python syntax."""
+    return p.replace("(?P<", "(?P<").replace("\\z", "\\Z")
+
+
+def _new_problem(t, desc, context, default, opts):
+    resolved = False
+    answer = []
+    if desc == "":
+        raise ProblemError("Empty Description")
+    default = [d for d in (default or [])]
+    opts = list(opts or [])
+    if t == MULTISELECT:
+        if len(opts) == 0:
+            resolved = True
+        for d in default:
+            if not common.is_string_present(opts, d):
+                raise ProblemError("Default value [%s] not present in options [%s]" % (d, opts))
+    elif t == SELECT:
+        if len(opts) == 0:
+            raise ProblemError("Atleast one option is required for question %s" % desc)
+        if len(opts) == 1:
+            answer = list(opts)
+            resolved = True
+        if len(default) > 1:
+            log.warning("Only one default is allowed for question %s. Setting default as first value %s", desc, default)
+            default = [default[0]]
+        if len(default) == 0:
+            default = [opts[0]]
+        elif not common.is_string_present(opts, default[0]):
+            raise ProblemError("Default value [%s] not present in options [%s]" % (default[0], opts))
+    elif t == CONFIRM:
+        if opts:
+            log.warning("Options is not required for confirm question type : %s", desc)
+        if len(default) > 1:
+            log.warning("Only one default is allowed for question %s.", desc)
+        if len(default) == 0:
+            default = ["false"]
+        else:
+            try:
+                _parse_bool(default[0])
+                default = [default[0]]
+            except ValueError:
+                log.warning("Unable to parse default value %s. Setting as false", default[0])
+                default = ["false"]
+    elif t in (INPUT, MULTILINE):
+        if len(default) > 1:
+            log.warning("Only one default value supported for %s. Ignoring others.", desc)
+            default = [default[0]]
+        if opts:
+            log.warning("Options not supported for %s. Ignoring options.", desc)
+            opts = []
+    elif t == PASSWORD:
+        if default:
+            log.warning("Default not supported for %s. Ignoring default.", desc)
+            default = []
+        if opts:
+            log.warning("Options not supported for %s. Ignoring options.", desc)
+            opts = []
+    return Problem(_next_id(), desc, list(context or []), t, default, opts, answer, resolved)
+
+
+def new_select_problem(desc, context, default, opts):
+    return _new_problem(SELECT, desc, context, [default], opts)
+
+
+def new_multiselect_problem(desc, context, default, opts):
+    return _new_problem(MULTISELECT, desc, context, default, opts)
+
+
+def new_confirm_problem(desc, context, default):
+    return _new_problem(CONFIRM, desc, context, ["true" if default else "false"], [])
+
+
+def new_input_problem(desc, context, default):
+    return _new_problem(INPUT, desc, context, [default], [])
+
+
+def new_multiline_input_problem(desc, context, default):
+    return _new_problem(MULTILINE, desc, context, [default], [])
+
+
+def new_password_problem(desc, context):
+    return _new_problem(PASSWORD, desc, context, [], [])
+
+
+class Cache:
+    """``kind: QACache`` file (cache.go)."""
+
+    def __init__(self, file=""):
+        self.api_version = SCHEME_GROUP_VERSION
+        self.kind = QACACHE_KIND
+        self.name = ""
+        self.file = file
+        self.problems = []
+        self._lock = threading.Lock()
+
+    def to_yaml(self):
+        d = {}
+        if self.api_version:
+            d["apiVersion"] = self.api_version
+        d["kind"] = self.kind
+        if self.name:
+            d["metadata"] = {"name": self.name}
+        if self.problems:
+            d["spec"] = {"solutions": [p.to_yaml() for p in self.problems]}
+        return d
+
+    @classmethod
+    def from_yaml(cls, d, file=""):
+        d = as_map(d)
+        c = cls(file)
+        c.api_version = as_str(d.get("apiVersion"))
+        c.kind = as_str(d.get("kind"))
+        c.name = as_str(as_map(d.get("metadata")).get("name"))
+        c.problems = [Problem.from_yaml(x) for x in as_list(as_map(d.get("spec")).get("solutions"))]
+        return c
+
+    def load(self):
+        """Load and merge the cache file (cache.go:45-60)."""
+        data = common.read_move2kube_yaml(self.file)
+        other = Cache.from_yaml(data, self.file)
+        self._merge(other)
+        for p in self.problems:
+            p.resolved = True
+
+    def write(self):
+        try:
+            common.write_text(self.file, yamlio.dump(self.to_yaml()))
+        except OSError as e:
+            log.warning("Unable to write cache : %s", e)
+            raise
+
+    def add_problem_solution(self, p):
+        if p.type == PASSWORD:
+            log.debug("Passwords are not added to the cache.")
+            return False
+        if not p.resolved:
+            log.warning("Unresolved problem. Not going to be added to cache.")
+            return False
+        with self._lock:
+            for i, cp in enumerate(self.problems):
+                if cp.matches(p):
+                    log.warning("A solution already exists in cache for [%s], rewriting", p.desc)
+                    self.problems[i] = p.copy()
+                    break
+            else:
+                self.problems.append(p.copy())
+            try:
+                self.write()
+            except OSError as e:
+                log.error("Unable to persist cache : %s", e)
+        return True
+
+    def get_solution(self, p):
+        if p.resolved:
+            log.warning("Problem already solved.")
+            return p
+        for cp in self.problems:
+            if cp.matches(p) and cp.resolved:
+                p.set_answer(cp.answer)
+                return p
+        raise ProblemError("The problem %r was not found in the cache" % (p.desc,))
+
+    def _merge(self, other):
+        # the reference's inner ``continue`` does not skip duplicates;
+        # "fixed" compat drops later duplicates as the log message intends.
+        from ..utils.constants import settings
+        for p in other.problems:
+            dup = any(op.matches(p) for op in self.problems)
+            if dup:
+                log.warning("There are two answers for %s in cache. Ignoring latter ones.", p.desc)
+                if settings.fixed:
+                    continue
+            self.problems.append(p)

@@ -1,0 +1,221 @@
+"""Top-level operations behind the CLI verbs (reference ``internal/move2kube/``):
+``collect``, ``create_plan``, ``curate_plan``, ``translate``, ``get_version``."""
+
+import os
+import shutil
+
+from . import collector, customizer, metadata, optimizer, parameterizer, qaengine, transformer
+from .models import info, qa
+from .models import plan as plantypes
+from .source import translator as source_translator
+from .utils import common, fsindex, log, yamlio
+from .utils.constants import DEFAULT_CLUSTER_TYPE
+
+
+def collect(input_path, output_path, annotations=()):
+    """``Collect`` (collector.go): run the annotation-selected collectors."""
+    collector.collect(input_path, output_path, list(annotations))
+
+
+def create_plan(input_path, project_name):
+    """``CreatePlan`` (planner.go:30-64): every source translator proposes
+    service options, then metadata loaders annotate the plan.  All planners
+    share one cached directory index of ``input_path``."""
+    p = plantypes.new_plan()
+    p.name = project_name
+    p.root_dir = input_path
+    with fsindex.scope():
+        log.info("Planning Translation")
+        for t in source_translator.get_source_loaders():
+            log.info("[%r] Planning translation", t)
+            try:
+                services = t.get_service_options(input_path, p)
+            except Exception as e:  # noqa: BLE001
+                if isinstance(e, log.FatalError):
+                    raise
+                log.warning("[%r] Failed : %s", t, e)
+                continue
+            p.add_services_to_plan(services)
+            log.info("[%r] Done", t)
+        log.info("Translation planning done")
+        log.info("Planning Metadata")
+        for loader in metadata.get_loaders():
+            log.info("[%r] Planning metadata", loader)
+            try:
+                loader.update_plan(input_path, p)
+            except Exception as e:  # noqa: BLE001
+                if isinstance(e, log.FatalError):
+                    raise
+                log.warning("[%r] Failed : %s", loader, e)
+                continue
+            log.info("[%r] Done", loader)
+        log.info("Metadata planning done")
+    return p
+
+
+_CONVERTED_BUILD_TYPES = [plantypes.NEW_DOCKERFILE, plantypes.REUSE_DOCKERFILE, plantypes.S2I]
+
+
+def _ask(prob):
+    return qaengine.fetch_answer(prob)
+
+
+def curate_plan(p):
+    """``CuratePlan`` (planner.go:66-222): QA-driven selection of services,
+    containerization modes, artifact type and target cluster."""
+    qaengine.add_caches(list(reversed(p.qa_caches)))
+    names = sorted(p.services)
+    sel = _ask(qa.new_multiselect_problem("Select all services that are needed:",
+                                          ["The services unselected here will be ignored."], names, names)).get_slice_answer()
+    p.services = {s: p.services[s] for s in sel if s in p.services}
+
+    con_types = []
+    for sn in sorted(p.services):
+        for so in p.services[sn]:
+            if not common.is_string_present(con_types, so.container_build_type):
+                con_types.append(so.container_build_type)
+    sel_types = _ask(qa.new_multiselect_problem(
+        "Select all containerization modes that is of interest:",
+        ["The services which does not support any of the containerization technique you are interested will be ignored."],
+        con_types, con_types)).get_slice_answer()
+    if not sel_types:
+        log.fatal("No containerization technique was selected; Terminating.")
+
+    services = {}
+    for sn in sorted(p.services):
+        options = p.services[sn]
+        s_types = [so.container_build_type for so in options if common.is_string_present(sel_types, so.container_build_type)]
+        if not s_types:
+            log.warning("Ignoring service %s, since it does not support any selected containerization technique.", sn)
+            continue
+        chosen = s_types[0]
+        if len(s_types) > 1:
+            chosen = _ask(qa.new_select_problem("Select containerization technique for service " + sn + ":",
+                                                ["Choose the containerization technique of interest."], chosen,
+                                                s_types)).get_string_answer()
+        for so in options:
+            if so.container_build_type != chosen:
+                continue
+            conv = common.is_string_present(_CONVERTED_BUILD_TYPES, so.container_build_type)
+            if len(so.target_options) > 1:
+                opts = so.target_options
+                if conv:
+                    opts = []
+                    for o in so.target_options:
+                        try:
+                            opts.append(p.get_relative_path(o))
+                        except ValueError as e:
+                            log.error("Failed to make the option path %r relative to the root directory. Error: %r",
+                                      o, str(e))
+                mode = _ask(qa.new_select_problem("Select containerization technique's mode for service " + sn + ":",
+                                                  ["Choose the containerization technique mode of interest."], opts[0],
+                                                  opts)).get_string_answer()
+                if conv:
+                    try:
+                        mode = p.get_absolute_path(mode)
+                    except ValueError as e:
+                        log.error("Failed to make the option path %r absolute. Error: %r", mode, str(e))
+                so.target_options = [mode]
+            services[sn] = [so]
+            break
+    p.services = services
+
+    art = _ask(qa.new_select_problem("Choose the artifact type:",
+                                     ["Yamls - Generate Kubernetes Yamls", "Helm - Generate Helm chart",
+                                      "Knative - Create Knative artifacts"],
+                                     plantypes.YAMLS, [plantypes.YAMLS, plantypes.HELM, plantypes.KNATIVE])).get_string_answer()
+    p.kubernetes.artifact_type = art
+
+    clusters = sorted(metadata.ClusterMDLoader.get_clusters(p))
+    ctype = _ask(qa.new_select_problem("Choose the cluster type:", ["Choose the cluster type you would like to target"],
+                                       DEFAULT_CLUSTER_TYPE, clusters)).get_string_answer()
+    p.kubernetes.target_cluster_type = ctype
+    p.kubernetes.target_cluster_path = ""
+    return p
+
+
+def translate(p, outpath, qadisablecli=False):
+    """``Translate`` (translator.go:31-107): plan -> IR -> metadata ->
+    optimize -> compose output -> customize -> (helm) parameterize -> CI/CD
+    -> k8s/knative output."""
+    try:
+        ir = source_translator.translate(p)
+    except Exception as e:  # noqa: BLE001
+        if isinstance(e, log.FatalError):
+            raise
+        log.fatal("Failed to translate the plan to intermediate representation. Error: %r", str(e))
+    log.debug("Total storages loaded : %d", len(ir.storages))
+
+    log.info("Begin Metadata loading")
+    for loader in metadata.get_loaders():
+        log.debug("[%r] Begin metadata loading", loader)
+        try:
+            loader.load_to_ir(p, ir)
+        except Exception as e:  # noqa: BLE001
+            if isinstance(e, log.FatalError):
+                raise
+            log.warning("[%r] Failed : %s", loader, e)
+        else:
+            log.debug("[%r] Done", loader)
+    log.info("Metadata loading done")
+    log.debug("Total services loaded : %d", len(ir.services))
+    log.debug("Total containers loaded : %d", len(ir.containers))
+
+    ir = optimizer.optimize(ir)
+    log.debug("Total services optimized : %d", len(ir.services))
+
+    if os.path.lexists(outpath):
+        try:
+            if os.path.isdir(outpath) and not os.path.islink(outpath):
+                shutil.rmtree(outpath)
+            else:
+                os.remove(outpath)
+        except OSError as e:
+            log.error("Failed to remove the existing file/directory at the output path %r Error: %r", outpath, str(e))
+            log.error("Anything in the output path will get overwritten.")
+
+    dct = transformer.ComposeTransformer()
+    try:
+        dct.transform(ir)
+        dct.write_objects(outpath)
+    except Exception as e:  # noqa: BLE001
+        if isinstance(e, log.FatalError):
+            raise
+        log.error("Unable to write docker compose objects : %s", e)
+
+    ir = customizer.customize(ir)
+    log.debug("Total storages customized : %d", len(ir.storages))
+    if p.kubernetes.artifact_type == plantypes.HELM:
+        ir = parameterizer.parameterize(ir)
+
+    if any(c.new for c in ir.containers):
+        cicd = transformer.CICDTransformer()
+        try:
+            cicd.transform(ir)
+            cicd.write_objects(outpath)
+        except Exception as e:  # noqa: BLE001
+            if isinstance(e, log.FatalError):
+                raise
+            log.error("Unable to write the CI/CD artifacts to files. Error: %r", str(e))
+
+    ir.add_copy_sources_warning = qadisablecli
+    t = transformer.get_transformer(ir)
+    try:
+        t.transform(ir)
+    except Exception as e:  # noqa: BLE001
+        if isinstance(e, log.FatalError):
+            raise
+        log.fatal("Error during translate. Error: %r", str(e))
+    try:
+        t.write_objects(outpath)
+    except Exception as e:  # noqa: BLE001
+        if isinstance(e, log.FatalError):
+            raise
+        log.fatal("Unable to write objects Error: %r", str(e))
+    log.info("Execution completed")
+
+
+def get_version(long=False):
+    if not long:
+        return info.get_version()
+    return yamlio.dump(info.get_version_info().to_yaml())

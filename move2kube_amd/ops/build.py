@@ -1,0 +1,90 @@
+"""In-tree build of the native extensions.
+
+* ``_m2k_native*.so`` - C++17 pybind11 module (host runtime), built with g++.
+* ``libm2k_ed_hip.so`` - HIP library for gfx950 (``hipcc --offload-arch=gfx950``).
+
+Run ``python -m move2kube_amd.ops.build`` (or ``__graft_entry__.build()``).
+Builds are incremental: a target is rebuilt only when its source is newer.
+"""
+
+import os
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+
+
+def _ext_suffix():
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def native_target():
+    return os.path.join(HERE, "_m2k_native" + _ext_suffix())
+
+
+def hip_target():
+    return os.path.join(HERE, "libm2k_ed_hip.so")
+
+
+def _stale(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _run(cmd):
+    print("+ " + " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build_native(force=False):
+    import pybind11
+    src = os.path.join(CSRC, "m2k_native.cpp")
+    out = native_target()
+    if not force and not _stale(out, [src]):
+        return out
+    inc = sysconfig.get_paths()["include"]
+    cxx = os.environ.get("CXX", "g++")
+    _run([cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall",
+          "-I" + pybind11.get_include(), "-I" + inc, src, "-o", out + ".tmp", "-lpthread"])
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def find_hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
+            try:
+                subprocess.run([c, "--version"], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True)
+                return c
+            except (OSError, subprocess.CalledProcessError):
+                continue
+    return None
+
+
+def build_hip(force=False, arch="gfx950"):
+    src = os.path.join(CSRC, "ed_kernel.hip")
+    out = hip_target()
+    if not force and not _stale(out, [src]):
+        return out
+    hipcc = find_hipcc()
+    if hipcc is None:
+        raise RuntimeError("hipcc not found; cannot build the gfx950 kernel library")
+    _run([hipcc, "--offload-arch=" + arch, "-O3", "-std=c++17", "-shared", "-fPIC", src, "-o", out + ".tmp"])
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build_all(force=False):
+    outs = [build_native(force)]
+    outs.append(build_hip(force))
+    return outs
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    for o in build_all(force):
+        print(o)

@@ -1,0 +1,495 @@
+// Native runtime for move2kube_amd: the CPU/file-system hot path.
+//
+// The reference (a Go binary) spends its planning time in (a) repeated
+// filepath.Walk passes over the source tree (internal/common/utils.go:47-120,
+// internal/source/dockerfile2kube.go:154-167), (b) running every file through
+// buildkit's Dockerfile parser (dockerfile2kube.go:117-144) and (c) forking
+// one /bin/sh per (detector x directory) pair serially
+// (internal/containerizer/dockerfilecontainerizer.go:76-83).  This module
+// provides native replacements:
+//   walk()               one lexical-order lstat walk (Go filepath.Walk order)
+//   sniff_dockerfiles()  multi-threaded "first non-ARG instruction" scan
+//   run_commands()       bounded-parallel posix_spawn pool with captured stdout
+//   crc64_ecma/fnv64a    naming hashes (utils.go:292, compose/utils.go:121)
+//   edit_distance_batch  Wagner-Fischer (1,1,2) for fuzzy buildpack matching
+// All long-running entry points release the GIL.
+
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdint>
+#include <cstring>
+#include <fcntl.h>
+#include <poll.h>
+#include <signal.h>
+#include <spawn.h>
+#include <string>
+#include <sys/stat.h>
+#include <sys/time.h>
+#include <sys/types.h>
+#include <sys/wait.h>
+#include <thread>
+#include <time.h>
+#include <tuple>
+#include <unistd.h>
+#include <vector>
+#include <dirent.h>
+
+extern char **environ;
+
+namespace py = pybind11;
+
+namespace {
+
+// ----------------------------------------------------------------------------
+// walk
+// ----------------------------------------------------------------------------
+enum Kind { K_FILE = 0, K_DIR = 1, K_SYMLINK = 2, K_OTHER = 3 };
+
+struct WalkResult {
+  std::vector<std::string> paths;
+  std::vector<int> kinds;
+  std::vector<std::pair<std::string, std::string>> errors;
+};
+
+void walk_dir(const std::string &dir, WalkResult &r) {
+  r.paths.push_back(dir);
+  r.kinds.push_back(K_DIR);
+  DIR *d = opendir(dir.c_str());
+  if (!d) {
+    r.errors.emplace_back(dir, std::string("open ") + dir + ": " + strerror(errno));
+    return;
+  }
+  int dfd = dirfd(d);
+  struct Ent {
+    std::string name;
+    unsigned char type;
+  };
+  std::vector<Ent> ents;
+  while (struct dirent *e = readdir(d)) {
+    if (e->d_name[0] == '.' && (e->d_name[1] == 0 || (e->d_name[1] == '.' && e->d_name[2] == 0)))
+      continue;
+    ents.push_back({e->d_name, e->d_type});
+  }
+  // Go sorts directory entries by name (byte order) before walking.
+  std::sort(ents.begin(), ents.end(), [](const Ent &a, const Ent &b) { return a.name < b.name; });
+  const std::string prefix = (dir == "/") ? std::string("/") : dir + "/";
+  for (auto &e : ents) {
+    std::string p = prefix + e.name;
+    unsigned char t = e.type;
+    if (t == DT_UNKNOWN) {
+      struct stat st;
+      if (fstatat(dfd, e.name.c_str(), &st, AT_SYMLINK_NOFOLLOW) != 0) {
+        r.errors.emplace_back(p, std::string("lstat ") + p + ": " + strerror(errno));
+        continue;
+      }
+      if (S_ISDIR(st.st_mode)) t = DT_DIR;
+      else if (S_ISLNK(st.st_mode)) t = DT_LNK;
+      else if (S_ISREG(st.st_mode)) t = DT_REG;
+      else t = DT_FIFO;
+    }
+    if (t == DT_DIR) {
+      walk_dir(p, r);
+    } else {
+      r.paths.push_back(p);
+      r.kinds.push_back(t == DT_LNK ? K_SYMLINK : (t == DT_REG ? K_FILE : K_OTHER));
+    }
+  }
+  closedir(d);
+}
+
+py::tuple walk(const std::string &root) {
+  WalkResult r;
+  {
+    py::gil_scoped_release nogil;
+    struct stat st;
+    if (lstat(root.c_str(), &st) != 0) {
+      r.errors.emplace_back(root, std::string("lstat ") + root + ": " + strerror(errno));
+    } else if (S_ISDIR(st.st_mode)) {
+      walk_dir(root, r);
+    } else {
+      r.paths.push_back(root);
+      r.kinds.push_back(S_ISLNK(st.st_mode) ? K_SYMLINK : K_FILE);
+    }
+  }
+  return py::make_tuple(r.paths, r.kinds, r.errors);
+}
+
+// ----------------------------------------------------------------------------
+// Dockerfile sniffing (buildkit parser semantics for the first instructions)
+// ----------------------------------------------------------------------------
+// Returns, per file, the "Original" logical line of the first instruction that
+// is not ARG if that instruction is FROM; "" otherwise.  A file that fails to
+// parse (no instructions, over-long line, unreadable) yields "".
+
+inline bool is_space(unsigned char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n' || c == '\v' || c == '\f'; }
+
+std::string ltrim(const std::string &s) {
+  size_t i = 0;
+  while (i < s.size() && is_space((unsigned char)s[i])) i++;
+  return s.substr(i);
+}
+
+std::string lower_word(const std::string &s) {
+  size_t i = 0;
+  while (i < s.size() && !is_space((unsigned char)s[i])) i++;
+  std::string w = s.substr(0, i);
+  for (auto &c : w) c = (char)tolower((unsigned char)c);
+  return w;
+}
+
+// trim a trailing escape char followed by optional blanks: returns true if the line continues
+bool trim_continuation(std::string &line, char esc) {
+  size_t n = line.size();
+  while (n > 0 && (line[n - 1] == ' ' || line[n - 1] == '\t')) n--;
+  if (n > 0 && line[n - 1] == esc) {
+    line.resize(n - 1);
+    return true;
+  }
+  return false;
+}
+
+std::string sniff_one(const std::string &path) {
+  const size_t kMaxLine = 64 * 1024;  // bufio.Scanner default token limit
+  int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return "";
+  struct stat st;
+  if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
+    close(fd);
+    return "";
+  }
+  std::string buf;
+  size_t pos = 0;
+  bool eof = false;
+  auto fill = [&]() -> bool {
+    if (eof) return false;
+    char tmp[16384];
+    ssize_t k = read(fd, tmp, sizeof(tmp));
+    if (k <= 0) {
+      eof = true;
+      return false;
+    }
+    buf.append(tmp, (size_t)k);
+    return true;
+  };
+  // read a physical line (without the newline); returns false at EOF with no data
+  bool too_long = false;
+  auto next_line = [&](std::string &out) -> bool {
+    for (;;) {
+      size_t nl = buf.find('\n', pos);
+      if (nl != std::string::npos) {
+        out.assign(buf, pos, nl - pos);
+        pos = nl + 1;
+        if (!out.empty() && out.back() == '\r') out.pop_back();
+        if (out.size() > kMaxLine) too_long = true;
+        return true;
+      }
+      if (buf.size() - pos > kMaxLine) {
+        too_long = true;
+        return false;
+      }
+      if (!fill()) {
+        if (pos < buf.size()) {
+          out.assign(buf, pos, buf.size() - pos);
+          pos = buf.size();
+          if (!out.empty() && out.back() == '\r') out.pop_back();
+          return true;
+        }
+        return false;
+      }
+      if (pos > (1 << 20)) {
+        buf.erase(0, pos);
+        pos = 0;
+      }
+    }
+  };
+  char esc = '\\';
+  bool directives_open = true;
+  bool first_physical = true;
+  std::string result;
+  std::string phys;
+  while (next_line(phys)) {
+    if (too_long) break;
+    if (first_physical) {
+      first_physical = false;
+      if (phys.size() >= 3 && (unsigned char)phys[0] == 0xEF && (unsigned char)phys[1] == 0xBB && (unsigned char)phys[2] == 0xBF)
+        phys.erase(0, 3);
+    }
+    std::string line = ltrim(phys);
+    if (directives_open) {
+      // parser directives: "# escape=`" / "# syntax=..." before anything else
+      if (!line.empty() && line[0] == '#') {
+        std::string body = ltrim(line.substr(1));
+        std::string key;
+        size_t i = 0;
+        while (i < body.size() && (isalnum((unsigned char)body[i]) || body[i] == '_')) key += (char)tolower((unsigned char)body[i++]);
+        size_t j = i;
+        while (j < body.size() && (body[j] == ' ' || body[j] == '\t')) j++;
+        if (!key.empty() && j < body.size() && body[j] == '=') {
+          std::string val = ltrim(body.substr(j + 1));
+          while (!val.empty() && is_space((unsigned char)val.back())) val.pop_back();
+          if (key == "escape" && (val == "`" || val == "\\")) esc = val[0];
+          continue;
+        }
+        directives_open = false;
+      } else if (!line.empty()) {
+        directives_open = false;
+      }
+    }
+    if (line.empty() || line[0] == '#') continue;
+    bool cont = trim_continuation(line, esc);
+    while (cont) {
+      std::string nxt;
+      if (!next_line(nxt) || too_long) {
+        cont = false;
+        break;
+      }
+      std::string t = ltrim(nxt);
+      if (!t.empty() && t[0] == '#') continue;  // comment inside continuation
+      if (t.empty()) continue;                   // empty continuation line
+      cont = trim_continuation(nxt, esc);
+      line += nxt;
+    }
+    if (too_long) break;
+    std::string cmd = lower_word(line);
+    if (cmd == "arg") continue;
+    if (cmd == "from") result = line;
+    break;
+  }
+  close(fd);
+  if (too_long) return "";
+  return result;
+}
+
+std::vector<std::string> sniff_dockerfiles(const std::vector<std::string> &paths, int nthreads) {
+  std::vector<std::string> out(paths.size());
+  py::gil_scoped_release nogil;
+  if (nthreads <= 1 || paths.size() < 64) {
+    for (size_t i = 0; i < paths.size(); i++) out[i] = sniff_one(paths[i]);
+    return out;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> pool;
+  int nt = std::min<int>(nthreads, (int)((paths.size() + 31) / 32));
+  for (int t = 0; t < nt; t++) {
+    pool.emplace_back([&]() {
+      for (;;) {
+        size_t i = next.fetch_add(1);
+        if (i >= paths.size()) break;
+        out[i] = sniff_one(paths[i]);
+      }
+    });
+  }
+  for (auto &th : pool) th.join();
+  return out;
+}
+
+// ----------------------------------------------------------------------------
+// hashes
+// ----------------------------------------------------------------------------
+uint64_t crc_table[256];
+bool crc_init = false;
+
+uint64_t crc64_ecma(const py::bytes &b) {
+  if (!crc_init) {
+    for (int i = 0; i < 256; i++) {
+      uint64_t c = (uint64_t)i;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0xC96C5795D7870F42ULL : (c >> 1);
+      crc_table[i] = c;
+    }
+    crc_init = true;
+  }
+  std::string s = b;
+  uint64_t crc = ~0ULL;
+  for (unsigned char c : s) crc = crc_table[(crc ^ c) & 0xFF] ^ (crc >> 8);
+  return ~crc;
+}
+
+uint64_t fnv64a(const py::bytes &b) {
+  std::string s = b;
+  uint64_t h = 0xcbf29ce484222325ULL;
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 0x100000001b3ULL;
+  }
+  return h;
+}
+
+// ----------------------------------------------------------------------------
+// Wagner-Fischer (smetrics.WagnerFischer semantics, byte-wise)
+// ----------------------------------------------------------------------------
+int wagner_fischer(const std::string &a, const std::string &b, int icost, int dcost, int scost) {
+  std::vector<int> row1(b.size() + 1), row2(b.size() + 1);
+  for (size_t i = 1; i <= b.size(); i++) row1[i] = (int)i * icost;
+  for (size_t i = 1; i <= a.size(); i++) {
+    row2[0] = (int)i * dcost;
+    for (size_t j = 1; j <= b.size(); j++) {
+      if (a[i - 1] == b[j - 1]) {
+        row2[j] = row1[j - 1];
+      } else {
+        int ins = row2[j - 1] + icost, del = row1[j] + dcost, sub = row1[j - 1] + scost;
+        if (ins < del && ins < sub) row2[j] = ins;
+        else if (del < sub) row2[j] = del;
+        else row2[j] = sub;
+      }
+    }
+    std::swap(row1, row2);
+  }
+  return row1[b.size()];
+}
+
+// distance matrix [len(as) x len(bs)], row-major
+std::vector<int> edit_distance_batch(const std::vector<std::string> &as, const std::vector<std::string> &bs,
+                                     int icost, int dcost, int scost, int nthreads) {
+  std::vector<int> out(as.size() * bs.size());
+  py::gil_scoped_release nogil;
+  size_t total = out.size();
+  auto work = [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; k++) out[k] = wagner_fischer(as[k / bs.size()], bs[k % bs.size()], icost, dcost, scost);
+  };
+  if (nthreads <= 1 || total < 4096) {
+    if (total) work(0, total);
+    return out;
+  }
+  std::vector<std::thread> pool;
+  size_t chunk = (total + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; t++) {
+    size_t lo = t * chunk, hi = std::min(total, lo + chunk);
+    if (lo >= hi) break;
+    pool.emplace_back(work, lo, hi);
+  }
+  for (auto &th : pool) th.join();
+  return out;
+}
+
+// ----------------------------------------------------------------------------
+// bounded-parallel process pool
+// ----------------------------------------------------------------------------
+struct Child {
+  pid_t pid = -1;
+  int outfd = -1;
+  size_t idx = 0;
+  std::string out;
+  bool done_reading = false;
+  double start = 0;
+  bool killed = false;
+};
+
+double now_s() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+// Runs argv[i] with working directory cwd[i]; stdout captured, stderr inherited
+// (the reference wires detector stderr to the console).  At most `parallel`
+// children run at once.  Returns (exit_code, stdout) per command; exit code
+// -1 means spawn failure, -2 timeout.
+std::vector<std::pair<int, py::bytes>> run_commands(const std::vector<std::vector<std::string>> &argvs,
+                                                     const std::vector<std::string> &cwds, int parallel,
+                                                     double timeout_s) {
+  std::vector<int> codes(argvs.size(), -1);
+  std::vector<std::string> outs(argvs.size());
+  {
+    py::gil_scoped_release nogil;
+    if (parallel < 1) parallel = 1;
+    std::vector<Child> running;
+    size_t next = 0;
+    auto spawn = [&](size_t i) -> bool {
+      int pfd[2];
+      if (pipe2(pfd, O_CLOEXEC) != 0) return false;
+      posix_spawn_file_actions_t fa;
+      posix_spawn_file_actions_init(&fa);
+      posix_spawn_file_actions_adddup2(&fa, pfd[1], 1);
+      int devnull = -1;
+      (void)devnull;
+      posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
+#if defined(__GLIBC__) && (__GLIBC__ > 2 || (__GLIBC__ == 2 && __GLIBC_MINOR__ >= 29))
+      if (!cwds[i].empty()) posix_spawn_file_actions_addchdir_np(&fa, cwds[i].c_str());
+#endif
+      std::vector<char *> argv;
+      for (auto &s : argvs[i]) argv.push_back(const_cast<char *>(s.c_str()));
+      argv.push_back(nullptr);
+      pid_t pid;
+      int rc = posix_spawnp(&pid, argv[0], &fa, nullptr, argv.data(), environ);
+      posix_spawn_file_actions_destroy(&fa);
+      close(pfd[1]);
+      if (rc != 0) {
+        close(pfd[0]);
+        return false;
+      }
+      Child c;
+      c.pid = pid;
+      c.outfd = pfd[0];
+      c.idx = i;
+      c.start = now_s();
+      running.push_back(std::move(c));
+      return true;
+    };
+    while (next < argvs.size() || !running.empty()) {
+      while ((int)running.size() < parallel && next < argvs.size()) {
+        size_t i = next++;
+        if (!spawn(i)) codes[i] = -1;
+      }
+      if (running.empty()) continue;
+      std::vector<struct pollfd> pfds;
+      for (auto &c : running) pfds.push_back({c.done_reading ? -1 : c.outfd, POLLIN, 0});
+      int pr = poll(pfds.data(), pfds.size(), 50);
+      (void)pr;
+      for (size_t k = 0; k < running.size(); k++) {
+        Child &c = running[k];
+        if (!c.done_reading && (pfds[k].revents & (POLLIN | POLLHUP | POLLERR))) {
+          char buf[8192];
+          ssize_t n = read(c.outfd, buf, sizeof(buf));
+          if (n > 0) c.out.append(buf, (size_t)n);
+          else c.done_reading = true;
+        }
+        if (!c.killed && timeout_s > 0 && now_s() - c.start > timeout_s) {
+          kill(c.pid, SIGKILL);
+          c.killed = true;
+        }
+      }
+      // reap finished children whose output is drained
+      for (size_t k = 0; k < running.size();) {
+        Child &c = running[k];
+        if (c.done_reading) {
+          int status = 0;
+          pid_t w = waitpid(c.pid, &status, c.killed ? 0 : WNOHANG);
+          if (w == c.pid) {
+            close(c.outfd);
+            int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+            if (c.killed) code = -2;
+            codes[c.idx] = code;
+            outs[c.idx] = std::move(c.out);
+            running.erase(running.begin() + k);
+            continue;
+          }
+        }
+        k++;
+      }
+    }
+  }
+  std::vector<std::pair<int, py::bytes>> res;
+  res.reserve(argvs.size());
+  for (size_t i = 0; i < argvs.size(); i++) res.emplace_back(codes[i], py::bytes(outs[i]));
+  return res;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_m2k_native, m) {
+  m.doc() = "move2kube_amd native runtime (walk, sniff, spawn pool, hashes, edit distance)";
+  m.def("walk", &walk, py::arg("root"));
+  m.def("sniff_dockerfiles", &sniff_dockerfiles, py::arg("paths"), py::arg("nthreads") = 8);
+  m.def("crc64_ecma", &crc64_ecma);
+  m.def("fnv64a", &fnv64a);
+  m.def("wagner_fischer", &wagner_fischer, py::arg("a"), py::arg("b"), py::arg("icost") = 1, py::arg("dcost") = 1,
+        py::arg("scost") = 2);
+  m.def("edit_distance_batch", &edit_distance_batch, py::arg("as"), py::arg("bs"), py::arg("icost") = 1,
+        py::arg("dcost") = 1, py::arg("scost") = 2, py::arg("nthreads") = 8);
+  m.def("run_commands", &run_commands, py::arg("argvs"), py::arg("cwds"), py::arg("parallel") = 8,
+        py::arg("timeout_s") = 0.0);
+}

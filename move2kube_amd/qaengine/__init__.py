@@ -1,0 +1,6 @@
+"""The QA engine: an ordered chain of answer sources (QA caches, defaults,
+an interactive CLI, or the HTTP REST API the UI drives) plus a write cache
+that checkpoints every answer."""
+
+from .engine import (add_caches, add_engine, fetch_answer, get_write_cache, reset,  # noqa: F401
+                     set_write_cache, start_engine)

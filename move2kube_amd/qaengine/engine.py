@@ -1,0 +1,144 @@
+"""QA engine chain (reference ``internal/qaengine/engine.go:29-123``).
+
+Engines are consulted in order until one resolves a problem; cache engines
+added with :func:`add_caches` are *prepended* (highest priority).  Every
+resolved answer is appended to the write cache (``<out>/m2kqacache.yaml``),
+which is rewritten on each answer - the resumable checkpoint of an
+interactive session.  Passwords are never cached.
+
+Difference from the reference: when no engine resolves a problem the
+reference loops forever on the last engine; here the last
+engine is retried a bounded number of times and then the problem's default is
+used (or an error raised when it has none).
+"""
+
+import os
+import threading
+
+from ..models import qa
+from ..utils import log
+from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION
+
+_lock = threading.RLock()
+_engines = []
+_write_cache = None
+MAX_LAST_ENGINE_RETRIES = 8
+
+
+class Engine:
+    def start_engine(self):
+        pass
+
+    def fetch_answer(self, prob):
+        raise NotImplementedError
+
+    def __repr__(self):
+        return type(self).__name__
+
+
+def reset():
+    """Drop all engines and the write cache (tests / in-process reuse)."""
+    global _engines, _write_cache
+    with _lock:
+        _engines = []
+        _write_cache = None
+
+
+def engines():
+    return list(_engines)
+
+
+def start_engine(qaskip=False, qaport=0, qadisablecli=False):
+    from .cli_engine import CliEngine
+    from .default_engine import DefaultEngine
+    from .rest_engine import HTTPRESTEngine
+    if qaskip:
+        e = DefaultEngine()
+    elif not qadisablecli:
+        e = CliEngine()
+    else:
+        e = HTTPRESTEngine(qaport)
+    add_engine(e)
+    return e
+
+
+def add_engine(e):
+    try:
+        e.start_engine()
+    except Exception as ex:  # noqa: BLE001
+        log.error("Ignoring engine %r due to error : %s", e, ex)
+        return
+    with _lock:
+        _engines.append(e)
+
+
+def add_caches(cache_files):
+    from .cache_engine import CacheEngine
+    new = []
+    for f in cache_files:
+        e = CacheEngine(f)
+        try:
+            e.start_engine()
+        except Exception as ex:  # noqa: BLE001
+            log.error("Ignoring engine %r due to error : %s", e, ex)
+            continue
+        new.append(e)
+    with _lock:
+        _engines[:0] = new
+
+
+def fetch_answer(prob):
+    """Resolve ``prob`` through the engine chain and record the answer."""
+    ans = prob
+    err = None
+    with _lock:
+        chain = list(_engines)
+    if not chain:
+        from .default_engine import DefaultEngine
+        chain = [DefaultEngine()]
+    for e in chain:
+        try:
+            ans = e.fetch_answer(prob.copy())
+            err = None
+        except Exception as ex:  # noqa: BLE001
+            err = ex
+            log.warning("Error while fetching answer using engine %r : %s", e, ex)
+            continue
+        if ans.resolved:
+            break
+    if not ans.resolved:
+        last = chain[-1]
+        for _ in range(MAX_LAST_ENGINE_RETRIES):
+            try:
+                ans = last.fetch_answer(prob.copy())
+                err = None
+            except Exception as ex:  # noqa: BLE001
+                err = ex
+                continue
+            if ans.resolved:
+                break
+        if not ans.resolved:
+            ans = prob.copy()
+            try:
+                ans.set_answer(prob.default)
+                err = None
+            except qa.ProblemError as ex:
+                log.fatal("Unable to get answer to %s : %s", prob.desc, err or ex)
+    if err is None and ans.resolved and _write_cache is not None:
+        _write_cache.add_problem_solution(ans)
+    return ans
+
+
+def set_write_cache(cache_file):
+    global _write_cache
+    d = os.path.dirname(cache_file)
+    if d:
+        os.makedirs(d, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+    c = qa.Cache(cache_file)
+    c.write()
+    _write_cache = c
+    return c
+
+
+def get_write_cache():
+    return _write_cache

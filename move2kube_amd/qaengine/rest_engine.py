@@ -1,0 +1,141 @@
+"""HTTP REST QA engine - the protocol the move2kube UI drives.
+
+Reference: ``internal/qaengine/httprestengine.go:33-143``.
+
+* ``GET  /problems/current``           -> current problem as JSON; blocks until
+  the translator produces one.
+* ``POST /problems/current/solution``  -> body is a JSON ``[]string`` answer.
+
+The translator thread and the HTTP handlers hand problems/answers over through
+queues; access to the current problem is guarded by a lock (the reference
+shares it across handler goroutines unsynchronised - SURVEY 2.13 #12).
+"""
+
+import json
+import queue
+import socket
+import threading
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+from ..models import qa
+from ..utils import log
+from .engine import Engine
+
+PROBLEMS_URL = "/problems"
+CURRENT_PROBLEM_URL = PROBLEMS_URL + "/current"
+CURRENT_SOLUTION_URL = CURRENT_PROBLEM_URL + "/solution"
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class HTTPRESTEngine(Engine):
+    def __init__(self, port=0, host=""):
+        self.port = port
+        self.host = host
+        self.current = qa.Problem(id=0, resolved=True)
+        self._cur_lock = threading.Lock()
+        self.problems = queue.Queue()
+        self.answers = queue.Queue()
+        self.server = None
+        self.thread = None
+
+    def start_engine(self):
+        if self.port == 0:
+            self.port = free_port()
+        engine = self
+
+        class Handler(BaseHTTPRequestHandler):
+            def log_message(self, fmt, *args):
+                log.debug("qa-http: " + fmt, *args)
+
+            def _send(self, code, body, ctype="application/json"):
+                data = body.encode() if isinstance(body, str) else body
+                self.send_response(code)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(data)))
+                self.end_headers()
+                self.wfile.write(data)
+
+            def do_GET(self):  # noqa: N802
+                if self.path.split("?")[0] != CURRENT_PROBLEM_URL:
+                    self._send(404, "404 page not found\n", "text/plain")
+                    return
+                self._send(200, json.dumps(engine.next_problem().to_json()) + "\n")
+
+            def do_POST(self):  # noqa: N802
+                if self.path.split("?")[0] != CURRENT_SOLUTION_URL:
+                    self._send(404, "404 page not found\n", "text/plain")
+                    return
+                n = int(self.headers.get("Content-Length") or 0)
+                body = self.rfile.read(n)
+                try:
+                    sol = json.loads(body.decode() or "null")
+                    if sol is not None and not (isinstance(sol, list) and all(isinstance(x, str) for x in sol)):
+                        raise ValueError("solution must be a JSON array of strings")
+                except ValueError as e:
+                    self._send(500, "Error in un-marshalling solution in QA engine: %s\n" % e, "text/plain")
+                    return
+                err = engine.submit_solution(sol or [])
+                if err:
+                    self._send(500, "Unsuitable answer : %s\n" % err, "text/plain")
+                else:
+                    self._send(200, "")
+
+        try:
+            self.server = ThreadingHTTPServer((self.host, self.port), Handler)
+        except OSError as e:
+            raise RuntimeError("Unable to listen on port %d : %s" % (self.port, e))
+        self.server.daemon_threads = True
+        self.thread = threading.Thread(target=self.server.serve_forever, name="m2k-qa-http", daemon=True)
+        self.thread.start()
+        log.info("Started QA engine on: localhost:%d", self.port)
+
+    def stop(self):
+        if self.server is not None:
+            self.server.shutdown()
+            self.server.server_close()
+
+    # called from HTTP handler threads
+    def next_problem(self):
+        with self._cur_lock:
+            cur = self.current
+            if cur.resolved or cur.id == 0:
+                need_new = True
+            else:
+                return cur.copy()
+        if need_new:
+            p = self.problems.get()
+            with self._cur_lock:
+                self.current = p
+                return p.copy()
+
+    def submit_solution(self, sol):
+        with self._cur_lock:
+            if self.current.id == 0 or self.current.resolved:
+                return "no open problem"
+            p = self.current.copy()
+            try:
+                p.set_answer(sol)
+            except qa.ProblemError as e:
+                return str(e)
+            self.current = p
+        self.answers.put(p.copy())
+        return None
+
+    # called from the translator thread
+    def fetch_answer(self, prob):
+        if prob.id == 0:
+            prob.resolved = True
+        if not prob.resolved:
+            log.debug("Passing problem to HTTP REST QA Engine ID: %d, desc: %s", prob.id, prob.desc)
+            self.problems.put(prob)
+            prob = self.answers.get()
+            if not prob.resolved:
+                raise qa.ProblemError("Unable to resolve question %s" % prob.desc)
+        return prob

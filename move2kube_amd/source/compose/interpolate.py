@@ -1,0 +1,87 @@
+"""Compose variable interpolation.
+
+* v3 follows docker/cli ``template.Substitute``: ``$$`` escapes, ``$VAR``,
+  ``${VAR}``, ``${VAR:-default}``, ``${VAR-default}``, ``${VAR:?err}``,
+  ``${VAR?err}``; an unset variable becomes the empty string; a malformed
+  ``$`` is an error.
+* v1/v2 follows libcompose: the same substitution syntax, unset variables are
+  replaced by "" with a warning.
+Only values are interpolated (not keys), recursively through maps and lists.
+"""
+
+import os
+import re
+
+from ...utils import log
+
+_PATTERN = re.compile(
+    r"\$(?:(?P<escaped>\$)|(?P<named>[_a-zA-Z][_a-zA-Z0-9]*)|\{(?P<braced>[_a-zA-Z][_a-zA-Z0-9]*(?::?[-?][^}]*)?)\}|(?P<invalid>))")
+
+
+class InterpolationError(ValueError):
+    pass
+
+
+def substitute(s, mapping, warn_missing=False):
+    def repl(m):
+        if m.group("escaped") is not None:
+            return "$"
+        name = m.group("named") or m.group("braced")
+        if name is None:
+            raise InterpolationError("Invalid template: %r" % s)
+        if m.group("braced") is not None:
+            mm = re.match(r"^([_a-zA-Z][_a-zA-Z0-9]*)(?:(:?)([-?])(.*))?$", name, re.S)
+            var, colon, op, arg = mm.group(1), mm.group(2), mm.group(3), mm.group(4)
+            val = mapping(var)
+            if op == "-":
+                if val is None or (colon and val == ""):
+                    return arg
+                return val
+            if op == "?":
+                if val is None or (colon and val == ""):
+                    raise InterpolationError("required variable %s is missing a value: %s" % (var, arg))
+                return val
+            name = var
+        val = mapping(name)
+        if val is None:
+            if warn_missing:
+                log.warning("The %s variable is not set. Substituting a blank string.", name)
+            return ""
+        return val
+    if "$" not in s:
+        return s
+    return _PATTERN.sub(repl, s)
+
+
+def interpolate(obj, mapping, warn_missing=False):
+    if isinstance(obj, str):
+        return substitute(obj, mapping, warn_missing)
+    if isinstance(obj, dict):
+        return {k: interpolate(v, mapping, warn_missing) for k, v in obj.items()}
+    if isinstance(obj, list):
+        return [interpolate(v, mapping, warn_missing) for v in obj]
+    return obj
+
+
+def os_env_mapping(env=None):
+    env = dict(os.environ) if env is None else env
+    return env.get
+
+
+def parse_env_file(path):
+    """Parse a docker env file (``KEY=VAL`` lines, ``#`` comments, bare ``KEY``
+    inherits from the OS environment)."""
+    out = {}
+    with open(path, encoding="utf-8", errors="replace") as f:
+        for raw in f:
+            line = raw.strip()
+            if not line or line.startswith("#"):
+                continue
+            if "=" in line:
+                k, v = line.split("=", 1)
+                out[k.strip()] = v
+            else:
+                v = os.environ.get(line)
+                if v is not None:
+                    out[line] = v
+    return out

@@ -1,0 +1,232 @@
+"""Compose helpers (reference ``internal/source/compose/utils.go``) plus the
+value parsers the Go compose libraries provide (durations, byte sizes, port
+specs, volume specs, Kubernetes quantity formatting)."""
+
+import os
+import re
+import shlex
+
+from ...utils import common, log
+from ...utils.constants import settings
+
+MODE_READ_ONLY = "ro"
+TMPFS_PATH = "tmpfs"
+DEFAULT_SECRET_BASE_PATH = "/var/secrets"
+ENV_FILE = "env_file"
+
+
+def get_environment_variables():
+    """OS environment as the v3 interpolation source (empty with --ignoreenv)."""
+    if settings.ignore_environment:
+        return {}
+    return dict(os.environ)
+
+
+def make_volumes_from_tmpfs(service_name, tfs_list):
+    vms, vols = [], []
+    for i, t in enumerate(tfs_list or []):
+        name = "%s-%s-%d" % (service_name, TMPFS_PATH, i)
+        vms.append({"name": name, "mountPath": t.split(":")[0]})
+        vols.append({"name": name, "emptyDir": {"medium": "Memory"}})
+    return vms, vols
+
+
+def is_path(s):
+    return "/" in s or s == "."
+
+
+def get_hash(data):
+    return common.fnv64a(data.encode() if isinstance(data, str) else data)
+
+
+def check_for_dockerfile(path):
+    if not os.path.exists(path):
+        log.error("There is no file at path %s", path)
+        return False
+    if os.path.isdir(path):
+        log.error("The path %s points to a directory. Expected a Dockerfile.", path)
+        return False
+    return True
+
+
+# ---------------------------------------------------------------------------
+# Go value parsers
+# ---------------------------------------------------------------------------
+
+_DUR_UNITS = {"ns": 1, "us": 1000, "µs": 1000, "μs": 1000, "ms": 10 ** 6, "s": 10 ** 9,
+              "m": 60 * 10 ** 9, "h": 3600 * 10 ** 9}
+_DUR_RE = re.compile(r"(\d+\.?\d*|\.\d+)(ns|us|µs|μs|ms|s|m|h)")
+
+
+def parse_duration(s):
+    """Go ``time.ParseDuration`` -> nanoseconds."""
+    if s is None:
+        raise ValueError("time: invalid duration")
+    s = str(s)
+    orig = s
+    neg = False
+    if s[:1] in "+-":
+        neg = s[0] == "-"
+        s = s[1:]
+    if s == "0":
+        return 0
+    if not s:
+        raise ValueError("time: invalid duration %r" % orig)
+    total = 0.0
+    pos = 0
+    while pos < len(s):
+        m = _DUR_RE.match(s, pos)
+        if not m:
+            raise ValueError("time: invalid duration %r" % orig)
+        total += float(m.group(1)) * _DUR_UNITS[m.group(2)]
+        pos = m.end()
+    v = int(total)
+    return -v if neg else v
+
+
+_RAM_RE = re.compile(r"^(\d+(?:\.\d+)*) ?([kKmMgGtTpP])?[iI]?[bB]?$")
+_RAM_MULT = {"k": 1024, "m": 1024 ** 2, "g": 1024 ** 3, "t": 1024 ** 4, "p": 1024 ** 5}
+
+
+def ram_in_bytes(v):
+    """docker/go-units ``RAMInBytes`` (binary multipliers); ints pass through."""
+    if isinstance(v, bool):
+        raise ValueError("invalid size")
+    if isinstance(v, (int, float)):
+        return int(v)
+    m = _RAM_RE.match(str(v).strip())
+    if not m:
+        raise ValueError("invalid size: %r" % v)
+    num = float(m.group(1))
+    unit = (m.group(2) or "").lower()
+    return int(num * _RAM_MULT.get(unit, 1))
+
+
+def format_quantity_decimal_exponent(value):
+    """apimachinery Quantity.String() for an int with an unknown format
+    (falls back to DecimalExponent)."""
+    if value == 0:
+        return "0"
+    neg = value < 0
+    v = abs(int(value))
+    exp = 0
+    while v % 1000 == 0 and v != 0:
+        v //= 1000
+        exp += 3
+    s = str(v) + ("e%d" % exp if exp else "")
+    return ("-" if neg else "") + s
+
+
+def format_milli_quantity(milli):
+    """Quantity.String() of NewMilliQuantity(milli, DecimalSI)."""
+    if milli == 0:
+        return "0"
+    neg = milli < 0
+    m = abs(int(milli))
+    if m % 1000 == 0:
+        v = m // 1000
+        suffixes = [(10 ** 18, "E"), (10 ** 15, "P"), (10 ** 12, "T"), (10 ** 9, "G"), (10 ** 6, "M"), (10 ** 3, "k")]
+        out = str(v)
+        for mult, suf in suffixes:
+            if v % mult == 0:
+                out = str(v // mult) + suf
+                break
+    else:
+        out = str(m) + "m"
+    return ("-" if neg else "") + out
+
+
+def shell_split(s):
+    """docker/cli ``ShellCommand`` (mattn/go-shellwords) for string commands."""
+    try:
+        return shlex.split(s)
+    except ValueError:
+        return s.split()
+
+
+# ---------------------------------------------------------------------------
+# port specs (docker/go-connections nat.ParsePortSpec)
+# ---------------------------------------------------------------------------
+
+def _port_range(s):
+    if "-" in s:
+        a, b = s.split("-", 1)
+        a, b = int(a), int(b)
+        if b < a:
+            raise ValueError("invalid range")
+        return list(range(a, b + 1))
+    return [int(s)]
+
+
+def parse_port_spec(raw):
+    """Returns [(host_ip, published, target, proto)]; published 0 when unset."""
+    spec = str(raw)
+    proto = "tcp"
+    if "/" in spec:
+        spec, proto = spec.rsplit("/", 1)
+        proto = proto.lower() or "tcp"
+    parts = spec.rsplit(":", 2) if spec.count(":") <= 2 else None
+    if parts is None:
+        # IPv6 host ip in brackets
+        m = re.match(r"^\[([^\]]+)\]:(.*)$", spec)
+        if not m:
+            raise ValueError("Invalid port spec %r" % raw)
+        rest = m.group(2).split(":")
+        parts = [m.group(1)] + rest
+    host_ip, host_port, cont = "", "", ""
+    if len(parts) == 1:
+        cont = parts[0]
+    elif len(parts) == 2:
+        host_port, cont = parts
+    else:
+        host_ip, host_port, cont = parts
+    if not cont:
+        raise ValueError("No port specified: %r" % raw)
+    cports = _port_range(cont)
+    hports = _port_range(host_port) if host_port else []
+    out = []
+    if hports and len(hports) != len(cports):
+        if len(hports) > 1:
+            raise ValueError("Invalid ranges specified for container and host Ports: %r" % raw)
+        # single host port range start for a container range -> docker picks a port
+        hports = hports * len(cports)
+    for i, c in enumerate(cports):
+        out.append((host_ip, hports[i] if hports else 0, c, proto))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# volume specs
+# ---------------------------------------------------------------------------
+
+def parse_volume_v3(spec):
+    """docker/cli ``loader.ParseVolume`` for Linux hosts.
+
+    Returns dict(type, source, target, read_only)."""
+    spec = str(spec)
+    parts = spec.split(":")
+    vol = {"type": "volume", "source": "", "target": "", "read_only": False}
+    if len(parts) == 1:
+        vol["target"] = parts[0]
+    else:
+        vol["source"] = parts[0]
+        vol["target"] = parts[1]
+        if len(parts) >= 3:
+            for opt in parts[2].split(","):
+                if opt == "ro":
+                    vol["read_only"] = True
+                elif opt == "rw":
+                    vol["read_only"] = False
+    src = vol["source"]
+    if src and (src[0] in "./~"):
+        vol["type"] = "bind"
+    return vol
+
+
+def resolve_bind_source(src, working_dir):
+    if src.startswith("~"):
+        home = os.path.expanduser("~")
+        src = home + src[1:]
+    if not os.path.isabs(src):
+        src = os.path.normpath(os.path.join(working_dir, src))
+    return src

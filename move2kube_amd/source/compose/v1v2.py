@@ -1,0 +1,375 @@
+"""Compose file format v1/v2 loader (reference ``internal/source/compose/v1v2.go``).
+
+Parsing mirrors libcompose as the reference configures it: interpolation with
+``.env`` (current directory) then OS environment lookups, schema validation
+(v1: every top-level key is a service; v2: ``services``/``networks``/
+``volumes``), pruning of missing env_files, and resolution of build contexts
+and bind-volume sources relative to the compose file.
+"""
+
+import os
+import re
+
+from ...containerizer.reusedockerfile import ReuseDockerfileContainerizer
+from ...models import ir as irtypes
+from ...utils import common, log, yamlio
+from ...utils.constants import VOLUME_PREFIX, settings
+from . import utils as cu
+from .interpolate import InterpolationError, interpolate, parse_env_file
+from .v3 import ComposeError, _as_list_of_str, _labels, _scalar_str
+
+V1_SERVICE_KEYS = {
+    "build", "cap_add", "cap_drop", "cgroup_parent", "command", "container_name", "cpu_shares", "cpu_quota",
+    "cpuset", "devices", "dns", "dns_search", "dockerfile", "domainname", "entrypoint", "env_file", "environment",
+    "expose", "extends", "external_links", "extra_hosts", "hostname", "image", "ipc", "labels", "links",
+    "log_driver", "log_opt", "mac_address", "mem_limit", "memswap_limit", "mem_swappiness", "net", "pid", "ports",
+    "privileged", "read_only", "restart", "security_opt", "shm_size", "stdin_open", "stop_signal", "tty",
+    "ulimits", "user", "volumes", "volume_driver", "volumes_from", "working_dir", "group_add", "tmpfs",
+    "stop_grace_period", "oom_score_adj", "cpus",
+}
+V2_SERVICE_KEYS = V1_SERVICE_KEYS - {"dockerfile", "log_driver", "log_opt", "net"} | {
+    "depends_on", "logging", "network_mode", "networks", "isolation", "healthcheck", "init", "sysctls",
+    "userns_mode", "pids_limit", "runtime", "storage_opt", "mem_reservation", "blkio_config", "cpu_count",
+    "cpu_percent", "cpu_period", "cpu_rt_period", "cpu_rt_runtime", "device_cgroup_rules", "scale"}
+V2_TOP_KEYS = {"version", "services", "networks", "volumes"}
+SUPPORTED_V2 = {"2", "2.0", "2.1"}
+
+
+def _normalize_project_name(s):
+    return re.sub(r"[^a-z0-9]", "", s.lower())
+
+
+def parse_v2(path):
+    """Parse a v1/v2 compose file -> {"version", "project", "services": [...], "networks": {...}}."""
+    try:
+        text = common.read_text(path)
+        parsed = yamlio.load(text)
+    except (OSError, yamlio.YAMLError) as e:
+        raise ComposeError("Failed to load docker compose file at path %s Error: %s" % (path, e))
+    if parsed is None:
+        raise ComposeError("Failed to load docker compose file at path %s Error: empty file" % path)
+    if not isinstance(parsed, dict):
+        raise ComposeError("Failed to load docker compose file at path %s Error: top-level must be a mapping" % path)
+    version = parsed.get("version")
+    if version is not None:
+        if isinstance(version, float):
+            version = yamlio.go_format_float(version)
+        version = str(version)
+        if version not in SUPPORTED_V2:
+            raise ComposeError("Unsupported config version %s" % version)
+        unknown = [k for k in parsed if k not in V2_TOP_KEYS]
+        if unknown:
+            raise ComposeError("Additional property %s is not allowed" % unknown[0])
+        raw_services = parsed.get("services") or {}
+        if not isinstance(raw_services, dict):
+            raise ComposeError("services must be a mapping")
+        allowed = V2_SERVICE_KEYS
+    else:
+        version = ""
+        raw_services = parsed
+        allowed = V1_SERVICE_KEYS
+    # env lookup: .env of the working directory first, then the OS environment (libcompose)
+    env_path = ".env" if settings.ignore_environment else os.path.abspath(".env")
+    dotenv = {}
+    if os.path.isfile(env_path):
+        try:
+            dotenv = parse_env_file(env_path)
+        except OSError:
+            dotenv = {}
+
+    def lookup(k):
+        if k in dotenv:
+            return dotenv[k]
+        return os.environ.get(k)
+    try:
+        raw_services = interpolate(raw_services, lookup, warn_missing=True)
+    except InterpolationError as e:
+        raise ComposeError(str(e))
+    base = os.path.dirname(os.path.abspath(path))
+    services = []
+    for name, svc in raw_services.items():
+        if not isinstance(name, str):
+            raise ComposeError("Non-string service name %r" % (name,))
+        if not isinstance(svc, dict):
+            raise ComposeError("Service %s has neither an image nor a build context specified" % name
+                               if svc is None else "Invalid type for service %s" % name)
+        for k in svc:
+            if k not in allowed:
+                raise ComposeError("Unsupported config option for %s service: '%s'" % (name, k))
+        if version == "":
+            has_build = "build" in svc or "dockerfile" in svc
+            if ("image" in svc) == ("build" in svc) or ("image" in svc and has_build):
+                raise ComposeError("Service %s has neither an image nor a build context specified. At least one must be provided." % name)
+        # prune env files that do not exist
+        if cu.ENV_FILE in svc:
+            ef = svc[cu.ENV_FILE]
+            if isinstance(ef, str):
+                p = ef if os.path.isabs(ef) else os.path.join(base, ef)
+                if not os.path.isfile(p):
+                    log.warning("Unable to find env config file %s referred in service %s in file %s. Ignoring it.", p, name, path)
+                    del svc[cu.ENV_FILE]
+            elif isinstance(ef, list):
+                kept = []
+                for e in ef:
+                    p = e if os.path.isabs(e) else os.path.join(base, e)
+                    if os.path.isfile(p):
+                        kept.append(e)
+                    else:
+                        log.warning("Unable to find env config file %s referred in service %s in file %s. Ignoring it.", p, name, path)
+                svc[cu.ENV_FILE] = kept
+        services.append(_load_service(name, svc, base, version))
+    services.sort(key=lambda s: s["name"])
+    networks = {}
+    if version:
+        for nname, spec in (parsed.get("networks") or {}).items():
+            spec = spec or {}
+            ext = spec.get("external")
+            external = bool(ext) if not isinstance(ext, dict) else True
+            real = nname
+            if external and isinstance(ext, dict) and ext.get("name"):
+                real = ext["name"]
+            networks[nname] = {"external": external, "real": real}
+    return {"version": version, "project": _normalize_project_name(os.path.basename(base)),
+            "services": services, "networks": networks}
+
+
+def _resolve(p, base):
+    if p.startswith("~"):
+        p = os.path.expanduser("~") + p[1:]
+    if os.path.isabs(p):
+        return p
+    return os.path.normpath(os.path.join(base, p))
+
+
+def _is_url(s):
+    return re.match(r"^(https?://|git://|github\.com/|git@)", s) is not None
+
+
+def _load_service(name, d, base, version):
+    s = {"name": name}
+    b = d.get("build")
+    ctx, dockerfile = "", ""
+    if isinstance(b, str):
+        ctx = b
+    elif isinstance(b, dict):
+        ctx = _scalar_str(b.get("context") or "")
+        dockerfile = _scalar_str(b.get("dockerfile") or "")
+    if version == "" and d.get("dockerfile"):
+        dockerfile = _scalar_str(d.get("dockerfile"))
+    if ctx and not _is_url(ctx):
+        ctx = _resolve(ctx, base)
+    s["build_context"], s["build_dockerfile"] = ctx, dockerfile
+    s["image"] = _scalar_str(d.get("image") or "")
+    s["container_name"] = _scalar_str(d.get("container_name") or "")
+    for key in ("command", "entrypoint"):
+        v = d.get(key)
+        s[key] = cu.shell_split(v) if isinstance(v, str) else (_as_list_of_str(v) if v is not None else None)
+    env = d.get("environment")
+    if isinstance(env, dict):
+        s["environment"] = ["%s=%s" % (k, _scalar_str(v)) if v is not None else str(k) for k, v in env.items()]
+    else:
+        s["environment"] = _as_list_of_str(env)
+    s["working_dir"] = _scalar_str(d.get("working_dir") or "")
+    s["stdin_open"] = bool(d.get("stdin_open"))
+    s["tty"] = bool(d.get("tty"))
+    s["ports"] = _as_list_of_str(d.get("ports"))
+    s["expose"] = _as_list_of_str(d.get("expose"))
+    s["privileged"] = bool(d.get("privileged"))
+    s["user"] = _scalar_str(d.get("user") or "")
+    s["cap_add"] = _as_list_of_str(d.get("cap_add"))
+    s["cap_drop"] = _as_list_of_str(d.get("cap_drop"))
+    s["group_add"] = _as_list_of_str(d.get("group_add"))
+    s["stop_grace_period"] = _scalar_str(d.get("stop_grace_period") or "")
+    mem = d.get("mem_limit")
+    s["mem_limit"] = cu.ram_in_bytes(mem) if mem not in (None, "") else 0
+    s["restart"] = _scalar_str(d.get("restart") or "")
+    s["labels"] = _labels(d.get("labels"))
+    s["hostname"] = _scalar_str(d.get("hostname") or "")
+    s["domainname"] = _scalar_str(d.get("domainname") or "")
+    nets = d.get("networks")
+    s["networks"] = list(nets.keys()) if isinstance(nets, dict) else _as_list_of_str(nets)
+    s["tmpfs"] = _as_list_of_str(d.get("tmpfs"))
+    s["volumes_from"] = _as_list_of_str(d.get("volumes_from"))
+    vols = []
+    for v in d.get("volumes") or []:
+        spec = _scalar_str(v) if not isinstance(v, dict) else ""
+        parts = spec.split(":")
+        vol = {"source": "", "destination": "", "access_mode": ""}
+        if len(parts) == 1:
+            vol["destination"] = parts[0]
+        else:
+            vol["source"], vol["destination"] = parts[0], parts[1]
+            if len(parts) > 2:
+                vol["access_mode"] = parts[2]
+        src = vol["source"]
+        if src and src[0] in "./~":
+            vol["source"] = _resolve(src, base)
+        vols.append(vol)
+    s["volumes"] = vols
+    return s
+
+
+class V1V2Loader:
+    def convert_to_ir(self, composefilepath, plan, service):
+        proj = parse_v2(composefilepath)
+        return self._convert(os.path.dirname(composefilepath), proj, plan, service)
+
+    def _convert(self, filedir, proj, plan, service):
+        ir = irtypes.empty_ir()
+        for cs in proj["services"]:
+            name = cs["name"]
+            if name != service.service_name:
+                continue
+            sc = irtypes.new_service_with_name(common.normalize_for_service_name(name))
+            sc.annotations = dict(cs["labels"]) if cs["labels"] else None
+            if cs["hostname"]:
+                sc.pod_spec["hostname"] = cs["hostname"]
+            if cs["domainname"]:
+                sc.pod_spec["subdomain"] = cs["domainname"]
+            cont = {"image": cs["image"] or name + ":latest"}
+            if cs["build_dockerfile"] or cs["build_context"]:
+                try:
+                    ir.add_container(ReuseDockerfileContainerizer().get_container(plan, service))
+                except Exception as e:  # noqa: BLE001
+                    log.warning("Unable to get containization script even though build parameters are present : %s", e)
+            cname = cs["container_name"].lower()
+            if cname != cs["container_name"]:
+                log.debug("Container name in service %r has been changed from %r to %r", name, cs["container_name"], cname)
+            cont["name"] = cname or sc.name
+            if cs["entrypoint"] is not None:
+                cont["command"] = cs["entrypoint"]
+            if cs["command"] is not None:
+                cont["args"] = cs["command"]
+            env = self.get_envs(cs["environment"])
+            if env:
+                cont["env"] = env
+            if cs["working_dir"]:
+                cont["workingDir"] = cs["working_dir"]
+            if cs["stdin_open"]:
+                cont["stdin"] = True
+            if cs["tty"]:
+                cont["tty"] = True
+            cont["ports"] = self.get_ports(cs["ports"], cs["expose"])
+            self.add_ports(cs["ports"], cs["expose"], sc)
+            secctx = {}
+            if cs["privileged"]:
+                secctx["privileged"] = True
+            if cs["user"]:
+                try:
+                    secctx["runAsUser"] = common.cast_to_int(cs["user"])
+                except ValueError:
+                    log.warning("Ignoring user directive. User to be specified as a UID (numeric).")
+            if cs["cap_add"] or cs["cap_drop"]:
+                secctx["capabilities"] = {"add": list(cs["cap_add"]), "drop": list(cs["cap_drop"])}
+            if secctx:
+                cont["securityContext"] = secctx
+            # group_add goes to a pod security context the reference never attaches (kept for parity)
+            try:
+                [int(g) for g in cs["group_add"]]
+            except ValueError as e:
+                log.warning("GroupAdd should be in gid format, not as group name : %s", e)
+            if cs["stop_grace_period"]:
+                try:
+                    sc.pod_spec["terminationGracePeriodSeconds"] = int(cu.parse_duration(cs["stop_grace_period"]) // 10 ** 9)
+                except ValueError:
+                    log.warning("Failed to parse duration %s for service %s", cs["stop_grace_period"], name)
+            if cs["mem_limit"]:
+                cont["resources"] = {"limits": {"memory": cu.format_quantity_decimal_exponent(cs["mem_limit"])}}
+            if cs["restart"] == "unless-stopped":
+                log.warning("Restart policy 'unless-stopped' in service %s is not supported, convert it to 'always'", name)
+                sc.restart_policy = "Always"
+            for n in cs["networks"]:
+                if n != "default":
+                    net = proj["networks"].get(n)
+                    if net is None:
+                        real = proj["project"] + "_" + n
+                    elif net["external"]:
+                        real = net["real"]
+                    else:
+                        real = proj["project"] + "_" + n
+                    sc.networks.append(real)
+            vms, vols = cu.make_volumes_from_tmpfs(name, cs["tmpfs"])
+            for v in vols:
+                sc.add_volume(v)
+            mounts = list(vms)
+            if cs["volumes_from"]:
+                log.warning("Ignoring VolumeFrom in compose for service %s : %s", service.service_name, cs["volumes_from"])
+            for vol in cs["volumes"]:
+                ro = vol["access_mode"] == cu.MODE_READ_ONLY
+                if cu.is_path(vol["source"]):
+                    vname = "%s%d" % (VOLUME_PREFIX, cu.get_hash(vol["source"]))
+                    m = {"name": vname, "mountPath": vol["destination"]}
+                    if ro:
+                        m["readOnly"] = True
+                    mounts.append(m)
+                    sc.add_volume({"name": vname, "hostPath": {"path": vol["source"]}})
+                else:
+                    m = {"name": vol["source"], "mountPath": vol["destination"]}
+                    if ro:
+                        m["readOnly"] = True
+                    mounts.append(m)
+                    pvc = {"claimName": vol["source"]}
+                    if ro:
+                        pvc["readOnly"] = True
+                    sc.add_volume({"name": vol["source"], "persistentVolumeClaim": pvc})
+                    mode = "ReadOnlyMany" if ro else "ReadWriteMany"
+                    ir.add_storage(irtypes.Storage(name=vol["source"], storage_type=irtypes.PVC_KIND,
+                                                   pvc_spec={"accessModes": [mode]}))
+            if mounts:
+                cont["volumeMounts"] = mounts
+            sc.containers = [cont]
+            ir.services[name] = sc
+        return ir
+
+    @staticmethod
+    def get_envs(envars):
+        out = []
+        for e in envars:
+            m = re.search(r"[=:]", e)
+            if m is None:
+                out.append({"name": e, "value": "unknown"})
+            else:
+                out.append({"name": e[:m.start()], "value": e[m.start() + 1:]})
+        return out
+
+    @staticmethod
+    def parse_container_port(value):
+        proto = "TCP"
+        if "/" in value:
+            parts = value.split("/")
+            value = parts[0]
+            if parts[1].upper() == "UDP":
+                proto = "UDP"
+        if ":" not in value:
+            p = common.cast_to_int(value)
+            return p, p, proto
+        parts = value.split(":")
+        if len(parts) > 3:
+            raise ValueError("Failed to parse the port %s properly" % value)
+        sp, pp = parts[0], parts[1]
+        if len(parts) == 3:
+            sp, pp = parts[1], parts[2]
+        return common.cast_to_int(sp), common.cast_to_int(pp), proto
+
+    def get_ports(self, ports, expose):
+        out, exist = [], set()
+        for p in list(ports) + list(expose):
+            try:
+                _, pod, proto = self.parse_container_port(p)
+            except ValueError:
+                continue
+            if pod not in exist:
+                out.append({"containerPort": pod, "protocol": proto})
+                exist.add(pod)
+        return out
+
+    def add_ports(self, ports, expose, service):
+        exist = set()
+        for p in list(ports) + list(expose):
+            try:
+                sp, pp, _ = self.parse_container_port(p)
+            except ValueError:
+                continue
+            if sp not in exist:
+                service.add_port_forwarding(irtypes.Port(sp), irtypes.Port(pp))
+                exist.add(sp)

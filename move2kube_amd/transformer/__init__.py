@@ -1,0 +1,358 @@
+"""IR -> output artifacts (reference ``internal/transformer/``).
+
+* :class:`K8sTransformer` - Deployment/Service/Ingress/... YAMLs (or a Helm
+  chart + optional operator), converted to the first version the target
+  cluster supports; ``deploy.sh``/``NOTES.txt``/``Readme.md``.
+* :class:`KnativeTransformer` - knative Services.
+* :class:`ComposeTransformer` - a docker-compose v3.5 file.
+* :class:`CICDTransformer` - Tekton pipeline/trigger objects under ``cicd/``.
+
+``write_containers`` emits the new-image build scripts (reference
+``transformer.go:48-151``); ``write_transformed_objects`` serialises one file
+per object as ``<name>-<lowercase kind>.yaml`` through the typed-struct
+marshaller + go-yaml emitter (``transformer.go:153-200``).
+"""
+
+import os
+import shutil
+import subprocess
+
+from .. import assets
+from ..apiresource.base import GOTYPE
+from ..apiresourceset import K8sAPIResourceSet, KnativeAPIResourceSet, TektonAPIResourceSet
+from ..k8s import convert, schema
+from ..models import plan as plantypes
+from ..utils import common, log, yamlio
+from ..utils.constants import (DEFAULT_DIRECTORY_PERMISSION, DEFAULT_EXECUTABLE_PERMISSION, DEFAULT_FILE_PERMISSION,
+                               EXPOSE_SELECTOR, settings)
+
+HELM_TEMPLATES_REL_PATH = "templates"
+CONTAINERS_DIR = "containers"
+KNATIVE_GROUP = "serving.knative.dev"
+
+
+def _mkdir(p):
+    os.makedirs(p, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+
+
+def write_containers(containers, outpath, root_dir, registry_url, registry_namespace):
+    """Write new-container files and build/push scripts; True if any new image exists."""
+    cpath = os.path.join(outpath, CONTAINERS_DIR)
+    try:
+        _mkdir(cpath)
+    except OSError as e:
+        log.error("Unable to create directory %s : %s", cpath, e)
+    log.debug("Total number of containers : %d", len(containers))
+    buildscripts, dockerimages, manualimages = [], [], []
+    for c in containers:
+        if not c.new:
+            continue
+        if not c.new_files:
+            manualimages.extend(c.image_names)
+        log.debug("New Container : %s", c.image_names[0] if c.image_names else "")
+        dockerimages.extend(c.image_names)
+        for rel in sorted(c.new_files):
+            wp = os.path.join(cpath, rel)
+            try:
+                _mkdir(os.path.dirname(wp))
+            except OSError as e:
+                log.error("Unable to create directory %s : %s", os.path.dirname(wp), e)
+                continue
+            mode = DEFAULT_FILE_PERMISSION
+            if common.go_ext(wp) == ".sh":
+                mode = DEFAULT_EXECUTABLE_PERMISSION
+                buildscripts.append(os.path.join(CONTAINERS_DIR, rel))
+            try:
+                common.write_text(wp, c.new_files[rel], mode)
+            except OSError as e:
+                log.warning("Error writing file at %s : %s", wp, e)
+    if manualimages:
+        wp = os.path.join(outpath, "Manualimages.md")
+        if settings.fixed:
+            common.write_template_to_file(assets.template("manualimages.md.tpl"), {"Images": manualimages}, wp,
+                                          DEFAULT_FILE_PERMISSION)
+        else:
+            # the reference hands the template a struct without the field it ranges over,
+            # so template execution fails and no file is written
+            log.error("Unable to create manual image : template: manualimages:5:17: executing \"manualimages\" at "
+                      "<.Images>: can't evaluate field Images in type struct { Scripts []string }")
+    if buildscripts:
+        script_map = {}
+        for v in buildscripts:
+            d, f = os.path.split(v)
+            script_map[f] = d + "/" if d else ""
+        common.write_template_to_file(assets.template("buildimages.sh.tpl"), script_map,
+                                      os.path.join(outpath, "buildimages.sh"), DEFAULT_EXECUTABLE_PERMISSION)
+        try:
+            rel_root = common.go_rel(outpath, root_dir)
+        except ValueError as e:
+            log.error("Failed to make the root directory path %r relative to the output directory %r Error %r",
+                      root_dir, outpath, str(e))
+            rel_root = root_dir
+        common.write_template_to_file(assets.template("copysources.sh.tpl"), {"RelRootDir": rel_root, "Dst": CONTAINERS_DIR},
+                                      os.path.join(outpath, "copysources.sh"), DEFAULT_EXECUTABLE_PERMISSION)
+    if dockerimages:
+        common.write_template_to_file(assets.template("pushimages.sh.tpl"),
+                                      {"Images": dockerimages, "RegistryURL": registry_url,
+                                       "RegistryNamespace": registry_namespace},
+                                      os.path.join(outpath, "pushimages.sh"), DEFAULT_EXECUTABLE_PERMISSION)
+        return True
+    return False
+
+
+def serialize_object(obj):
+    """One object -> YAML text exactly as the reference writes it."""
+    clean = {k: v for k, v in obj.items() if k != GOTYPE}
+    return yamlio.dumps_k8s(schema.marshal(clean))
+
+
+def write_transformed_objects(path, objs):
+    written = []
+    try:
+        _mkdir(path)
+    except OSError as e:
+        log.error("Unable to create directory %s : %s", path, e)
+        raise
+    for obj in objs:
+        try:
+            data = serialize_object(obj)
+        except Exception as e:  # noqa: BLE001
+            log.error("Error while Encoding object : %s", e)
+            continue
+        name = (obj.get("metadata") or {}).get("name", "")
+        f = os.path.join(path, "%s-%s.yaml" % (name, obj.get("kind", "").lower()))
+        try:
+            common.write_text(f, data, DEFAULT_FILE_PERMISSION)
+        except OSError as e:
+            log.error("Failed to write %r Error: %r", obj.get("kind"), str(e))
+            continue
+        written.append(f)
+        log.debug("%r created", f)
+    return written
+
+
+class Transformer:
+    def transform(self, ir):
+        raise NotImplementedError
+
+    def write_objects(self, outpath):
+        raise NotImplementedError
+
+
+def get_transformer(ir):
+    if ir.kubernetes.artifact_type == plantypes.KNATIVE:
+        return KnativeTransformer()
+    return K8sTransformer()
+
+
+class K8sTransformer(Transformer):
+    def __init__(self):
+        self.root_dir = ""
+        self.transformed_objects = []
+        self.containers = []
+        self.values = None
+        self.target_cluster_spec = None
+        self.helm = False
+        self.name = ""
+        self.ignore_unsupported_kinds = False  # never set by the reference's Transform
+        self.exposed_service_paths = {}
+        self.add_copy_sources_warning = False
+
+    def transform(self, ir):
+        log.debug("Starting Kubernetes transform")
+        log.debug("Total services to be transformed : %d", len(ir.services))
+        self.name = ir.name
+        self.values = ir.values
+        self.containers = ir.containers
+        self.target_cluster_spec = ir.target_cluster_spec
+        self.helm = ir.kubernetes.artifact_type == plantypes.HELM
+        if settings.fixed:
+            self.ignore_unsupported_kinds = ir.kubernetes.ignore_unsupported_kinds
+        self.transformed_objects = K8sAPIResourceSet().create_api_resources(ir)
+        self.root_dir = ir.root_dir
+        self.add_copy_sources_warning = ir.add_copy_sources_warning
+        for s in ir.sorted_services():
+            if s.has_valid_annotation(EXPOSE_SELECTOR):
+                self.exposed_service_paths[s.name] = s.service_rel_path
+        log.debug("Total transformed objects : %d", len(self.transformed_objects))
+
+    def convert_objects(self):
+        objs = []
+        for obj in self.transformed_objects:
+            kind = obj.get("kind", "")
+            versions = self.target_cluster_spec.get_supported_versions(kind)
+            version = obj.get("apiVersion", "")
+            if versions is None:
+                if self.ignore_unsupported_kinds:
+                    log.error("Kind %s unsupported in target cluster. Will ignore object.", kind)
+                    continue
+            elif kind == "Service":
+                for v in versions:
+                    if not v.startswith(KNATIVE_GROUP):
+                        version = v
+            else:
+                version = versions[0]
+            try:
+                obj = convert.convert_to_version(obj, version)
+            except convert.ConversionError as e:
+                log.error("Error while transforming version : %s. Writing in original version.", e)
+            objs.append(obj)
+        return objs
+
+    def write_objects(self, outpath):
+        new_images = write_containers(self.containers, outpath, self.root_dir, self.values.registry_url,
+                                      self.values.registry_namespace)
+        artifacts = os.path.join(outpath, self.name)
+        if self.helm:
+            try:
+                self.generate_helm_metadata(artifacts)
+            except OSError as e:
+                log.debug("Failed to generate helm metadata properly, continuing anyway. Error: %r", str(e))
+            artifacts = os.path.join(artifacts, HELM_TEMPLATES_REL_PATH)
+        log.debug("Total services to be serialized : %d", len(self.transformed_objects))
+        try:
+            write_transformed_objects(artifacts, self.convert_objects())
+        except OSError as e:
+            log.error("Error occurred while writing transformed objects %s", e)
+        if self.helm:
+            self.create_operator(self.name, outpath)
+        else:
+            self.write_deploy_script(self.name, outpath)
+        self.write_readme(self.name, new_images, self.helm, self.add_copy_sources_warning, outpath)
+
+    def generate_helm_metadata(self, d):
+        _mkdir(d)
+        common.write_text(os.path.join(d, "README.md"), "This chart was created by Move2Kube\n")
+        base = common.go_base(d)
+        common.write_template_to_file(assets.template("chart.yaml.tpl"), {"Name": base}, os.path.join(d, "Chart.yaml"),
+                                      DEFAULT_FILE_PERMISSION)
+        _mkdir(os.path.join(d, HELM_TEMPLATES_REL_PATH))
+        notes = common.get_string_from_template(assets.template("notes.txt.tpl"),
+                                                {"IsHelm": True, "ExposedServicePaths": self.exposed_service_paths})
+        common.write_text(os.path.join(d, HELM_TEMPLATES_REL_PATH, "NOTES.txt"), assets.template("helmnotes.txt") + notes)
+        common.write_yaml(os.path.join(d, "values.yaml"), self.values)
+        common.write_template_to_file(assets.template("helminstall.sh.tpl"), {"Project": base},
+                                      os.path.join(os.path.dirname(d), "helminstall.sh"), DEFAULT_EXECUTABLE_PERMISSION)
+
+    @staticmethod
+    def create_operator(project, basepath):
+        sdk = shutil.which("operator-sdk")
+        if sdk is None:
+            log.warning("Unable to find operator-sdk. Skipping operator generation : exec: \"operator-sdk\": "
+                        "executable file not found in $PATH")
+            return False
+        opath = os.path.join(basepath, project + "-operator")
+        if os.path.exists(opath):
+            shutil.rmtree(opath, ignore_errors=True)
+        _mkdir(opath)
+        chart = os.path.abspath(os.path.join(basepath, project))
+        p = subprocess.run([sdk, "init", "--plugins=helm", "--helm-chart=" + chart, "--domain=io", "--group=" + project,
+                            "--version=v1alpha1"], cwd=opath, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           stdin=subprocess.DEVNULL)
+        if p.returncode != 0:
+            log.warning("Error during operator creation : exit status %d, %s", p.returncode, p.stdout.decode("utf-8", "replace"))
+            return False
+        return True
+
+    def write_deploy_script(self, proj, outpath):
+        common.write_template_to_file(assets.template("deploy.sh.tpl"), {"Project": proj},
+                                      os.path.join(outpath, "deploy.sh"), DEFAULT_EXECUTABLE_PERMISSION)
+        common.write_template_to_file(assets.template("notes.txt.tpl"),
+                                      {"IsHelm": False, "IngressHost": self.target_cluster_spec.host,
+                                       "ExposedServicePaths": self.exposed_service_paths},
+                                      os.path.join(outpath, "NOTES.txt"), DEFAULT_FILE_PERMISSION)
+
+    @staticmethod
+    def write_readme(project, new_images, helm, warn, outpath):
+        common.write_template_to_file(assets.template("k8sreadme.md.tpl"),
+                                      {"Project": project, "NewImages": new_images, "Helm": helm,
+                                       "AddCopySourcesWarning": warn},
+                                      os.path.join(outpath, "Readme.md"), DEFAULT_FILE_PERMISSION)
+
+
+class KnativeTransformer(Transformer):
+    def __init__(self):
+        self.transformed_objects = []
+        self.name = ""
+
+    def transform(self, ir):
+        log.debug("Starting Knative transform")
+        self.name = ir.name
+        self.values = ir.values
+        self.containers = ir.containers
+        self.target_cluster_spec = ir.target_cluster_spec
+        self.ignore_unsupported_kinds = ir.kubernetes.ignore_unsupported_kinds
+        self.transformed_objects = KnativeAPIResourceSet().create_api_resources(ir)
+        self.root_dir = ir.root_dir
+
+    def write_objects(self, outpath):
+        new_images = write_containers(self.containers, outpath, self.root_dir, self.values.registry_url,
+                                      self.values.registry_namespace)
+        try:
+            write_transformed_objects(os.path.join(outpath, self.name), self.transformed_objects)
+        except OSError as e:
+            log.error("Error occurred while writing transformed objects %s", e)
+        common.write_template_to_file(assets.template("deploy.sh.tpl"), {"Project": self.name},
+                                      os.path.join(outpath, "deploy.sh"), DEFAULT_EXECUTABLE_PERMISSION)
+        common.write_template_to_file(assets.template("knativereadme.md.tpl"),
+                                      {"Project": self.name, "NewImages": new_images},
+                                      os.path.join(outpath, "Readme.md"), DEFAULT_FILE_PERMISSION)
+
+
+class ComposeTransformer(Transformer):
+    """docker-compose v3.5 output: one entry per service (last container wins),
+    published ports allocated from 8080 upwards."""
+
+    def transform(self, ir):
+        log.debug("Starting Compose transform")
+        self.name = ir.name
+        self.containers = ir.containers
+        services = {}
+        exposed = 8080
+        for s in ir.sorted_services():
+            for c in s.containers:
+                ports = []
+                for p in c.get("ports") or []:
+                    pc = {}
+                    if p.get("containerPort"):
+                        pc["target"] = p["containerPort"]
+                    pc["published"] = exposed
+                    ports.append(pc)
+                    exposed += 1
+                env = {}
+                envs = c.get("env") or []
+                for e in envs:
+                    env[e.get("name", "")] = e.get("value", "")
+                if envs and not settings.fixed:
+                    # `&e.Value` of the shared range variable: every entry ends up pointing
+                    # at the last value (go<1.22 loop semantics)
+                    last = envs[-1].get("value", "")
+                    env = {k: last for k in env}
+                svc = {}
+                if c.get("name"):
+                    svc["container_name"] = c["name"]
+                if env:
+                    svc["environment"] = yamlio.GoMap(env)
+                if c.get("image"):
+                    svc["image"] = c["image"]
+                if ports:
+                    svc["ports"] = ports
+                services[s.name] = svc
+        self.compose = {"version": "3.5", "services": yamlio.GoMap(services)} if services else {"version": "3.5"}
+
+    def write_objects(self, outpath):
+        _mkdir(outpath)
+        common.write_yaml(os.path.join(outpath, "docker-compose.yaml"), self.compose)
+
+
+class CICDTransformer(Transformer):
+    def transform(self, ir):
+        self.cached_objs = TektonAPIResourceSet().create_api_resources(ir)
+
+    def write_objects(self, outpath):
+        p = os.path.join(outpath, "cicd")
+        try:
+            _mkdir(p)
+        except OSError as e:
+            log.fatal("Failed to create the CI/CD directory at path %r. Error: %r", p, str(e))
+        write_transformed_objects(p, self.cached_objs)

@@ -1,0 +1,450 @@
+"""Common helpers (reference ``internal/common/utils.go:47-718``).
+
+File-system discovery goes through :mod:`move2kube_amd.utils.fsindex` (one
+indexed walk shared by every planner instead of the reference's >=8 serial
+``filepath.Walk`` passes); the hashing/naming primitives are bit-exact with
+the reference (CRC-64/ECMA, FNV-64a, SHA-256 truncation).
+"""
+
+import hashlib
+import json
+import os
+import re
+import shutil
+
+from . import log, yamlio
+from .constants import (DEFAULT_FILE_PERMISSION, GROUP_NAME, SCHEME_VERSION)
+
+# ---------------------------------------------------------------------------
+# hashing primitives (native when available; pure-python fallback is exact)
+# ---------------------------------------------------------------------------
+
+_CRC64_ECMA_POLY = 0xC96C5795D7870F42
+_CRC_TABLE = None
+
+
+def _crc64_table():
+    global _CRC_TABLE
+    if _CRC_TABLE is None:
+        tbl = []
+        for i in range(256):
+            crc = i
+            for _ in range(8):
+                crc = (crc >> 1) ^ _CRC64_ECMA_POLY if crc & 1 else crc >> 1
+            tbl.append(crc)
+        _CRC_TABLE = tbl
+    return _CRC_TABLE
+
+
+def crc64_ecma_py(data):
+    """Go ``crc64.Checksum(data, crc64.MakeTable(0xC96C5795D7870F42))``."""
+    tbl = _crc64_table()
+    crc = 0xFFFFFFFFFFFFFFFF
+    for b in data:
+        crc = tbl[(crc ^ b) & 0xFF] ^ (crc >> 8)
+    return crc ^ 0xFFFFFFFFFFFFFFFF
+
+
+def fnv64a_py(data):
+    """Go ``hash/fnv`` New64a over ``data``."""
+    h = 0xCBF29CE484222325
+    for b in data:
+        h ^= b
+        h = (h * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def crc64_ecma(data):
+    from ..ops import native
+    if isinstance(data, str):
+        data = data.encode()
+    return native.crc64_ecma(data)
+
+
+def fnv64a(data):
+    from ..ops import native
+    if isinstance(data, str):
+        data = data.encode()
+    return native.fnv64a(data)
+
+
+def get_sha256_hash(s):
+    return hashlib.sha256(s.encode()).hexdigest()
+
+
+# ---------------------------------------------------------------------------
+# file discovery
+# ---------------------------------------------------------------------------
+
+def get_files_by_ext(input_path, exts):
+    """Files under ``input_path`` whose extension is in ``exts`` (lexical walk order).
+
+    Raises FileNotFoundError if ``input_path`` does not exist (reference returns an error)."""
+    from .fsindex import get_index
+    return get_index(input_path).files_by_ext(exts)
+
+
+def get_files_by_name(input_path, names):
+    from .fsindex import get_index
+    return get_index(input_path).files_by_name(names)
+
+
+# ---------------------------------------------------------------------------
+# YAML / JSON IO
+# ---------------------------------------------------------------------------
+
+def read_text(path):
+    with open(path, "rb") as f:
+        return f.read().decode("utf-8", errors="surrogateescape")
+
+
+def write_text(path, text, mode=DEFAULT_FILE_PERMISSION):
+    data = text.encode("utf-8", errors="surrogateescape") if isinstance(text, str) else text
+    with open(path, "wb") as f:
+        f.write(data)
+    try:
+        os.chmod(path, mode)
+    except OSError:
+        pass
+
+
+def yaml_attr_present(path, attr):
+    try:
+        data = yamlio.load(read_text(path))
+    except (OSError, yamlio.YAMLError) as e:
+        log.warning("Error in reading/unmarshalling yaml file %s: %s. Skipping", path, e)
+        return False, None
+    if isinstance(data, dict) and attr in data:
+        return True, data[attr]
+    return False, None
+
+
+def write_yaml(output_path, data, sort_maps=False):
+    """Write ``data`` (a plain structure or an object with ``to_yaml()``) like go-yaml v3."""
+    if hasattr(data, "to_yaml"):
+        data = data.to_yaml()
+    write_text(output_path, yamlio.dump(data, sort_maps=sort_maps))
+
+
+def read_yaml(path):
+    return yamlio.load(read_text(path))
+
+
+def parse_group_version(gv):
+    """k8s ``schema.ParseGroupVersion``."""
+    if gv == "" or gv == "/":
+        return "", ""
+    parts = gv.split("/")
+    if len(parts) == 1:
+        return "", parts[0]
+    if len(parts) == 2:
+        return parts[0], parts[1]
+    raise ValueError("unexpected GroupVersion string: %s" % gv)
+
+
+class Move2KubeYamlError(ValueError):
+    pass
+
+
+def read_move2kube_yaml(path, raw=True):
+    """Read a move2kube-group YAML (plan, cache, cluster metadata ...).
+
+    Checks that ``apiVersion``'s group is ``move2kube.konveyor.io`` and warns on a
+    version mismatch (``internal/common/utils.go:210-251``).  Returns the decoded
+    document (scalars kept as raw strings when ``raw``)."""
+    text = read_text(path)
+    data = yamlio.load(text)
+    if not isinstance(data, dict):
+        raise Move2KubeYamlError("The file at path %s is not a yaml mapping" % path)
+    gv = data.get("apiVersion")
+    if gv is None:
+        raise Move2KubeYamlError("Did not find apiVersion in the yaml file at path %s" % path)
+    if not isinstance(gv, str):
+        raise Move2KubeYamlError("The apiVersion is not a string in the yaml file at path %s" % path)
+    try:
+        group, version = parse_group_version(gv)
+    except ValueError as e:
+        raise Move2KubeYamlError(str(e))
+    if group != GROUP_NAME:
+        raise Move2KubeYamlError("The file at path %s doesn't have the correct group. Expected group %s Actual group %s"
+                                 % (path, GROUP_NAME, group))
+    if version != SCHEME_VERSION:
+        log.warning("The file at path %s was generated using a different version. File version is %s and move2kube version is %s",
+                    path, version, SCHEME_VERSION)
+    return yamlio.load_raw(text) if raw else data
+
+
+def write_json(output_path, data):
+    write_text(output_path, json.dumps(data, separators=(",", ":")) + "\n")
+
+
+def read_json(path):
+    with open(path) as f:
+        return json.load(f)
+
+
+# ---------------------------------------------------------------------------
+# naming
+# ---------------------------------------------------------------------------
+
+def get_image_name_and_tag(image):
+    parts = image.split("/")
+    it = parts[-1].split(":")
+    name = it[0]
+    tag = "latest" if len(it) == 1 else it[1]
+    return name, tag
+
+
+def normalize_for_filename(name):
+    processed = make_file_name_compliant(name)
+    if len(processed) > 15:
+        processed = processed[:15]
+    return processed + "-" + format(crc64_ecma(name.encode()), "x")
+
+
+_SVC_RE = re.compile(r"[._]")
+
+
+def normalize_for_service_name(svc_name):
+    new = _SVC_RE.sub("-", svc_name).lower()
+    if new != svc_name:
+        log.info("Changing service name to %s from %s", svc_name, new)
+    return new
+
+
+def is_string_present(lst, value):
+    """Case-insensitive membership (Go ``strings.EqualFold``)."""
+    if not lst:
+        return False
+    v = value.casefold()
+    for x in lst:
+        if x == value or x.casefold() == v:
+            return True
+    return False
+
+
+def is_int_present(lst, value):
+    return value in (lst or [])
+
+
+def merge_string_slices(a, b):
+    a = list(a or [])
+    for item in b or []:
+        if not is_string_present(a, item):
+            a.append(item)
+    return a
+
+
+def merge_int_slices(a, b):
+    a = list(a or [])
+    for item in b or []:
+        if item not in a:
+            a.append(item)
+    return a
+
+
+def merge_string_maps(a, b):
+    out = dict(a or {})
+    out.update(b or {})
+    return out
+
+
+def get_string_from_template(tpl, config):
+    from .gotemplate import render
+    return render(tpl, config)
+
+
+def write_template_to_file(tpl, config, write_path, mode):
+    write_text(write_path, get_string_from_template(tpl, config), mode)
+
+
+_TOKEN_RE = re.compile(r"[^a-zA-Z0-9]+")
+
+
+def get_closest_matching_string(options, search):
+    """Option with least Wagner-Fischer distance (ins=1, del=1, sub=2) to ``search``
+    after stripping non-alphanumerics and lower-casing (``utils.go:377-401``)."""
+    from ..ops import editdistance
+    if not options:
+        return ""
+    s = _TOKEN_RE.sub("", search).lower()
+    toks = [_TOKEN_RE.sub("", o).lower() for o in options]
+    dists = editdistance.distances(toks, s)
+    best, best_d = "", 2 ** 31 - 1
+    for o, d in zip(options, dists):
+        if d < best_d:
+            best, best_d = o, d
+    return best
+
+
+_FILENAME_INVALID = re.compile(r"[^a-zA-Z0-9\-.]+")
+
+
+def make_file_name_compliant(name):
+    if not name:
+        log.error("The input name is empty.")
+        return ""
+    base = os.path.basename(name.rstrip("/")) or "/"
+    processed = _FILENAME_INVALID.sub("-", base)
+    if len(processed) > 63:
+        log.debug("Warning: The processed name %r is longer than 63 characters long.", processed)
+    return processed
+
+
+_DNS_INVALID = re.compile(r"[^a-z0-9\-.]")
+
+
+def make_string_dns_name_compliant(s):
+    name = _DNS_INVALID.sub("-", s.lower())
+    if name and (name[0] in "-." or name[-1] in "-."):
+        log.warning("The first and/or last characters of the string %r are not alphanumeric.", s)
+    return name
+
+
+def make_string_dns_subdomain_name_compliant(s):
+    name = s
+    if len(name) > 253:
+        h = get_sha256_hash(name)
+        name = name[:253 - 65] + "-" + h
+    return make_string_dns_name_compliant(name)
+
+
+def make_string_dns_label_name_compliant(s):
+    name = s
+    if len(name) > 63:
+        h = get_sha256_hash(name)[:32]
+        name = name[:63 - 33] + "-" + h
+    return make_string_dns_name_compliant(name)
+
+
+def clean_and_find_common_directory(paths):
+    return find_common_directory([os.path.normpath(p) if p else "." for p in paths])
+
+
+def find_common_directory(paths):
+    if not paths:
+        return ""
+    common = paths[0]
+    while common != "/":
+        if all((p + "/").startswith(common + "/") for p in paths):
+            break
+        nxt = go_dir(common)
+        if nxt == common:  # relative paths bottom out at "." (the reference would spin here)
+            break
+        common = nxt
+    return common
+
+
+def copy_file(dst, src):
+    shutil.copyfile(src, dst)
+    os.chmod(dst, DEFAULT_FILE_PERMISSION)
+
+
+def unique_strings(xs):
+    seen = set()
+    out = []
+    for x in xs:
+        if x not in seen:
+            seen.add(x)
+            out.append(x)
+    return out
+
+
+def go_rel(base, target):
+    """Go ``filepath.Rel`` (lexical; error if one is absolute and the other is not)."""
+    if os.path.isabs(base) != os.path.isabs(target):
+        raise ValueError("Rel: can't make %s relative to %s" % (target, base))
+    return os.path.relpath(os.path.normpath(target), os.path.normpath(base))
+
+
+def go_join(*parts):
+    """Go ``filepath.Join``: joins non-empty parts and cleans (an absolute later part
+    does NOT reset the path, unlike os.path.join)."""
+    ps = [p for p in parts if p]
+    if not ps:
+        return ""
+    return os.path.normpath("/".join(ps)).replace("//", "/")
+
+
+def go_clean(p):
+    if p == "":
+        return "."
+    c = os.path.normpath(p)
+    if c.startswith("//"):
+        c = "/" + c.lstrip("/")
+    return c
+
+
+def go_ext(p):
+    """Go ``filepath.Ext``: suffix from the final dot in the final element."""
+    base = p.rsplit("/", 1)[-1]
+    i = base.rfind(".")
+    return base[i:] if i >= 0 else ""
+
+
+def go_base(p):
+    if p == "":
+        return "."
+    p = p.rstrip("/")
+    if p == "":
+        return "/"
+    return p.rsplit("/", 1)[-1]
+
+
+def go_dir(p):
+    d = os.path.dirname(p)
+    return go_clean(d) if d else "."
+
+
+def cast_to_bool(s):
+    """spf13/cast ToBoolE for strings (strconv.ParseBool)."""
+    if isinstance(s, bool):
+        return s
+    if isinstance(s, (int, float)):
+        return s != 0
+    t = str(s)
+    if t in ("1", "t", "T", "TRUE", "true", "True"):
+        return True
+    if t in ("0", "f", "F", "FALSE", "false", "False"):
+        return False
+    raise ValueError("strconv.ParseBool: parsing %r: invalid syntax" % t)
+
+
+def cast_to_int(s):
+    """spf13/cast ToIntE (base-0 parsing for strings)."""
+    if isinstance(s, bool):
+        return int(s)
+    if isinstance(s, int):
+        return s
+    if isinstance(s, float):
+        return int(s)
+    t = str(s).strip()
+    try:
+        return int(t, 0)
+    except ValueError:
+        if re.match(r"^[-+]?0\d+$", t):
+            return int(t, 8)
+        raise ValueError("unable to cast %r of type string to int" % t)
+
+
+def go_bool_str(b):
+    return "true" if b else "false"
+
+
+def get_closest_matching_strings(options, searches):
+    """Batched :func:`get_closest_matching_string`: one all-pairs distance matrix
+    (GPU-offloaded when large) instead of len(searches) separate scans."""
+    from ..ops import editdistance
+    if not options or not searches:
+        return [""] * len(searches)
+    toks = [_TOKEN_RE.sub("", o).lower() for o in options]
+    qs = [_TOKEN_RE.sub("", s).lower() for s in searches]
+    m = editdistance.matrix(toks, qs)
+    out = []
+    for j in range(len(qs)):
+        best, best_d = "", 2 ** 31 - 1
+        for i, o in enumerate(options):
+            if m[i][j] < best_d:
+                best, best_d = o, m[i][j]
+        out.append(best)
+    return out

@@ -1,0 +1,57 @@
+"""Global constants and mutable process-wide settings.
+
+Mirrors the reference's ``internal/common/constants.go:27-73`` and
+``types/types.go:23-52``.  The mutable settings (``IGNORE_ENVIRONMENT``,
+``TEMP_PATH``, ``ASSETS_PATH``) live on the :data:`settings` object so that
+every module sees the same values after the CLI (or a test) changes them.
+"""
+
+import os
+
+APP_NAME = "move2kube"
+APP_NAME_SHORT = "m2k"
+GROUP_NAME = APP_NAME + ".konveyor.io"
+SCHEME_VERSION = "v1alpha1"
+SCHEME_GROUP_VERSION = GROUP_NAME + "/" + SCHEME_VERSION
+
+DEFAULT_PROJECT_NAME = "myproject"
+DEFAULT_PLAN_FILE = APP_NAME_SHORT + ".plan"
+TEMP_DIR_PREFIX = APP_NAME_SHORT + "-"
+ASSETS_DIR = APP_NAME_SHORT + "assets"
+VOLUME_PREFIX = "vol"
+DEFAULT_STORAGE_CLASS_NAME = "default"
+DEFAULT_DIRECTORY_PERMISSION = 0o755
+DEFAULT_EXECUTABLE_PERMISSION = 0o744
+DEFAULT_FILE_PERMISSION = 0o644
+DEFAULT_REGISTRY_URL = "docker.io"
+IMAGE_PULL_SECRET_PREFIX = "imagepullsecret"
+QA_CACHE_FILE = APP_NAME_SHORT + "qacache.yaml"
+DEFAULT_CLUSTER_TYPE = "Kubernetes"
+IGNORE_FILENAME = "." + APP_NAME_SHORT + "ignore"
+EXPOSE_SELECTOR = GROUP_NAME + "/service.expose"
+ANNOTATION_LABEL_VALUE = "true"
+DEFAULT_SERVICE_PORT = 8080
+DEFAULT_PVC_SIZE = "100Mi"
+
+
+class _Settings:
+    """Process-wide mutable configuration (the reference's package globals)."""
+
+    def __init__(self):
+        self.ignore_environment = False
+        self.temp_path = TEMP_DIR_PREFIX + "temp"
+        self.assets_path = os.path.join(self.temp_path, ASSETS_DIR)
+        # Behaviour switch for output-affecting quirks of the reference
+        # (SURVEY.md section 2.13).  "reference" keeps byte-compatible output,
+        # "fixed" applies the documented bug fixes.  Crash/hang bugs are always
+        # fixed regardless of this switch.
+        self.compat = os.environ.get("M2K_COMPAT", "reference")
+        # Number of parallel workers used for detector scripts and file sniffing.
+        self.workers = int(os.environ.get("M2K_WORKERS", "0") or 0) or min(32, (os.cpu_count() or 4))
+
+    @property
+    def fixed(self):
+        return self.compat == "fixed"
+
+
+settings = _Settings()

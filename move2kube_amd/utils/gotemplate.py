@@ -1,0 +1,882 @@
+"""A Go ``text/template`` interpreter (the subset the reference relies on).
+
+Go templates are part of the reference's user-facing extension ABI: the
+Dockerfile/S2I detector directories carry ``Dockerfile`` and
+``.s2i/environment`` templates rendered with the JSON a detect script prints
+(``internal/containerizer/dockerfilecontainerizer.go:134``,
+``s2icontainerizer.go:160``), and every output script/readme is a Go
+template (``internal/transformer/templates/*``).  Users who wrote custom
+detectors for the reference must be able to reuse them unchanged, so this is
+a faithful interpreter, not a Jinja translation.
+
+Supported: text/actions with ``{{-``/``-}}`` trimming, comments, ``if`` /
+``else if`` / ``else`` / ``with`` / ``range`` (with ``$k, $v :=``) /
+``define`` / ``template`` / ``block`` / ``break`` / ``continue``, variables
+and assignment, field chains on maps and objects, pipelines, parenthesised
+pipelines, literals, and the builtin functions (and, or, not, len, index,
+slice, print, printf, println, eq, ne, lt, le, gt, ge, html, js, urlquery,
+call).  Values print with Go ``fmt`` ``%v`` semantics.
+"""
+
+import html as _html
+import json
+import math
+import re
+import urllib.parse
+
+from .yamlio import go_format_float
+
+
+class TemplateError(Exception):
+    pass
+
+
+class _NoValue:
+    """The zero reflect.Value (a missing map key): prints ``<no value>``."""
+
+    def __repr__(self):
+        return "<no value>"
+
+    def __bool__(self):
+        return False
+
+
+NO_VALUE = _NoValue()
+
+
+# ---------------------------------------------------------------------------
+# Formatting (fmt %v)
+# ---------------------------------------------------------------------------
+
+def go_sprint(v, top=True):
+    if v is NO_VALUE:
+        return "<no value>"
+    if v is None:
+        return "<nil>"
+    if v is True:
+        return "true"
+    if v is False:
+        return "false"
+    if isinstance(v, int):
+        return str(v)
+    if isinstance(v, float):
+        if math.isinf(v):
+            return "+Inf" if v > 0 else "-Inf"
+        if math.isnan(v):
+            return "NaN"
+        return go_format_float(v)
+    if isinstance(v, str):
+        return v
+    if isinstance(v, bytes):
+        return "[" + " ".join(str(b) for b in v) + "]"
+    if isinstance(v, dict):
+        items = []
+        for k in sorted(v.keys(), key=_sort_key):
+            items.append("%s:%s" % (go_sprint(k, False), go_sprint(v[k], False)))
+        return "map[" + " ".join(items) + "]"
+    if isinstance(v, (list, tuple)):
+        return "[" + " ".join(go_sprint(x, False) for x in v) + "]"
+    if hasattr(v, "__dict__"):
+        return "{" + " ".join(go_sprint(x, False) for x in vars(v).values()) + "}"
+    return str(v)
+
+
+def _sort_key(k):
+    if isinstance(k, (int, float)) and not isinstance(k, bool):
+        return (0, k, "")
+    return (1, 0, str(k))
+
+
+def _truth(v):
+    if v is NO_VALUE or v is None:
+        return False
+    if isinstance(v, bool):
+        return v
+    if isinstance(v, (int, float)):
+        return v != 0
+    if isinstance(v, (str, bytes, list, tuple, dict)):
+        return len(v) > 0
+    return True
+
+
+def go_sprintf(fmt, args):
+    out = []
+    i = 0
+    ai = 0
+    n = len(fmt)
+    while i < n:
+        c = fmt[i]
+        if c != "%":
+            out.append(c)
+            i += 1
+            continue
+        i += 1
+        if i >= n:
+            out.append("%!(NOVERB)")
+            break
+        flags = ""
+        while i < n and fmt[i] in "+-# 0":
+            flags += fmt[i]
+            i += 1
+        width = ""
+        while i < n and fmt[i].isdigit():
+            width += fmt[i]
+            i += 1
+        prec = None
+        if i < n and fmt[i] == ".":
+            i += 1
+            prec = ""
+            while i < n and fmt[i].isdigit():
+                prec += fmt[i]
+                i += 1
+        if i >= n:
+            break
+        verb = fmt[i]
+        i += 1
+        if verb == "%":
+            out.append("%")
+            continue
+        if ai >= len(args):
+            out.append("%!" + verb + "(MISSING)")
+            continue
+        a = args[ai]
+        ai += 1
+        if verb in "vs":
+            s = go_sprint(a)
+            if prec:
+                s = s[:int(prec)]
+        elif verb == "q":
+            s = json.dumps(go_sprint(a)) if not isinstance(a, int) else "'%s'" % chr(a)
+        elif verb == "d":
+            s = str(int(a)) if isinstance(a, (int, float)) else "%!d(" + go_sprint(a) + ")"
+        elif verb in "xX":
+            if isinstance(a, int):
+                s = format(a, verb)
+            else:
+                s = go_sprint(a).encode().hex()
+                if verb == "X":
+                    s = s.upper()
+        elif verb in "feEgG":
+            p = int(prec) if prec else 6
+            if verb == "g":
+                s = go_format_float(float(a)) if prec is None else ("%." + str(p) + "g") % a
+            else:
+                s = ("%." + str(p) + verb) % a
+        elif verb == "t":
+            s = go_sprint(bool(a))
+        elif verb == "T":
+            s = type(a).__name__
+        else:
+            s = go_sprint(a)
+        if width:
+            w = int(width)
+            if "-" in flags:
+                s = s.ljust(w)
+            elif "0" in flags and verb in "dxXfeEgG":
+                s = s.rjust(w, "0")
+            else:
+                s = s.rjust(w)
+        out.append(s)
+    if ai < len(args):
+        out.append("%!(EXTRA " + ", ".join(go_sprint(a) for a in args[ai:]) + ")")
+    return "".join(out)
+
+
+# ---------------------------------------------------------------------------
+# Lexer
+# ---------------------------------------------------------------------------
+
+_TOKEN_RE = re.compile(r"""
+    (?P<ws>\s+)
+  | (?P<comment>/\*.*?\*/)
+  | (?P<str>"(?:[^"\\]|\\.)*")
+  | (?P<raw>`[^`]*`)
+  | (?P<char>'(?:[^'\\]|\\.)+')
+  | (?P<decl>:=)
+  | (?P<assign>=)
+  | (?P<pipe>\|)
+  | (?P<lparen>\()
+  | (?P<rparen>\))
+  | (?P<comma>,)
+  | (?P<var>\$[A-Za-z0-9_]*)
+  | (?P<field>(?:\.[A-Za-z_][A-Za-z0-9_]*)+)
+  | (?P<dot>\.)
+  | (?P<num>[-+]?(?:0[xX][0-9a-fA-F_]+|0[bB][01_]+|0[oO][0-7_]+|(?:\d[\d_]*)?\.?\d[\d_]*(?:[eE][-+]?\d+)?)i?)
+  | (?P<ident>[A-Za-z_][A-Za-z0-9_]*)
+""", re.S | re.X)
+
+
+def _lex_action(src, pos, right_delim):
+    """Tokenise an action starting at pos; returns (tokens, end_pos_after_delim, trim_right)."""
+    toks = []
+    n = len(src)
+    while True:
+        if pos >= n:
+            raise TemplateError("unclosed action")
+        # closing delimiter (optionally with trim marker)
+        if src.startswith(" -" + right_delim, pos) or (src.startswith("-" + right_delim, pos) and pos > 0 and src[pos - 1].isspace()):
+            off = 2 if src[pos] == " " else 1
+            return toks, pos + off + len(right_delim), True
+        if src.startswith(right_delim, pos):
+            return toks, pos + len(right_delim), False
+        m = _TOKEN_RE.match(src, pos)
+        if not m:
+            raise TemplateError("unexpected %r in action" % src[pos:pos + 10])
+        kind = m.lastgroup
+        text = m.group(kind)
+        pos = m.end()
+        if kind == "ws":
+            continue
+        # a field chain directly after a closing paren or variable: (x).Field, $x.Field
+        if kind == "field" and toks and toks[-1][0] in ("rparen", "var") and src[m.start()] == ".":
+            if toks[-1][0] == "var":
+                toks[-1] = ("var", toks[-1][1] + text)
+            else:
+                toks.append(("chain", text))
+            continue
+        if kind == "var" and pos < n and src[pos] == ".":
+            # $x.Field.Sub
+            m2 = re.compile(r"(?:\.[A-Za-z_][A-Za-z0-9_]*)+").match(src, pos)
+            if m2:
+                text += m2.group(0)
+                pos = m2.end()
+        toks.append((kind, text))
+
+
+# ---------------------------------------------------------------------------
+# AST
+# ---------------------------------------------------------------------------
+
+class _Text:
+    __slots__ = ("text",)
+
+    def __init__(self, text):
+        self.text = text
+
+
+class _Action:
+    __slots__ = ("pipe",)
+
+    def __init__(self, pipe):
+        self.pipe = pipe
+
+
+class _If:
+    def __init__(self, kind, pipe, body, else_body):
+        self.kind, self.pipe, self.body, self.else_body = kind, pipe, body, else_body
+
+
+class _TemplateCall:
+    def __init__(self, name, pipe):
+        self.name, self.pipe = name, pipe
+
+
+class _Break:
+    pass
+
+
+class _Continue:
+    pass
+
+
+class _BreakSignal(Exception):
+    pass
+
+
+class _ContinueSignal(Exception):
+    pass
+
+
+class _Pipe:
+    def __init__(self, decls, cmds, is_assign=False):
+        self.decls, self.cmds, self.is_assign = decls, cmds, is_assign
+
+
+# operands: ("field", [names]), ("var", name, [fields]), ("dot",), ("lit", value),
+# ("ident", name), ("pipe", _Pipe, [fields]), ("nil",)
+
+def _parse_string(tok):
+    kind, text = tok
+    if kind == "raw":
+        return text[1:-1]
+    if kind == "char":
+        return ord(json.loads('"' + text[1:-1].replace('"', '\\"') + '"'))
+    try:
+        return json.loads(text)
+    except ValueError:
+        return text[1:-1].encode().decode("unicode_escape")
+
+
+def _parse_number(text):
+    t = text.replace("_", "")
+    if t.endswith("i"):
+        raise TemplateError("complex numbers unsupported")
+    low = t.lower().lstrip("+-")
+    sign = -1 if t.startswith("-") else 1
+    if low.startswith("0x"):
+        return sign * int(low[2:], 16)
+    if low.startswith("0b"):
+        return sign * int(low[2:], 2)
+    if low.startswith("0o"):
+        return sign * int(low[2:], 8)
+    if re.match(r"^[-+]?\d+$", t):
+        if len(low) > 1 and low.startswith("0"):
+            return sign * int(low, 8)
+        return int(t)
+    return float(t)
+
+
+class _Parser:
+    def __init__(self, toks):
+        self.toks = toks
+        self.i = 0
+
+    def peek(self):
+        return self.toks[self.i] if self.i < len(self.toks) else (None, None)
+
+    def next(self):
+        t = self.peek()
+        self.i += 1
+        return t
+
+    def done(self):
+        return self.i >= len(self.toks)
+
+    def pipeline(self, allow_decl=True, stop=None):
+        decls = []
+        is_assign = False
+        if allow_decl:
+            # $x := ... | $k, $v := ... | $x = ...
+            j = self.i
+            vs = []
+            while j < len(self.toks) and self.toks[j][0] == "var" and "." not in self.toks[j][1]:
+                vs.append(self.toks[j][1])
+                j += 1
+                if j < len(self.toks) and self.toks[j][0] == "comma":
+                    j += 1
+                    continue
+                break
+            if vs and j < len(self.toks) and self.toks[j][0] in ("decl", "assign"):
+                is_assign = self.toks[j][0] == "assign"
+                decls = vs
+                self.i = j + 1
+        cmds = []
+        while True:
+            cmd = self.command(stop)
+            if not cmd:
+                raise TemplateError("missing command")
+            cmds.append(cmd)
+            k, _ = self.peek()
+            if k == "pipe":
+                self.next()
+                continue
+            break
+        return _Pipe(decls, cmds, is_assign)
+
+    def command(self, stop=None):
+        args = []
+        while not self.done():
+            k, t = self.peek()
+            if k in ("pipe", "rparen") or k == stop:
+                break
+            args.append(self.operand())
+        return args
+
+    def operand(self):
+        k, t = self.next()
+        if k == "field":
+            return ("field", t[1:].split("."))
+        if k == "dot":
+            return ("dot",)
+        if k == "var":
+            parts = t.split(".")
+            return ("var", parts[0], parts[1:])
+        if k in ("str", "raw", "char"):
+            return ("lit", _parse_string((k, t)))
+        if k == "num":
+            return ("lit", _parse_number(t))
+        if k == "ident":
+            if t == "true":
+                return ("lit", True)
+            if t == "false":
+                return ("lit", False)
+            if t == "nil":
+                return ("nil",)
+            return ("ident", t)
+        if k == "lparen":
+            p = self.pipeline(allow_decl=False)
+            k2, _ = self.next()
+            if k2 != "rparen":
+                raise TemplateError("unclosed parenthesis")
+            fields = []
+            if self.peek()[0] == "chain":
+                fields = self.next()[1][1:].split(".")
+            return ("pipe", p, fields)
+        raise TemplateError("unexpected token %r" % (t,))
+
+
+def _split_template(src, left="{{", right="}}"):
+    """Yield ('text', str) and ('action', tokens, trim_left, trim_right)."""
+    items = []
+    pos = 0
+    n = len(src)
+    while pos < n:
+        j = src.find(left, pos)
+        if j < 0:
+            items.append(["text", src[pos:]])
+            break
+        items.append(["text", src[pos:j]])
+        k = j + len(left)
+        trim_left = False
+        if src.startswith("- ", k) or (src.startswith("-", k) and k + 1 < n and src[k + 1] in "\t\r\n"):
+            trim_left = True
+            k += 1
+        # comment
+        rest = src[k:].lstrip(" \t\r\n") if trim_left else src[k:]
+        kk = k + (len(src[k:]) - len(rest))
+        if rest.startswith("/*"):
+            end = src.find("*/", kk)
+            if end < 0:
+                raise TemplateError("unclosed comment")
+            p = end + 2
+            trim_right = False
+            while p < n and src[p] in " \t\r\n" and not src.startswith(right, p):
+                p += 1
+            if src.startswith("-" + right, p):
+                trim_right = True
+                p += 1
+            if not src.startswith(right, p):
+                raise TemplateError("comment ends before closing delimiter")
+            items.append(["comment", None, trim_left, trim_right])
+            pos = p + len(right)
+            continue
+        toks, pos, trim_right = _lex_action(src, k, right)
+        items.append(["action", toks, trim_left, trim_right])
+    # apply trimming
+    for idx, it in enumerate(items):
+        if it[0] in ("action", "comment"):
+            if it[2] and idx > 0 and items[idx - 1][0] == "text":
+                items[idx - 1][1] = items[idx - 1][1].rstrip(" \t\r\n")
+            if it[3] and idx + 1 < len(items) and items[idx + 1][0] == "text":
+                items[idx + 1][1] = items[idx + 1][1].lstrip(" \t\r\n")
+    return items
+
+
+class Template:
+    """A parsed Go text/template."""
+
+    def __init__(self, src, name=""):
+        self.name = name
+        self.defines = {}
+        items = _split_template(src)
+        self._items = items
+        self._i = 0
+        body, term = self._parse_list(())
+        if term is not None:
+            raise TemplateError("unexpected {{%s}}" % term)
+        self.root = body
+
+    # -- parsing -----------------------------------------------------------
+    def _parse_list(self, terminators):
+        nodes = []
+        while self._i < len(self._items):
+            it = self._items[self._i]
+            self._i += 1
+            if it[0] == "text":
+                if it[1]:
+                    nodes.append(_Text(it[1]))
+                continue
+            if it[0] == "comment":
+                continue
+            toks = it[1]
+            if not toks:
+                raise TemplateError("missing value for command")
+            k, t = toks[0]
+            if k == "ident" and t in ("end", "else"):
+                if t not in terminators:
+                    raise TemplateError("unexpected {{%s}}" % t)
+                return nodes, (t, toks[1:])
+            if k == "ident" and t in ("if", "with", "range"):
+                p = _Parser(toks[1:])
+                pipe = p.pipeline(allow_decl=True)
+                body, term = self._parse_list(("end", "else"))
+                nodes.append(_If(t, pipe, body, self._parse_else(t, term)))
+                continue
+            if k == "ident" and t in ("define", "block"):
+                name = _parse_string(toks[1])
+                pipe = None
+                if t == "block":
+                    pipe = _Parser(toks[2:]).pipeline(allow_decl=False) if len(toks) > 2 else None
+                body, _ = self._parse_list(("end",))
+                self.defines[name] = body
+                if t == "block":
+                    nodes.append(_TemplateCall(name, pipe))
+                continue
+            if k == "ident" and t == "template":
+                name = _parse_string(toks[1])
+                pipe = _Parser(toks[2:]).pipeline(allow_decl=False) if len(toks) > 2 else None
+                nodes.append(_TemplateCall(name, pipe))
+                continue
+            if k == "ident" and t == "break":
+                nodes.append(_Break())
+                continue
+            if k == "ident" and t == "continue":
+                nodes.append(_Continue())
+                continue
+            p = _Parser(toks)
+            pipe = p.pipeline(allow_decl=True)
+            if not p.done():
+                raise TemplateError("unexpected %r in operand" % (p.peek()[1],))
+            nodes.append(_Action(pipe))
+        if terminators:
+            raise TemplateError("unexpected EOF")
+        return nodes, None
+
+    def _parse_else(self, kind, term):
+        """Parse what follows ``{{else ...}}``; ``{{else if x}}`` is sugar for a
+        nested if sharing the outer ``{{end}}``."""
+        if term[0] == "end":
+            return None
+        rest = term[1]
+        if rest and rest[0][0] == "ident" and rest[0][1] in ("if", "with") and kind != "range":
+            sub = rest[0][1]
+            pipe = _Parser(rest[1:]).pipeline(allow_decl=True)
+            body, term2 = self._parse_list(("end", "else"))
+            return [_If(sub, pipe, body, self._parse_else(sub, term2))]
+        body, _ = self._parse_list(("end",))
+        return body
+
+    # -- execution ---------------------------------------------------------
+    def execute(self, data, funcs=None):
+        out = []
+        st = _State(self, data, funcs or {})
+        st.walk(self.root, data, [("$", data)], out)
+        return "".join(out)
+
+
+class _State:
+    def __init__(self, tmpl, root, funcs):
+        self.tmpl = tmpl
+        self.root = root
+        self.funcs = dict(_BUILTINS)
+        self.funcs.update(funcs)
+
+    def walk(self, nodes, dot, scope, out):
+        mark = len(scope)
+        try:
+            for node in nodes:
+                if isinstance(node, _Text):
+                    out.append(node.text)
+                elif isinstance(node, _Action):
+                    val = self.eval_pipe(node.pipe, dot, scope)
+                    if not node.pipe.decls:
+                        out.append(go_sprint(val))
+                elif isinstance(node, _If):
+                    self.walk_control(node, dot, scope, out)
+                elif isinstance(node, _TemplateCall):
+                    body = self.tmpl.defines.get(node.name)
+                    if body is None:
+                        raise TemplateError("no such template %q" % node.name)
+                    newdot = self.eval_pipe(node.pipe, dot, scope) if node.pipe else None
+                    self.walk(body, newdot, [("$", newdot)], out)
+                elif isinstance(node, _Break):
+                    raise _BreakSignal()
+                elif isinstance(node, _Continue):
+                    raise _ContinueSignal()
+        finally:
+            del scope[mark:]
+
+    def walk_control(self, node, dot, scope, out):
+        mark = len(scope)
+        try:
+            if node.kind == "range":
+                val = self.eval_pipe(node.pipe, dot, scope, declare=False)
+                items = []
+                if isinstance(val, dict):
+                    items = [(k, val[k]) for k in sorted(val.keys(), key=_sort_key)]
+                elif isinstance(val, (list, tuple, str, bytes)):
+                    if isinstance(val, str):
+                        raise TemplateError("range can't iterate over %s" % val)
+                    items = list(enumerate(val))
+                elif isinstance(val, int) and not isinstance(val, bool):
+                    items = [(i, i) for i in range(val)]
+                elif val is None or val is NO_VALUE:
+                    items = []
+                else:
+                    raise TemplateError("range can't iterate over %s" % go_sprint(val))
+                if not items:
+                    if node.else_body is not None:
+                        self.walk(node.else_body, dot, scope, out)
+                    return
+                decls = node.pipe.decls
+                for k, v in items:
+                    inner = len(scope)
+                    if len(decls) == 1:
+                        scope.append((decls[0], v))
+                    elif len(decls) == 2:
+                        scope.append((decls[0], k))
+                        scope.append((decls[1], v))
+                    try:
+                        self.walk(node.body, v, scope, out)
+                    except _BreakSignal:
+                        break
+                    except _ContinueSignal:
+                        pass
+                    finally:
+                        del scope[inner:]
+                return
+            val = self.eval_pipe(node.pipe, dot, scope)
+            if _truth(val):
+                self.walk(node.body, val if node.kind == "with" else dot, scope, out)
+            elif node.else_body is not None:
+                self.walk(node.else_body, dot, scope, out)
+        finally:
+            del scope[mark:]
+
+    # -- pipelines -----------------------------------------------------------
+    def eval_pipe(self, pipe, dot, scope, declare=True):
+        val = None
+        final = None
+        for i, cmd in enumerate(pipe.cmds):
+            val = self.eval_cmd(cmd, dot, scope, final if i > 0 else None, has_final=i > 0)
+            final = val
+        if pipe.decls and declare:
+            if pipe.is_assign:
+                for name in pipe.decls:
+                    for idx in range(len(scope) - 1, -1, -1):
+                        if scope[idx][0] == name:
+                            scope[idx] = (name, val)
+                            break
+                    else:
+                        raise TemplateError("undefined variable: %s" % name)
+            else:
+                scope.append((pipe.decls[0], val))
+        return val
+
+    def eval_cmd(self, cmd, dot, scope, final, has_final):
+        first = cmd[0]
+        if first[0] == "ident":
+            name = first[1]
+            fn = self.funcs.get(name)
+            if fn is None:
+                raise TemplateError('function "%s" not defined' % name)
+            if name in ("and", "or"):
+                args = cmd[1:]
+                vals = [self.eval_arg(a, dot, scope) for a in args]
+                if has_final:
+                    vals.append(final)
+                return fn(*vals)
+            args = [self.eval_arg(a, dot, scope) for a in cmd[1:]]
+            if has_final:
+                args.append(final)
+            try:
+                return fn(*args)
+            except TemplateError:
+                raise
+            except Exception as e:  # noqa: BLE001
+                raise TemplateError("error calling %s: %s" % (name, e))
+        if len(cmd) > 1 or has_final:
+            # method-style calls with args are not supported on data values
+            if first[0] in ("field",) and (len(cmd) > 1 or has_final):
+                raise TemplateError("can't give argument to non-function %s" % ".".join(first[1]))
+        return self.eval_arg(first, dot, scope)
+
+    def eval_arg(self, a, dot, scope):
+        kind = a[0]
+        if kind == "lit":
+            return a[1]
+        if kind == "nil":
+            return None
+        if kind == "dot":
+            return dot
+        if kind == "field":
+            return self.fields(dot, a[1])
+        if kind == "var":
+            name = a[1]
+            for idx in range(len(scope) - 1, -1, -1):
+                if scope[idx][0] == name:
+                    return self.fields(scope[idx][1], a[2])
+            raise TemplateError("undefined variable: %s" % name)
+        if kind == "pipe":
+            v = self.eval_pipe(a[1], dot, scope, declare=False)
+            return self.fields(v, a[2])
+        if kind == "ident":
+            fn = self.funcs.get(a[1])
+            if fn is None:
+                raise TemplateError('function "%s" not defined' % a[1])
+            return fn()
+        raise TemplateError("bad operand")
+
+    @staticmethod
+    def fields(val, names):
+        for name in names:
+            if val is NO_VALUE or val is None:
+                if val is None:
+                    raise TemplateError("nil pointer evaluating .%s" % name)
+                return NO_VALUE
+            if isinstance(val, dict):
+                val = val.get(name, NO_VALUE)
+            elif hasattr(val, name):
+                val = getattr(val, name)
+                if callable(val):
+                    val = val()
+            else:
+                raise TemplateError("can't evaluate field %s in type %s" % (name, type(val).__name__))
+        return val
+
+
+# ---------------------------------------------------------------------------
+# Builtins
+# ---------------------------------------------------------------------------
+
+def _and(*args):
+    v = True
+    for v in args:
+        if not _truth(v):
+            return v
+    return v
+
+
+def _or(*args):
+    v = False
+    for v in args:
+        if _truth(v):
+            return v
+    return v
+
+
+def _basic(v):
+    if v is NO_VALUE:
+        return None
+    return v
+
+
+def _eq(a, *bs):
+    if not bs:
+        raise TemplateError("missing argument for comparison")
+    a = _basic(a)
+    for b in bs:
+        b = _basic(b)
+        if isinstance(a, bool) != isinstance(b, bool) and a is not None and b is not None:
+            raise TemplateError("incompatible types for comparison")
+        if a == b:
+            return True
+    return False
+
+
+def _ne(a, b):
+    return not _eq(a, b)
+
+
+def _cmp(op):
+    def f(a, b):
+        a, b = _basic(a), _basic(b)
+        try:
+            return op(a, b)
+        except TypeError:
+            raise TemplateError("incompatible types for comparison")
+    return f
+
+
+def _index(item, *idx):
+    v = item
+    for i in idx:
+        if v is NO_VALUE or v is None:
+            raise TemplateError("index of untyped nil")
+        if isinstance(v, dict):
+            v = v.get(i, NO_VALUE)
+        elif isinstance(v, (list, tuple, str, bytes)):
+            if not isinstance(i, int) or i < 0 or i >= len(v):
+                raise TemplateError("index out of range: %s" % (i,))
+            v = v[i]
+            if isinstance(v, str) and len(v) == 1 and isinstance(item, str):
+                v = ord(v)
+        else:
+            raise TemplateError("can't index item of type %s" % type(v).__name__)
+    return v
+
+
+def _slice(item, *idx):
+    if len(idx) == 0:
+        return item
+    if len(idx) == 1:
+        return item[idx[0]:]
+    return item[idx[0]:idx[1]]
+
+
+def _len(v):
+    if v is NO_VALUE or v is None:
+        raise TemplateError("len of nil pointer")
+    try:
+        return len(v)
+    except TypeError:
+        raise TemplateError("len of type %s" % type(v).__name__)
+
+
+def _print(*args):
+    # fmt.Sprint: spaces between operands when neither is a string
+    out = []
+    prev_str = True
+    for i, a in enumerate(args):
+        is_str = isinstance(a, str)
+        if i > 0 and not is_str and not prev_str:
+            out.append(" ")
+        out.append(go_sprint(a))
+        prev_str = is_str
+    return "".join(out)
+
+
+def _println(*args):
+    return " ".join(go_sprint(a) for a in args) + "\n"
+
+
+def _printf(fmt, *args):
+    return go_sprintf(fmt, list(args))
+
+
+def _html_escape(*args):
+    return _html.escape(_print(*args), quote=True).replace("&#x27;", "&#39;")
+
+
+def _js_escape(*args):
+    s = _print(*args)
+    out = []
+    for ch in s:
+        if ch in "\\'\"<>&=":
+            out.append("\\u%04X" % ord(ch) if ch in "<>&=" else "\\" + ch)
+        elif ord(ch) < 0x20:
+            out.append("\\u%04X" % ord(ch))
+        else:
+            out.append(ch)
+    return "".join(out)
+
+
+def _urlquery(*args):
+    return urllib.parse.quote_plus(_print(*args))
+
+
+def _call(fn, *args):
+    return fn(*args)
+
+
+_BUILTINS = {
+    "and": _and, "or": _or, "not": lambda v: not _truth(v), "len": _len, "index": _index,
+    "slice": _slice, "print": _print, "println": _println, "printf": _printf,
+    "eq": _eq, "ne": _ne,
+    "lt": _cmp(lambda a, b: a < b), "le": _cmp(lambda a, b: a <= b),
+    "gt": _cmp(lambda a, b: a > b), "ge": _cmp(lambda a, b: a >= b),
+    "html": _html_escape, "js": _js_escape, "urlquery": _urlquery, "call": _call,
+}
+
+
+_CACHE = {}
+
+
+def render(src, data, funcs=None):
+    """Parse (cached) and execute a Go template against ``data``."""
+    t = _CACHE.get(src)
+    if t is None:
+        t = Template(src)
+        if len(_CACHE) < 512:
+            _CACHE[src] = t
+    return t.execute(data, funcs)

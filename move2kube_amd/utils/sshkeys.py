@@ -1,0 +1,154 @@
+"""SSH keys for the CI/CD git secrets (reference ``internal/common/sshkeys/sshkeys.go``).
+
+Public host keys for github.com, gitlab.com and bitbucket.org are built in;
+the user's ``~/.ssh/known_hosts`` and private keys are only read after a QA
+confirmation.  Private keys are re-encoded to PEM (RSA/ECDSA, the formats
+Tekton's git-init accepts) with ``ssh-keygen``; an encrypted key is decrypted
+with a passphrase asked through a Password problem (never cached).
+"""
+
+import os
+import shutil
+import subprocess
+import tempfile
+
+from . import log
+from .knownhosts import KnownHostsError, parse_known_hosts
+
+DOMAIN_TO_PUBLIC_KEYS = {
+    "github.com": ["github.com ssh-rsa AAAAB3NzaC1yc2EAAAABIwAAAQEAq2A7hRGmdnm9tUDbO9IDSwBK6TbQa+PXYPCPy6rbTrTtw7PHkccKrpp0yVhp5HdEIcKr6pLlVDBfOLX9QUsyCOV0wzfjIJNlGEYsdlLJizHhbn2mUjvSAHQqZETYP81eFzLQNnPHt4EVVUh7VfDESU84KezmD5QlWpXLmvU31/yMf+Se8xhHTvKSCZIFImWwoG6mbUoWf9nzpIoaSjB+weqqUUmpaaasXVal72J+UX2B+2RPW3RcT0eOzQgqlJL3RKrTJvdsjE3JEAvGq3lGHSZXy28G3skua2SmVi/w4yCE6gbODqnTWlg7+wC604ydGXA8VJiS5ap43JXiUFFAaQ=="],
+    "gitlab.com": ["gitlab.com ssh-ed25519 AAAAC3NzaC1lZDI1NTE5AAAAIAfuCHKVTjquxvt6CM6tdG4SLp1Btn/nOeHHE5UOzRdf",
+                   "gitlab.com ssh-rsa AAAAB3NzaC1yc2EAAAADAQABAAABAQCsj2bNKTBSpIYDEGk9KxsGh3mySTRgMtXL583qmBpzeQ+jqCMRgBqB98u3z++J1sKlXHWfM9dyhSevkMwSbhoR8XIq/U0tCNyokEi/ueaBMCvbcTHhO7FcwzY92WK4Yt0aGROY5qX2UKSeOvuP4D6TPqKF1onrSzH9bx9XUf2lEdWT/ia1NEKjunUqu1xOB/StKDHMoX4/OKyIzuS0q/T1zOATthvasJFoPrAjkohTyaDUz2LN5JoH839hViyEG82yB+MjcFV5MU3N1l1QL3cVUCh93xSaua1N85qivl+siMkPGbO5xR/En4iEY6K2XPASUEMaieWVNTRCtJ4S8H+9",
+                   "gitlab.com ecdsa-sha2-nistp256 AAAAE2VjZHNhLXNoYTItbmlzdHAyNTYAAAAIbmlzdHAyNTYAAABBBFSMqzJeV9rUzU4kWitGjeR4PWSa29SPqJ1fVkhtj3Hw9xjLVXVYrU9QlYWrOLXBpQ6KWjbjTDTdDkoohFzgbEY="],
+    "bitbucket.org": ["bitbucket.org ssh-rsa AAAAB3NzaC1yc2EAAAABIwAAAQEAubiN81eDcafrgMeLzaFPsw2kNvEcqTKl/VqLat/MaB33pZy0y3rJZtnqwR2qOOvbwKZYKiEO1O6VqNEBxKvJJelCq0dTXWT5pbO2gDXC6h6QDXCaHo6pOHGPUy+YBaGQRGuSusMEASYiWunYN0vCAI8QaXnWMXNMdFP3jHAJH0eDsoiGnLPBlBp4TNm6rYI74nMzgz3B9IikW4WVK+dc8KZJZWYjAuORU3jc1c/NPskD2ASinf8v3xnfXeukU0sJ5N6m5E8VLjObPEO+mN2t/FZTMZLiFqPWc/ALSqnMnnhwrNi2rbfg/rd/IpL8Le3pSBne8+seeFVBoGqzHM9yXw=="],
+}
+
+_state = {"known_hosts_loaded": False, "keys_loaded": False, "key_dir": "", "keys": []}
+
+
+def reset():
+    _state.update({"known_hosts_loaded": False, "keys_loaded": False, "key_dir": "", "keys": []})
+
+
+def _home():
+    return os.path.expanduser("~")
+
+
+def load_known_hosts_of_current_user():
+    from ..models import qa
+    from ..qaengine import fetch_answer
+    if _state["known_hosts_loaded"]:
+        return
+    _state["known_hosts_loaded"] = True
+    path = os.path.join(_home(), ".ssh", "known_hosts")
+    msg = ("The CI/CD pipeline needs access to the git repos in order to clone, build and push.\n"
+           "Move2Kube has public keys for github.com, gitlab.com, and bitbucket.org by default.\n"
+           "If any of the repos use ssh authentication we will need public keys in order to verify.\n"
+           "Do you want to load the public keys from your [%s]?:" % path)
+    prob = qa.new_confirm_problem(msg, ["No, I will add them later if necessary."], False)
+    if not fetch_answer(prob).get_bool_answer():
+        log.debug("Don't read public keys from known_hosts. They will be added later if necessary.")
+        return
+    try:
+        keys = parse_known_hosts(path)
+    except (OSError, KnownHostsError) as e:
+        log.warning("Failed to get public keys from the known_hosts file at path %r Error: %r", path, str(e))
+        return
+    for domain, lines in keys.items():
+        DOMAIN_TO_PUBLIC_KEYS.setdefault(domain, lines)
+
+
+def _load_ssh_keys_of_current_user():
+    from ..models import qa
+    from ..qaengine import fetch_answer
+    if _state["keys_loaded"]:
+        return
+    _state["keys_loaded"] = True
+    d = os.path.join(_home(), ".ssh")
+    _state["key_dir"] = d
+    msg = ("The CI/CD pipeline needs access to the git repos in order to clone, build and push.\n"
+           "If any of the repos require ssh keys you will need to provide them.\n"
+           "Do you want to load the private ssh keys from [%s]?:" % d)
+    prob = qa.new_confirm_problem(msg, ["No, I will add them later if necessary."], False)
+    if not fetch_answer(prob).get_bool_answer():
+        log.debug("Don't read private keys. They will be added later if necessary.")
+        return
+    try:
+        names = sorted(os.listdir(d))
+    except OSError as e:
+        log.error("Failed to read the ssh directory at path %r Error: %r", d, str(e))
+        return
+    if not names:
+        log.warning("No key files where found in %s", d)
+        return
+    prob = qa.new_multiselect_problem("These are the files we found in %r . Which keys should we consider?" % d,
+                                      ["Select all the keys that give acess to git repos."], names, names)
+    names = fetch_answer(prob).get_slice_answer()
+    if not names:
+        log.info("All key files ignored.")
+        return
+    _state["keys"] = names
+
+
+def _to_pem(path, passphrase=""):
+    """Re-encode a private key file as PEM (PKCS#1 RSA / SEC1 EC) via ssh-keygen."""
+    if shutil.which("ssh-keygen") is None:
+        with open(path) as f:
+            return f.read()
+    with tempfile.TemporaryDirectory() as td:
+        tmp = os.path.join(td, "key")
+        shutil.copyfile(path, tmp)
+        os.chmod(tmp, 0o600)
+        p = subprocess.run(["ssh-keygen", "-p", "-m", "PEM", "-P", passphrase, "-N", "", "-f", tmp],
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, stdin=subprocess.DEVNULL, timeout=30)
+        if p.returncode != 0:
+            raise ValueError(p.stderr.decode("utf-8", "replace").strip() or "ssh-keygen failed")
+        with open(tmp) as f:
+            return f.read()
+
+
+def _is_encrypted(path):
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return False
+    if b"ENCRYPTED" in data:
+        return True
+    if shutil.which("ssh-keygen") is None:
+        return False
+    p = subprocess.run(["ssh-keygen", "-y", "-P", "", "-f", path], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, stdin=subprocess.DEVNULL, timeout=30)
+    return p.returncode != 0 and b"incorrect passphrase" in p.stderr
+
+
+def load_ssh_key(filename):
+    from ..models import qa
+    from ..qaengine import fetch_answer
+    path = os.path.join(_state["key_dir"], filename)
+    passphrase = ""
+    if _is_encrypted(path):
+        prob = qa.new_password_problem("Enter the password to decrypt the private key %r : " % filename, ["Password:"])
+        passphrase = fetch_answer(prob).get_string_answer()
+    return _to_pem(path, passphrase)
+
+
+def get_ssh_key(domain):
+    """(pem, True) for the key the user picks for ``domain``; ('', False) otherwise."""
+    from ..models import qa
+    from ..qaengine import fetch_answer
+    _load_ssh_keys_of_current_user()
+    if not _state["keys"]:
+        return "", False
+    names = list(_state["keys"]) + ["NONE"]
+    prob = qa.new_select_problem("Select the key to use to for the git domain %s :" % domain,
+                                 ["If none of the keys are correct, select None."], "NONE", names)
+    name = fetch_answer(prob).get_string_answer()
+    if name == "NONE":
+        log.debug("No key selected for domain %s", domain)
+        return "", False
+    try:
+        return load_ssh_key(name), True
+    except (OSError, ValueError, subprocess.SubprocessError) as e:
+        log.warning("Failed to load the key %r Error %r", name, str(e))
+        return "", False

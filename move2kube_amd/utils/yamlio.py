@@ -1,0 +1,579 @@
+"""YAML reading and a byte-compatible re-implementation of go-yaml v3 output.
+
+Every file the reference writes goes through ``gopkg.in/yaml.v3`` with
+``SetIndent(2)`` (``internal/common/utils.go:159-177``,
+``internal/transformer/transformer.go:162-204``).  Plans, QA caches, cluster
+metadata and the generated Kubernetes manifests must round-trip
+byte-for-byte (the reference's ``TestWritePlan`` compares bytes), so this
+module re-implements the parts of the libyaml emitter that go-yaml v3 uses:
+
+* scalar style selection (``yaml_emitter_analyze_scalar`` +
+  ``yaml_emitter_select_scalar_style`` + go-yaml's ``stringv`` resolve check),
+* block mappings/sequences with sequences indented under their key,
+* literal block scalars with chomping/indentation hints,
+* the natural key order go-yaml uses for Go maps (``sorter.go``).
+
+Ordering model: a plain ``dict`` is emitted in insertion order (Go struct
+field order) unless ``sort_maps=True``; a :class:`GoMap` is always sorted with
+the go-yaml key comparator (Go maps).
+"""
+
+import functools
+import math
+import re
+
+import yaml
+
+__all__ = [
+    "GoMap", "dump", "dumps_k8s", "load", "load_raw", "load_all", "go_key_sorted",
+    "YAMLError",
+]
+
+YAMLError = yaml.YAMLError
+
+
+class GoMap(dict):
+    """A mapping that go-yaml would encode with sorted keys (a Go map)."""
+
+
+# ---------------------------------------------------------------------------
+# go-yaml key ordering (yaml.v3 sorter.go keyList.Less)
+# ---------------------------------------------------------------------------
+
+def _kind_rank(v):
+    # reflect.Kind order used when kinds differ: Bool(1) < Int(2..) < Uint < Float(13/14) < String(24)
+    if isinstance(v, bool):
+        return 1
+    if isinstance(v, int):
+        return 2
+    if isinstance(v, float):
+        return 14
+    if isinstance(v, str):
+        return 24
+    return 30
+
+
+def _go_key_cmp(a, b):
+    if not isinstance(a, str) or not isinstance(b, str):
+        ka, kb = _kind_rank(a), _kind_rank(b)
+        if ka != kb:
+            return -1 if ka < kb else 1
+        if isinstance(a, (int, float)) and isinstance(b, (int, float)):
+            return (a > b) - (a < b)
+        return 0
+    ar, br = a, b
+    digits = False
+    n = min(len(ar), len(br))
+    for i in range(n):
+        if ar[i] == br[i]:
+            digits = ar[i].isdigit()
+            continue
+        al = ar[i].isalpha()
+        bl = br[i].isalpha()
+        if al and bl:
+            return -1 if ar[i] < br[i] else 1
+        if al or bl:
+            if digits:
+                return -1 if al else 1
+            return -1 if bl else 1
+        an = bn = 0
+        if ar[i] == "0" or br[i] == "0":
+            j = i - 1
+            while j >= 0 and ar[j].isdigit():
+                if ar[j] != "0":
+                    an = bn = 1
+                    break
+                j -= 1
+        ai = i
+        while ai < len(ar) and ar[ai].isdigit():
+            an = an * 10 + (ord(ar[ai]) - 48)
+            ai += 1
+        bi = i
+        while bi < len(br) and br[bi].isdigit():
+            bn = bn * 10 + (ord(br[bi]) - 48)
+            bi += 1
+        if an != bn:
+            return -1 if an < bn else 1
+        if ai != bi:
+            return -1 if ai < bi else 1
+        return -1 if ar[i] < br[i] else 1
+    return (len(ar) > len(br)) - (len(ar) < len(br))
+
+
+_go_key = functools.cmp_to_key(_go_key_cmp)
+
+
+def go_key_sorted(keys):
+    """Sort keys the way go-yaml v3 sorts Go map keys."""
+    return sorted(keys, key=_go_key)
+
+
+# ---------------------------------------------------------------------------
+# Plain-scalar resolution (what a plain scalar would decode to)
+# ---------------------------------------------------------------------------
+
+_YAML_FLOAT = re.compile(r"^[-+]?(\.[0-9]+|[0-9]+(\.[0-9]*)?)([eE][-+]?[0-9]+)?$")
+_TIMESTAMP_FORMATS = [
+    re.compile(r"^\d{4}-\d{1,2}-\d{1,2}[Tt]\d{1,2}:\d{1,2}:\d{1,2}(\.\d+)?(Z|[+-]\d{1,2}(:\d{2})?)$"),
+    re.compile(r"^\d{4}-\d{1,2}-\d{1,2} \d{1,2}:\d{1,2}:\d{1,2}(\.\d+)?$"),
+    re.compile(r"^\d{4}-\d{1,2}-\d{1,2}$"),
+]
+_NULLS = {"", "~", "null", "Null", "NULL"}
+_BOOLS = {"true", "True", "TRUE", "false", "False", "FALSE"}
+_OLD_BOOLS = {"y", "Y", "yes", "Yes", "YES", "on", "On", "ON",
+              "n", "N", "no", "No", "NO", "off", "Off", "OFF"}
+_SPECIAL_FLOATS = {".inf", ".Inf", ".INF", "+.inf", "+.Inf", "+.INF",
+                   "-.inf", "-.Inf", "-.INF", ".nan", ".NaN", ".NAN"}
+_BASE60 = re.compile(r"^[-+]?[0-9][0-9_]*(?::[0-5]?[0-9])+(?:\.[0-9_]*)?$")
+
+
+def _go_parse_int(s):
+    """strconv.ParseInt(s, 0, 64) acceptance (after '_' removal)."""
+    t = s
+    if t[:1] in "+-":
+        t = t[1:]
+    if not t:
+        return False
+    low = t.lower()
+    try:
+        if low.startswith("0x"):
+            int(t[2:], 16)
+            return len(t) > 2
+        if low.startswith("0o"):
+            int(t[2:], 8)
+            return len(t) > 2
+        if low.startswith("0b"):
+            int(t[2:], 2)
+            return len(t) > 2
+        if len(t) > 1 and t[0] == "0":
+            int(t[1:], 8)
+            return True
+        if not t.isdigit():
+            return False
+        return True
+    except ValueError:
+        return False
+
+
+def resolves_to_string(s):
+    """True if ``s`` written as a plain scalar would decode back as a string."""
+    if s in _NULLS or s in _BOOLS:
+        return False
+    if not s:
+        return False
+    c = s[0]
+    if c.isdigit() or c in "+-.":
+        if s in _SPECIAL_FLOATS:
+            return False
+        if c.isdigit():
+            for rx in _TIMESTAMP_FORMATS:
+                if rx.match(s):
+                    return False
+        plain = s.replace("_", "")
+        if _go_parse_int(plain):
+            return False
+        if _YAML_FLOAT.match(plain):
+            return False
+        if c == "." :
+            try:
+                float(s)
+                return False
+            except ValueError:
+                pass
+    if s.startswith("<<") and s == "<<":
+        return False
+    return True
+
+
+# ---------------------------------------------------------------------------
+# libyaml scalar analysis
+# ---------------------------------------------------------------------------
+
+def _is_break(ch):
+    return ch in "\r\n\x85  "
+
+
+def _is_space(ch):
+    return ch == " "
+
+
+def _is_printable(ch):
+    o = ord(ch)
+    return (o == 0x0A or 0x20 <= o <= 0x7E or o == 0x85 or 0xA0 <= o <= 0xD7FF
+            or 0xE000 <= o <= 0xFFFD and o != 0xFEFF or 0x10000 <= o <= 0x10FFFF)
+
+
+def _analyze(value):
+    """Return (multiline, block_plain_allowed, single_quoted_allowed, block_allowed)."""
+    if value == "":
+        return False, True, True, False
+    block_indicators = flow_indicators = False
+    line_breaks = special = tabs = False
+    leading_space = leading_break = trailing_space = trailing_break = False
+    break_space = space_break = False
+    previous_space = previous_break = False
+    if value.startswith("---") or value.startswith("..."):
+        block_indicators = flow_indicators = True
+    preceded_by_ws = True
+    n = len(value)
+    for i, ch in enumerate(value):
+        followed_by_ws = i + 1 >= n or value[i + 1] in " \t\r\n\x85  "
+        if i == 0:
+            if ch in "#,[]{}&*!|>'\"%@`":
+                flow_indicators = block_indicators = True
+            elif ch in "?:":
+                flow_indicators = True
+                if followed_by_ws:
+                    block_indicators = True
+            elif ch == "-":
+                if followed_by_ws:
+                    flow_indicators = block_indicators = True
+        else:
+            if ch in ",?[]{}":
+                flow_indicators = True
+            elif ch == ":":
+                flow_indicators = True
+                if followed_by_ws:
+                    block_indicators = True
+            elif ch == "#":
+                if preceded_by_ws:
+                    flow_indicators = block_indicators = True
+        if ch == "\t":
+            tabs = True
+        elif not _is_printable(ch):
+            special = True
+        if _is_space(ch):
+            if i == 0:
+                leading_space = True
+            if i == n - 1:
+                trailing_space = True
+            if previous_break:
+                break_space = True
+            previous_space, previous_break = True, False
+        elif _is_break(ch):
+            line_breaks = True
+            if i == 0:
+                leading_break = True
+            if i == n - 1:
+                trailing_break = True
+            if previous_space:
+                space_break = True
+            previous_space, previous_break = False, True
+        else:
+            previous_space = previous_break = False
+        preceded_by_ws = ch in " \t\r\n\x85  \x00"
+    block_plain = True
+    single_quoted = True
+    block_allowed = True
+    if leading_space or leading_break or trailing_space or trailing_break:
+        block_plain = False
+    if trailing_space:
+        block_allowed = False
+    if break_space:
+        block_plain = False
+        single_quoted = False
+    if space_break or tabs or special:
+        block_plain = False
+        single_quoted = False
+    if space_break or special:
+        block_allowed = False
+    if line_breaks:
+        block_plain = False
+    if block_indicators:
+        block_plain = False
+    return line_breaks, block_plain, single_quoted, block_allowed
+
+
+_ESCAPES = {
+    "\x00": "\\0", "\x07": "\\a", "\x08": "\\b", "\t": "\\t", "\n": "\\n",
+    "\x0b": "\\v", "\x0c": "\\f", "\r": "\\r", "\x1b": "\\e", '"': '\\"',
+    "\\": "\\\\", "\x85": "\\N", "\xa0": "\\_", " ": "\\L", " ": "\\P",
+}
+
+
+def _double_quoted(s):
+    out = ['"']
+    for ch in s:
+        if ch in _ESCAPES:
+            out.append(_ESCAPES[ch])
+        elif not _is_printable(ch) or ch == "﻿":
+            o = ord(ch)
+            if o <= 0xFF:
+                out.append("\\x%02X" % o)
+            elif o <= 0xFFFF:
+                out.append("\\u%04X" % o)
+            else:
+                out.append("\\U%08X" % o)
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
+def _single_quoted(s):
+    return "'" + s.replace("'", "''") + "'"
+
+
+PLAIN, SINGLE, DOUBLE, LITERAL = range(4)
+
+
+def _string_style(s, key=False):
+    """Style go-yaml v3 would emit for a Go string value ``s``."""
+    can_plain = resolves_to_string(s) and not _BASE60.match(s) and s not in _OLD_BOOLS
+    if "\n" in s:
+        style = LITERAL
+    elif can_plain:
+        style = PLAIN
+    else:
+        style = DOUBLE
+    multiline, block_plain, single_ok, block_ok = _analyze(s)
+    if key and multiline:
+        style = DOUBLE
+    if style == PLAIN:
+        if not block_plain:
+            style = SINGLE
+        if s == "" and key:
+            style = SINGLE
+    if style == SINGLE and not single_ok:
+        style = DOUBLE
+    if style == LITERAL and (not block_ok or key):
+        style = DOUBLE
+    return style
+
+
+def _literal(s, indent):
+    hint = ""
+    if s and (s[0] == " " or _is_break(s[0])):
+        hint += "2"
+    if s == "" or not _is_break(s[-1]):
+        hint += "-"
+    elif len(s) == 1 or _is_break(s[-2]):
+        hint += "+"
+    lines = ["|" + hint]
+    pad = " " * indent
+    buf = []
+    breaks = True
+    for ch in s:
+        if _is_break(ch):
+            lines.append("".join(buf))
+            buf = []
+            breaks = True
+        else:
+            if breaks:
+                buf.append(pad)
+                breaks = False
+            buf.append(ch)
+    if buf:
+        lines.append("".join(buf))
+    # the first element is the header; content lines follow, each terminated by \n
+    return lines
+
+
+def _format_float(f):
+    if math.isnan(f):
+        return ".nan"
+    if math.isinf(f):
+        return ".inf" if f > 0 else "-.inf"
+    return go_format_float(f)
+
+
+def go_format_float(f):
+    """strconv.FormatFloat(f, 'g', -1, 64)."""
+    if f == 0:
+        return "-0" if math.copysign(1.0, f) < 0 else "0"
+    neg = f < 0
+    a = -f if neg else f
+    # shortest round-trip decimal digits (Python's repr is shortest round-trip)
+    s = "%.17e" % a
+    for prec in range(1, 18):
+        s = "%.*e" % (prec - 1, a)
+        if float(s) == a:
+            break
+    mant, e = s.split("e")
+    e = int(e)
+    digits = mant.replace(".", "").rstrip("0") or "0"
+    nd = len(digits)
+    # Go: with shortest formatting eprec is 6; %e when exp < -4 || exp >= eprec
+    if e < -4 or e >= 6:
+        m = digits[0] + ("." + digits[1:] if nd > 1 else "")
+        out = "%se%s%02d" % (m, "-" if e < 0 else "+", abs(e))
+    elif e >= nd - 1:
+        out = digits + "0" * (e - nd + 1)
+    elif e >= 0:
+        out = digits[:e + 1] + "." + digits[e + 1:]
+    else:
+        out = "0." + "0" * (-e - 1) + digits
+    return ("-" if neg else "") + out
+
+
+# ---------------------------------------------------------------------------
+# Emitter
+# ---------------------------------------------------------------------------
+
+class _Emitter:
+    def __init__(self, sort_maps):
+        self.sort_maps = sort_maps
+        self.out = []
+
+    def _keys(self, d):
+        if isinstance(d, GoMap) or self.sort_maps:
+            return go_key_sorted(d.keys())
+        return list(d.keys())
+
+    def scalar(self, v, indent, key=False):
+        """Return list of lines; first line is the inline part."""
+        if v is None:
+            return ["null"]
+        if v is True:
+            return ["true"]
+        if v is False:
+            return ["false"]
+        if isinstance(v, int):
+            return [str(v)]
+        if isinstance(v, float):
+            return [_format_float(v)]
+        if isinstance(v, bytes):
+            import base64
+            return ["!!binary " + base64.b64encode(v).decode()]
+        s = str(v)
+        style = _string_style(s, key=key)
+        if style == PLAIN:
+            return [s]
+        if style == SINGLE:
+            return [_single_quoted(s)]
+        if style == DOUBLE:
+            return [_double_quoted(s)]
+        return _literal(s, indent)
+
+    @staticmethod
+    def _is_coll(v):
+        return isinstance(v, (dict, list, tuple))
+
+    def emit_map(self, d, indent, first_prefix=None):
+        pad = " " * indent
+        first = True
+        for k in self._keys(d):
+            v = d[k]
+            kl = self.scalar(k, indent, key=True)[0]
+            prefix = first_prefix if (first and first_prefix is not None) else pad
+            first = False
+            self._emit_value(prefix + kl + ":", v, indent)
+
+    def emit_seq(self, seq, indent, first_prefix=None):
+        pad = " " * indent
+        first = True
+        for item in seq:
+            prefix = first_prefix if (first and first_prefix is not None) else pad
+            first = False
+            if isinstance(item, dict) and item:
+                self.emit_map(item, indent + 2, first_prefix=prefix + "- ")
+            elif isinstance(item, (list, tuple)) and item:
+                self.emit_seq(item, indent + 2, first_prefix=prefix + "- ")
+            elif isinstance(item, dict):
+                self.out.append(prefix + "- {}")
+            elif isinstance(item, (list, tuple)):
+                self.out.append(prefix + "- []")
+            else:
+                lines = self.scalar(item, indent + 2)
+                self.out.append(prefix + "- " + lines[0])
+                self.out.extend(lines[1:])
+
+    def _emit_value(self, head, v, indent):
+        if isinstance(v, dict):
+            if not v:
+                self.out.append(head + " {}")
+            else:
+                self.out.append(head)
+                self.emit_map(v, indent + 2)
+        elif isinstance(v, (list, tuple)):
+            if not v:
+                self.out.append(head + " []")
+            else:
+                self.out.append(head)
+                self.emit_seq(v, indent + 2)
+        else:
+            lines = self.scalar(v, indent + 2)
+            self.out.append(head + " " + lines[0])
+            self.out.extend(lines[1:])
+
+    def document(self, data):
+        if isinstance(data, dict):
+            if data:
+                self.emit_map(data, 0)
+            else:
+                self.out.append("{}")
+        elif isinstance(data, (list, tuple)):
+            if data:
+                self.emit_seq(data, 0)
+            else:
+                self.out.append("[]")
+        else:
+            lines = self.scalar(data, 2)
+            self.out.append(lines[0])
+            self.out.extend(lines[1:])
+        return "\n".join(self.out) + "\n"
+
+
+def dump(data, sort_maps=False):
+    """Encode ``data`` like go-yaml v3 ``Encoder`` with ``SetIndent(2)``."""
+    return _Emitter(sort_maps).document(data)
+
+
+def dumps_k8s(obj):
+    """Encode a JSON-shaped object the way the reference writes manifests
+    (json.Marshal -> yaml.Unmarshal into interface{} -> yaml.v3 encode): every
+    mapping becomes a Go map, so keys are sorted."""
+    return dump(obj, sort_maps=True)
+
+
+# ---------------------------------------------------------------------------
+# Loading
+# ---------------------------------------------------------------------------
+
+_BaseLoader = getattr(yaml, "CSafeLoader", yaml.SafeLoader)
+
+
+def _make_loader(name, keep_resolvers):
+    cls = type(name, (_BaseLoader,), {})
+    cls.yaml_implicit_resolvers = {}
+    for ch, resolvers in yaml.SafeLoader.yaml_implicit_resolvers.items():
+        kept = [(tag, rx) for tag, rx in resolvers if tag in keep_resolvers]
+        if kept:
+            cls.yaml_implicit_resolvers[ch] = kept
+    return cls
+
+
+# YAML 1.2-ish core schema as go-yaml v3 resolves it: no yes/no/on/off bools,
+# no timestamps (kept as strings for interface{} targets).
+_TypedLoader = _make_loader("_TypedLoader", {
+    "tag:yaml.org,2002:null", "tag:yaml.org,2002:int", "tag:yaml.org,2002:float",
+    "tag:yaml.org,2002:merge"})
+_TypedLoader.add_implicit_resolver(
+    "tag:yaml.org,2002:bool", re.compile(r"^(?:true|True|TRUE|false|False|FALSE)$"), list("tTfF"))
+
+# Every scalar is kept as its source text (what go-yaml does when decoding a
+# scalar into a Go string field); only nulls resolve.
+_RawLoader = _make_loader("_RawLoader", {"tag:yaml.org,2002:null"})
+
+
+def _construct_raw_scalar(loader, node):
+    return node.value
+
+
+for _tag in ("tag:yaml.org,2002:int", "tag:yaml.org,2002:float", "tag:yaml.org,2002:bool",
+             "tag:yaml.org,2002:timestamp"):
+    _RawLoader.add_constructor(_tag, _construct_raw_scalar)
+
+
+def load(text):
+    """Decode like go-yaml v3 into ``interface{}``."""
+    return yaml.load(text, Loader=_TypedLoader)
+
+
+def load_all(text):
+    return list(yaml.load_all(text, Loader=_TypedLoader))
+
+
+def load_raw(text):
+    """Decode keeping scalars as raw strings (for typed struct decoding)."""
+    return yaml.load(text, Loader=_RawLoader)

@@ -1,0 +1,3 @@
+module example.com/hello
+
+go 1.15

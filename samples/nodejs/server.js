@@ -1,0 +1,6 @@
+const http = require("http");
+const port = process.env.PORT || 8080;
+http.createServer((req, res) => {
+  res.writeHead(200, { "Content-Type": "text/plain" });
+  res.end("hello from node\n");
+}).listen(port);
