@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the batched fuzzy-matching path: gfx950 kernel vs the
+native multi-threaded CPU implementation, on a synthetic "CF foundation"
+(N app/buildpack names x M builder buildpack ids).  Prints one JSON line."""
+
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from move2kube_amd.ops import gpu, native  # noqa: E402
+
+
+def words(rng, n, lo, hi):
+    alpha = "abcdefghijklmnopqrstuvwxyz_-0123456789"
+    return ["".join(rng.choice(alpha) for _ in range(rng.randint(lo, hi))) for _ in range(n)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--options", type=int, default=200000)
+    ap.add_argument("--queries", type=int, default=2048)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cpu", action="store_true", help="also time the native CPU path")
+    a = ap.parse_args()
+    rng = random.Random(0)
+    opts = words(rng, a.options, 4, 40)
+    qs = words(rng, a.queries, 4, 64)
+    res = {"options": a.options, "queries": a.queries, "pairs": a.options * a.queries}
+    if gpu.available():
+        gpu.ed_matrix(opts[:1024], qs[:8])  # warm-up / context creation
+        t = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            m = gpu.ed_matrix(opts, qs)
+            t.append(time.perf_counter() - t0)
+        res["gpu_s"] = min(t)
+        res["gpu_gcups"] = sum(len(o) for o in opts) * a.queries / min(t) / 1e9
+        res["arch"] = gpu.device_arch()
+        res["check"] = m[0][0]
+    if a.cpu and native.available():
+        t0 = time.perf_counter()
+        native.module().edit_distance_batch(opts, qs, 1, 1, 2, min(16, os.cpu_count() or 1))
+        res["cpu_native_s"] = time.perf_counter() - t0
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

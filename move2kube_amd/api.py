@@ -1,0 +1,69 @@
+"""In-process programmatic API (what the CLI does, without argv parsing or
+process-global leftovers between runs).  Used by tests, ``bench.py`` and
+embedding applications."""
+
+import os
+
+from . import assets, move2kube, qaengine
+from .containerizer import cnb
+from .containerizer.cnb import providers
+from .models import plan as plantypes
+from .utils import sshkeys
+from .utils.constants import QA_CACHE_FILE, settings
+
+
+def reset_state():
+    """Forget engines, caches and provider probes from a previous run."""
+    qaengine.reset()
+    cnb.reset_cache()
+    providers.reset_providers()
+    sshkeys.reset()
+
+
+class Session:
+    """Assets directory + QA engine setup for one or more runs."""
+
+    def __init__(self, qaskip=True, qacaches=(), ignore_env=True):
+        self.qaskip = qaskip
+        self.qacaches = list(qacaches)
+        self.ignore_env = ignore_env
+        self._temp = None
+
+    def __enter__(self):
+        self._temp = assets.setup()
+        return self
+
+    def __exit__(self, *exc):
+        assets.cleanup(self._temp)
+        return False
+
+    def _start(self):
+        reset_state()
+        settings.ignore_environment = self.ignore_env
+        qaengine.start_engine(self.qaskip, 0, False)
+        qaengine.add_caches(list(reversed(self.qacaches)))
+
+    def plan(self, src, name="myproject"):
+        self._start()
+        return move2kube.create_plan(os.path.abspath(src), name)
+
+    def translate(self, src, outdir, name="myproject", plan=None, curate=True):
+        """``move2kube translate -s src -o outdir -n name`` (new plan unless one is
+        given).  Returns the project output directory."""
+        self._start()
+        if plan is None:
+            p = move2kube.create_plan(os.path.abspath(src), name)
+        else:
+            p = plan if isinstance(plan, plantypes.Plan) else plantypes.read_plan(plan)
+        out = os.path.join(os.path.abspath(outdir), p.name)
+        os.makedirs(out, exist_ok=True)
+        qaengine.set_write_cache(os.path.join(out, QA_CACHE_FILE))
+        if curate:
+            p = move2kube.curate_plan(p)
+        move2kube.translate(p, out, False)
+        return out
+
+
+def translate(src, outdir, name="myproject", qaskip=True, qacaches=()):
+    with Session(qaskip=qaskip, qacaches=qacaches) as s:
+        return s.translate(src, outdir, name)

@@ -387,10 +387,15 @@ _providers = None
 
 
 def providers():
+    """Provider chain dockerAPI -> podman/docker CLI -> pack -> runc.  ``M2K_DISABLE_CNB=1``
+    empties it (deterministic offline runs: benches, golden tests)."""
     global _providers
     with _lock:
         if _providers is None:
-            _providers = [DockerAPIProvider(), ContainerRuntimeProvider(), PackProvider(), RuncProvider()]
+            if os.environ.get("M2K_DISABLE_CNB", "") not in ("", "0"):
+                _providers = []
+            else:
+                _providers = [DockerAPIProvider(), ContainerRuntimeProvider(), PackProvider(), RuncProvider()]
         return _providers
 
 

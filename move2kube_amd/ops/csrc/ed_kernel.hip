@@ -20,6 +20,9 @@
 //  * blockIdx.x is remapped so consecutive option chunks of one query land on
 //    the same XCD (blockIdx % 8 selects the XCD under round-robin dispatch),
 //    keeping that query's slice of the option matrix in one L2.
+//  * results are written query-major ([nB][nA], one coalesced store per wave)
+//    and transposed on the host; queries are launched in slabs of <= 65535
+//    rows so gridDim.y stays within the hardware limit.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -29,10 +32,10 @@
 
 __global__ __launch_bounds__(THREADS) void lcs_dist_kernel(const uint8_t *__restrict__ optsT, const int *__restrict__ lenA,
                                                           const unsigned long long *__restrict__ qmask,
-                                                          const int *__restrict__ lenB, int nA, int nB,
-                                                          int *__restrict__ out) {
+                                                          const int *__restrict__ lenB, int nA, int q0,
+                                                          int *__restrict__ outT) {
   __shared__ unsigned long long M[256];
-  const int q = blockIdx.y;
+  const int q = q0 + blockIdx.y;
   for (int c = threadIdx.x; c < 256; c += THREADS) M[c] = qmask[(size_t)q * 256 + c];
   __syncthreads();
 
@@ -55,7 +58,7 @@ __global__ __launch_bounds__(THREADS) void lcs_dist_kernel(const uint8_t *__rest
       V = (V + U) | (V - U);
     }
     const int lcs = __popcll(~V & mask);
-    out[(size_t)a * nB + q] = la + lb - 2 * lcs;
+    outT[(size_t)q * nA + a] = la + lb - 2 * lcs;  // [query][option]: coalesced across lanes
   }
 }
 
@@ -109,11 +112,24 @@ int m2k_ed_batch(const uint8_t *opts, const int *lenA, int nA, const uint8_t *qu
     int chunks = (nA + THREADS - 1) / THREADS;
     if (chunks > 1024) chunks = 1024;
     if (chunks >= 8) chunks = (chunks / 8) * 8;  // multiple of 8 enables the XCD remap
-    dim3 grid(chunks, nB);
-    hipLaunchKernelGGL(lcs_dist_kernel, grid, dim3(THREADS), 0, 0, dT, dLA, dM, dLB, nA, nB, dOut);
-    if (hipGetLastError() != hipSuccess) rc = -5;
+    for (int q0 = 0; q0 < nB && rc == 0; q0 += 65535) {
+      const int rows = (nB - q0) < 65535 ? (nB - q0) : 65535;
+      dim3 grid(chunks, rows);
+      hipLaunchKernelGGL(lcs_dist_kernel, grid, dim3(THREADS), 0, 0, dT, dLA, dM, dLB, nA, q0, dOut);
+      if (hipGetLastError() != hipSuccess) rc = -5;
+    }
     if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = -6;
-    if (rc == 0) (void)hipMemcpy(out, dOut, sizeof(int) * (size_t)nA * nB, hipMemcpyDeviceToHost);
+    if (rc == 0) {
+      int *hOut = (int *)malloc(sizeof(int) * (size_t)nA * nB);
+      if (!hOut) {
+        rc = -3;
+      } else {
+        (void)hipMemcpy(hOut, dOut, sizeof(int) * (size_t)nA * nB, hipMemcpyDeviceToHost);
+        for (int j = 0; j < nB; j++)
+          for (int i = 0; i < nA; i++) out[(size_t)i * nB + j] = hOut[(size_t)j * nA + i];
+        free(hOut);
+      }
+    }
   }
   (void)hipFree(dT);
   (void)hipFree(dLA);

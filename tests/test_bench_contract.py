@@ -1,0 +1,52 @@
+"""bench.py contract: one JSON line, weak-scaling aggregate over ranks; the
+2-rank run goes through torch.distributed.run with the gloo backend on CPU."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _env():
+    env = dict(os.environ)
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["HIP_VISIBLE_DEVICES"] = ""
+    env["MASTER_ADDR"] = "127.0.0.1"
+    return env
+
+
+def _last_json(stdout):
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only contract test")
+def test_single_rank():
+    p = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1"], cwd=ROOT, env=_env(),
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+    assert p.returncode == 0, p.stderr.decode()
+    d = _last_json(p.stdout.decode())
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 1 and d["value"] > 0
+    assert d["manifest_diff"] == 0
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only contract test")
+def test_two_ranks_gloo():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29533", "bench.py", "--gpus", "2", "--steps", "1",
+           "--warmup", "1"]
+    p = subprocess.run(cmd, cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    d = _last_json(p.stdout.decode())
+    assert d["n_gpus"] == 2
+    assert d["config"]["parallelism"] == "dp2"
+    assert d["scaling"] == "weak"

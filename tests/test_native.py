@@ -1,0 +1,76 @@
+"""The C++ host runtime (``_m2k_native``) against pure-Python references."""
+
+import os
+import random
+
+import pytest
+
+from move2kube_amd.ops import editdistance, native
+from move2kube_amd.source import dockerfile_parser
+from move2kube_amd.utils import common, fsindex
+
+needs_native = pytest.mark.skipif(not native.available(), reason="native extension not built")
+
+
+@needs_native
+def test_walk_matches_python(tmp_path):
+    (tmp_path / "a" / "b").mkdir(parents=True)
+    (tmp_path / "a" / "f.txt").write_text("x")
+    (tmp_path / "a" / "b" / "g.yaml").write_text("y")
+    (tmp_path / "z.yml").write_text("z")
+    os.symlink(str(tmp_path / "z.yml"), str(tmp_path / "link.yml"))
+    paths, kinds, errors = native.module().walk(str(tmp_path))
+    ppaths, pkinds, perrors = fsindex._walk_py(str(tmp_path))
+    assert list(paths) == list(ppaths)
+    assert list(kinds) == list(pkinds)
+    assert list(errors) == list(perrors)
+
+
+@needs_native
+def test_hashes_match_python():
+    rng = random.Random(0)
+    for n in (0, 1, 7, 64, 1000):
+        data = bytes(rng.randrange(256) for _ in range(n))
+        assert native.module().crc64_ecma(data) == common.crc64_ecma_py(data)
+        assert native.module().fnv64a(data) == common.fnv64a_py(data)
+
+
+@needs_native
+def test_edit_distance_batch_matches_python():
+    rng = random.Random(1)
+    words = ["".join(rng.choice("abcde") for _ in range(rng.randint(0, 12))) for _ in range(40)]
+    flat = native.module().edit_distance_batch(words, words[:9], 1, 1, 2, 4)
+    for i, a in enumerate(words):
+        for j, b in enumerate(words[:9]):
+            assert flat[i * 9 + j] == editdistance.wagner_fischer_py(a, b)
+
+
+@needs_native
+def test_sniff_dockerfiles(tmp_path):
+    good = tmp_path / "Dockerfile"
+    good.write_text("# comment\nARG X=1\nFROM alpine:3 AS base\nRUN true\n")
+    bad = tmp_path / "notes.txt"
+    bad.write_text("hello\nFROM nothing\n")
+    arg_only = tmp_path / "args"
+    arg_only.write_text("ARG A\nRUN x\nFROM y\n")
+    got = native.module().sniff_dockerfiles([str(good), str(bad), str(arg_only)], 2)
+    want = [dockerfile_parser.sniff_first_from(str(p)) for p in (good, bad, arg_only)]
+    assert list(got) == want
+    assert got[0] != "" and got[1] == "" and got[2] == ""
+
+
+@needs_native
+def test_run_commands_parallel(tmp_path):
+    argvs = [["/bin/sh", "-c", "printf '%s' \"$(pwd)\""], ["/bin/sh", "-c", "exit 3"], ["/bin/sh", "-c", "echo hi"]]
+    cwds = [str(tmp_path), "", ""]
+    res = native.module().run_commands(argvs, cwds, 3, 0.0)
+    assert res[0][0] == 0 and res[0][1].decode() == str(tmp_path)
+    assert res[1][0] == 3
+    assert res[2] == (0, b"hi\n") or list(res[2]) == [0, b"hi\n"]
+
+
+def test_python_fallback_distance_is_weighted():
+    # sub = 2 = ins + del, so "ab" -> "ac" costs 2
+    assert editdistance.wagner_fischer_py("ab", "ac") == 2
+    assert editdistance.wagner_fischer_py("", "abc") == 3
+    assert editdistance.wagner_fischer_py("kitten", "sitting") == 5
