@@ -31,21 +31,27 @@ def main():
     opts = words(rng, a.options, 4, 40)
     qs = words(rng, a.queries, 4, 64)
     res = {"options": a.options, "queries": a.queries, "pairs": a.options * a.queries}
+    cells = sum(len(o) for o in opts) * a.queries  # option bytes x queries = bit-parallel steps
     if gpu.available():
-        gpu.ed_matrix(opts[:1024], qs[:8])  # warm-up / context creation
-        t = []
-        for _ in range(a.reps):
-            t0 = time.perf_counter()
-            m = gpu.ed_matrix(opts, qs)
-            t.append(time.perf_counter() - t0)
-        res["gpu_s"] = min(t)
-        res["gpu_gcups"] = sum(len(o) for o in opts) * a.queries / min(t) / 1e9
+        gpu.ed_closest(opts[:1024], qs[:8])  # warm-up / context creation
+        for name, fn in (("closest", gpu.ed_closest), ("matrix", gpu.ed_matrix)):
+            t = []
+            for _ in range(a.reps):
+                t0 = time.perf_counter()
+                r = fn(opts, qs)
+                t.append(time.perf_counter() - t0)
+            res["gpu_%s_s" % name] = min(t)
+            res["gpu_%s_gsteps_per_s" % name] = cells / min(t) / 1e9
         res["arch"] = gpu.device_arch()
-        res["check"] = m[0][0]
+        gi, gd = gpu.ed_closest(opts, qs)
     if a.cpu and native.available():
+        th = min(16, os.cpu_count() or 1)
         t0 = time.perf_counter()
-        native.module().edit_distance_batch(opts, qs, 1, 1, 2, min(16, os.cpu_count() or 1))
-        res["cpu_native_s"] = time.perf_counter() - t0
+        ci, cd = native.module().closest_batch(opts, qs, th)
+        res["cpu_native_closest_s"] = time.perf_counter() - t0
+        res["cpu_threads"] = th
+        if gpu.available():
+            res["gpu_cpu_agree"] = bool((gi == ci).all() and (gd == cd).all())
     print(json.dumps(res), flush=True)
 
 

@@ -11,9 +11,11 @@
 //   sniff_dockerfiles()  multi-threaded "first non-ARG instruction" scan
 //   run_commands()       bounded-parallel posix_spawn pool with captured stdout
 //   crc64_ecma/fnv64a    naming hashes (utils.go:292, compose/utils.go:121)
-//   edit_distance_batch  Wagner-Fischer (1,1,2) for fuzzy buildpack matching
+//   edit_distance_batch  weighted edit distance matrix (bit-parallel LCS for 1,1,2)
+//   closest_batch        fused argmin over options for every query
 // All long-running entry points release the GIL.
 
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -341,28 +343,122 @@ int wagner_fischer(const std::string &a, const std::string &b, int icost, int dc
   return row1[b.size()];
 }
 
-// distance matrix [len(as) x len(bs)], row-major
-std::vector<int> edit_distance_batch(const std::vector<std::string> &as, const std::vector<std::string> &bs,
-                                     int icost, int dcost, int scost, int nthreads) {
-  std::vector<int> out(as.size() * bs.size());
-  py::gil_scoped_release nogil;
-  size_t total = out.size();
-  auto work = [&](size_t lo, size_t hi) {
-    for (size_t k = lo; k < hi; k++) out[k] = wagner_fischer(as[k / bs.size()], bs[k % bs.size()], icost, dcost, scost);
-  };
-  if (nthreads <= 1 || total < 4096) {
-    if (total) work(0, total);
-    return out;
+// Bit-parallel LCS (Hyyro): with ins=del=1, sub=2 the weighted distance is
+// |a| + |b| - 2*LCS(a, b).  The query b is encoded once as per-byte match masks
+// over ceil(|b|/64) words; each byte of a then costs ~5 word ops per word.
+struct QueryMasks {
+  int len = 0, words = 0;
+  std::vector<uint64_t> m;  // [256][words]
+};
+
+QueryMasks make_masks(const std::string &b) {
+  QueryMasks q;
+  q.len = (int)b.size();
+  q.words = std::max(1, (q.len + 63) / 64);
+  q.m.assign((size_t)256 * q.words, 0);
+  for (int k = 0; k < q.len; k++) q.m[(size_t)(uint8_t)b[k] * q.words + k / 64] |= (1ULL << (k % 64));
+  return q;
+}
+
+int lcs_distance(const std::string &a, const QueryMasks &q, std::vector<uint64_t> &V) {
+  const int W = q.words;
+  if (W == 1) {
+    uint64_t v = ~0ULL;
+    for (unsigned char ch : a) {
+      const uint64_t u = v & q.m[ch];
+      v = (v + u) | (v - u);
+    }
+    const uint64_t mask = q.len >= 64 ? ~0ULL : ((1ULL << q.len) - 1ULL);
+    return (int)a.size() + q.len - 2 * __builtin_popcountll(~v & mask);
+  }
+  V.assign(W, ~0ULL);
+  for (unsigned char ch : a) {
+    const uint64_t *M = &q.m[(size_t)ch * W];
+    unsigned carry = 0;
+    for (int w = 0; w < W; w++) {
+      const uint64_t v = V[w], u = v & M[w];
+      const uint64_t sum1 = v + u;
+      const unsigned c1 = sum1 < v;
+      const uint64_t sum = sum1 + carry;
+      const unsigned c2 = sum < sum1;
+      carry = c1 | c2;
+      V[w] = sum | (v - u);
+    }
+  }
+  int lcs = 0;
+  for (int w = 0; w < W; w++) {
+    const int bits = std::min(64, q.len - 64 * w);
+    const uint64_t mask = bits >= 64 ? ~0ULL : ((1ULL << bits) - 1ULL);
+    lcs += __builtin_popcountll(~V[w] & mask);
+  }
+  return (int)a.size() + q.len - 2 * lcs;
+}
+
+template <class F>
+void parallel_for(size_t n, int nthreads, size_t grain, F f) {
+  if (nthreads <= 1 || n < grain) {
+    if (n) f(0, n);
+    return;
   }
   std::vector<std::thread> pool;
-  size_t chunk = (total + nthreads - 1) / nthreads;
+  const size_t chunk = (n + nthreads - 1) / nthreads;
   for (int t = 0; t < nthreads; t++) {
-    size_t lo = t * chunk, hi = std::min(total, lo + chunk);
+    const size_t lo = t * chunk, hi = std::min(n, lo + chunk);
     if (lo >= hi) break;
-    pool.emplace_back(work, lo, hi);
+    pool.emplace_back(f, lo, hi);
   }
   for (auto &th : pool) th.join();
-  return out;
+}
+
+// distance matrix [len(as) x len(bs)] as an int32 numpy array
+py::array_t<int32_t> edit_distance_batch(const std::vector<std::string> &as, const std::vector<std::string> &bs,
+                                         int icost, int dcost, int scost, int nthreads) {
+  const size_t na = as.size(), nb = bs.size();
+  py::array_t<int32_t> arr({na, nb});
+  int32_t *out = arr.mutable_data();
+  const bool lcs = (icost == 1 && dcost == 1 && scost == 2);
+  {
+    py::gil_scoped_release nogil;
+    if (lcs) {
+      std::vector<QueryMasks> qm(nb);
+      for (size_t j = 0; j < nb; j++) qm[j] = make_masks(bs[j]);
+      parallel_for(na, nthreads, 64, [&](size_t lo, size_t hi) {
+        std::vector<uint64_t> V;
+        for (size_t i = lo; i < hi; i++)
+          for (size_t j = 0; j < nb; j++) out[i * nb + j] = lcs_distance(as[i], qm[j], V);
+      });
+    } else {
+      parallel_for(na * nb, nthreads, 4096, [&](size_t lo, size_t hi) {
+        for (size_t k = lo; k < hi; k++) out[k] = wagner_fischer(as[k / nb], bs[k % nb], icost, dcost, scost);
+      });
+    }
+  }
+  return arr;
+}
+
+// For every query: (first index of the minimum distance, that distance); (-1, -1) without options.
+std::pair<py::array_t<int32_t>, py::array_t<int32_t>> closest_batch(const std::vector<std::string> &as,
+                                                                    const std::vector<std::string> &bs, int nthreads) {
+  const size_t na = as.size(), nb = bs.size();
+  py::array_t<int32_t> idx(nb), dist(nb);
+  int32_t *pi = idx.mutable_data(), *pd = dist.mutable_data();
+  {
+    py::gil_scoped_release nogil;
+    parallel_for(nb, nthreads, 2, [&](size_t lo, size_t hi) {
+      std::vector<uint64_t> V;
+      for (size_t j = lo; j < hi; j++) {
+        const QueryMasks q = make_masks(bs[j]);
+        int bi = -1, bd = -1;
+        for (size_t i = 0; i < na; i++) {
+          const int d = lcs_distance(as[i], q, V);
+          if (bi < 0 || d < bd) bi = (int)i, bd = d;
+        }
+        pi[j] = bi;
+        pd[j] = bd;
+      }
+    });
+  }
+  return {idx, dist};
 }
 
 // ----------------------------------------------------------------------------
@@ -490,6 +586,7 @@ PYBIND11_MODULE(_m2k_native, m) {
         py::arg("scost") = 2);
   m.def("edit_distance_batch", &edit_distance_batch, py::arg("as"), py::arg("bs"), py::arg("icost") = 1,
         py::arg("dcost") = 1, py::arg("scost") = 2, py::arg("nthreads") = 8);
+  m.def("closest_batch", &closest_batch, py::arg("as"), py::arg("bs"), py::arg("nthreads") = 8);
   m.def("run_commands", &run_commands, py::arg("argvs"), py::arg("cwds"), py::arg("parallel") = 8,
         py::arg("timeout_s") = 0.0);
 }

@@ -8,6 +8,8 @@ builder buildpack lists) are offloaded to the MI355X kernel in
 
 import os
 
+import numpy as np
+
 from . import gpu, native
 
 GPU_MIN_PAIRS = int(os.environ.get("M2K_GPU_MIN_PAIRS", "65536"))
@@ -39,32 +41,65 @@ def wagner_fischer_py(a, b, icost=1, dcost=1, scost=2):
     return row1[len(b)]
 
 
+def _use_gpu(pairs, device, queries):
+    if device == "cpu":
+        return False
+    fits = all(len(q.encode() if isinstance(q, str) else q) <= 64 for q in queries)
+    if device == "gpu":
+        if not fits:
+            raise gpu.GpuUnavailable("queries longer than 64 bytes are not supported on the GPU path")
+        return True
+    return fits and pairs >= GPU_MIN_PAIRS and gpu.gpu_host()
+
+
+def _threads():
+    return max(1, min(16, os.cpu_count() or 1))
+
+
 def matrix(options, queries, device="auto"):
-    """Distance matrix [len(options)][len(queries)].
+    """Distance matrix, int32 array of shape [len(options), len(queries)].
 
     device: "auto" | "cpu" | "gpu"."""
     na, nb = len(options), len(queries)
-    use_gpu = device == "gpu" or (
-        device == "auto" and na * nb >= GPU_MIN_PAIRS and gpu.gpu_host())
-    if use_gpu and all(len(q.encode() if isinstance(q, str) else q) <= 64 for q in queries):
+    if _use_gpu(na * nb, device, queries):
         return gpu.ed_matrix(options, queries)
-    if use_gpu and device == "gpu":
-        raise gpu.GpuUnavailable("queries longer than 64 bytes are not supported on the GPU path")
     m = native.module()
     if m is not None:
-        flat = m.edit_distance_batch(list(options), list(queries), 1, 1, 2, 8)
-        return [flat[i * nb:(i + 1) * nb] for i in range(na)]
-    return [[wagner_fischer_py(o, q) for q in queries] for o in options]
+        return m.edit_distance_batch(list(options), list(queries), 1, 1, 2, _threads())
+    return np.array([[wagner_fischer_py(o, q) for q in queries] for o in options], dtype=np.int32).reshape(na, nb)
+
+
+def closest_indices(options, queries, device="auto"):
+    """For every query the index of the first option with the minimum distance
+    and that distance (int32 arrays; -1 when there are no options).  The argmin
+    is fused into the distance computation (GPU kernel or native CPU)."""
+    na, nb = len(options), len(queries)
+    if na == 0 or nb == 0:
+        return np.full(nb, -1, dtype=np.int32), np.full(nb, -1, dtype=np.int32)
+    if _use_gpu(na * nb, device, queries):
+        return gpu.ed_closest(options, queries)
+    m = native.module()
+    if m is not None:
+        return m.closest_batch(list(options), list(queries), _threads())
+    idx = np.empty(nb, dtype=np.int32)
+    dist = np.empty(nb, dtype=np.int32)
+    for j, q in enumerate(queries):
+        bi, bd = -1, -1
+        for i, o in enumerate(options):
+            d = wagner_fischer_py(o, q)
+            if bi < 0 or d < bd:
+                bi, bd = i, d
+        idx[j], dist[j] = bi, bd
+    return idx, dist
 
 
 def distances(options, search):
     """Distances of each option to one search string."""
-    return [row[0] for row in matrix(options, [search])] if options else []
+    return [int(x) for x in matrix(options, [search])[:, 0]] if options else []
 
 
 def closest(options, search):
-    best, best_d = "", 2 ** 31 - 1
-    for o, d in zip(options, distances(options, search)):
-        if d < best_d:
-            best, best_d = o, d
-    return best
+    if not options:
+        return ""
+    idx, _ = closest_indices(options, [search])
+    return options[int(idx[0])]

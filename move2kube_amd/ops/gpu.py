@@ -9,6 +9,8 @@ callers use the native CPU path.
 import ctypes
 import os
 
+import numpy as np
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libm2k_ed_hip.so")
 
@@ -37,10 +39,13 @@ def _load():
             raise GpuUnavailable("HIP library %s not built (run __graft_entry__.build())" % LIB_PATH)
         return None
     lib = ctypes.CDLL(LIB_PATH)
-    lib.m2k_ed_batch.restype = ctypes.c_int
-    lib.m2k_ed_batch.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
-                                 ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
-                                 ctypes.POINTER(ctypes.c_int)]
+    i64p = ctypes.POINTER(ctypes.c_int64)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    for fn in (lib.m2k_ed_matrix, lib.m2k_ed_closest):
+        fn.restype = ctypes.c_int
+    lib.m2k_ed_matrix.argtypes = [ctypes.c_char_p, i64p, ctypes.c_int, ctypes.c_char_p, i64p, ctypes.c_int, i32p]
+    lib.m2k_ed_closest.argtypes = [ctypes.c_char_p, i64p, ctypes.c_int, ctypes.c_char_p, i64p, ctypes.c_int, i32p,
+                                   i32p]
     lib.m2k_gpu_device_count.restype = ctypes.c_int
     lib.m2k_gpu_arch.restype = ctypes.c_char_p
     _lib = lib
@@ -61,23 +66,60 @@ def device_arch():
     return lib.m2k_gpu_arch().decode() if lib is not None else ""
 
 
-def ed_matrix(options, queries):
-    """Distance matrix [len(options)][len(queries)] computed on the GPU.
+def _pack(strings):
+    """(packed bytes, int64 offsets[n+1], max length)."""
+    bs = [s.encode() if isinstance(s, str) else bytes(s) for s in strings]
+    lens = np.fromiter((len(b) for b in bs), dtype=np.int64, count=len(bs))
+    off = np.zeros(len(bs) + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    return b"".join(bs), off, int(lens.max()) if len(bs) else 0
 
-    Every query must be <= 64 bytes.  Raises GpuUnavailable on failure."""
+
+def _ptr(a, t):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def _lib_or_raise():
     lib = _load()
     if lib is None:
         raise GpuUnavailable("HIP library not available")
-    ob = [o.encode() if isinstance(o, str) else o for o in options]
-    qb = [q.encode() if isinstance(q, str) else q for q in queries]
-    na, nb = len(ob), len(qb)
+    return lib
+
+
+def ed_matrix(options, queries):
+    """Distance matrix, shape [len(options), len(queries)] (int32 numpy view of a
+    query-major device result).  Every query must be <= 64 bytes."""
+    lib = _lib_or_raise()
+    na, nb = len(options), len(queries)
     if na == 0 or nb == 0:
-        return [[0] * nb for _ in range(na)]
-    lena = (ctypes.c_int * na)(*[len(o) for o in ob])
-    lenb = (ctypes.c_int * nb)(*[len(q) for q in qb])
-    out = (ctypes.c_int * (na * nb))()
-    rc = lib.m2k_ed_batch(b"".join(ob), lena, na, b"".join(qb), lenb, nb, out)
+        return np.zeros((na, nb), dtype=np.int32)
+    a, offa, _ = _pack(options)
+    q, offb, qmax = _pack(queries)
+    if qmax > 64:
+        raise GpuUnavailable("queries longer than 64 bytes are not supported on the GPU path")
+    outT = np.empty((nb, na), dtype=np.int32)
+    rc = lib.m2k_ed_matrix(a, _ptr(offa, ctypes.c_int64), na, q, _ptr(offb, ctypes.c_int64), nb,
+                           _ptr(outT, ctypes.c_int32))
     if rc != 0:
-        raise GpuUnavailable("m2k_ed_batch failed with code %d" % rc)
-    flat = list(out)
-    return [flat[i * nb:(i + 1) * nb] for i in range(na)]
+        raise GpuUnavailable("m2k_ed_matrix failed with code %d" % rc)
+    return outT.T
+
+
+def ed_closest(options, queries):
+    """(index, distance) int32 arrays: for every query the first option with the
+    minimum distance (-1, -1 when there are no options)."""
+    lib = _lib_or_raise()
+    na, nb = len(options), len(queries)
+    idx = np.full(nb, -1, dtype=np.int32)
+    dist = np.full(nb, -1, dtype=np.int32)
+    if nb == 0 or na == 0:
+        return idx, dist
+    a, offa, _ = _pack(options)
+    q, offb, qmax = _pack(queries)
+    if qmax > 64:
+        raise GpuUnavailable("queries longer than 64 bytes are not supported on the GPU path")
+    rc = lib.m2k_ed_closest(a, _ptr(offa, ctypes.c_int64), na, q, _ptr(offb, ctypes.c_int64), nb,
+                            _ptr(idx, ctypes.c_int32), _ptr(dist, ctypes.c_int32))
+    if rc != 0:
+        raise GpuUnavailable("m2k_ed_closest failed with code %d" % rc)
+    return idx, dist

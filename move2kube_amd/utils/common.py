@@ -264,17 +264,9 @@ _TOKEN_RE = re.compile(r"[^a-zA-Z0-9]+")
 def get_closest_matching_string(options, search):
     """Option with least Wagner-Fischer distance (ins=1, del=1, sub=2) to ``search``
     after stripping non-alphanumerics and lower-casing (``utils.go:377-401``)."""
-    from ..ops import editdistance
     if not options:
         return ""
-    s = _TOKEN_RE.sub("", search).lower()
-    toks = [_TOKEN_RE.sub("", o).lower() for o in options]
-    dists = editdistance.distances(toks, s)
-    best, best_d = "", 2 ** 31 - 1
-    for o, d in zip(options, dists):
-        if d < best_d:
-            best, best_d = o, d
-    return best
+    return get_closest_matching_strings(options, [search])[0]
 
 
 _FILENAME_INVALID = re.compile(r"[^a-zA-Z0-9\-.]+")
@@ -432,19 +424,12 @@ def go_bool_str(b):
 
 
 def get_closest_matching_strings(options, searches):
-    """Batched :func:`get_closest_matching_string`: one all-pairs distance matrix
-    (GPU-offloaded when large) instead of len(searches) separate scans."""
+    """Batched :func:`get_closest_matching_string`: one fused distance+argmin pass
+    (gfx950 kernel when large, native bit-parallel CPU otherwise)."""
     from ..ops import editdistance
     if not options or not searches:
         return [""] * len(searches)
     toks = [_TOKEN_RE.sub("", o).lower() for o in options]
     qs = [_TOKEN_RE.sub("", s).lower() for s in searches]
-    m = editdistance.matrix(toks, qs)
-    out = []
-    for j in range(len(qs)):
-        best, best_d = "", 2 ** 31 - 1
-        for i, o in enumerate(options):
-            if m[i][j] < best_d:
-                best, best_d = o, m[i][j]
-        out.append(best)
-    return out
+    idx, _ = editdistance.closest_indices(toks, qs)
+    return [options[int(i)] for i in idx]

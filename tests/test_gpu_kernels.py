@@ -1,11 +1,12 @@
-"""Numerics of the gfx950 batched edit-distance kernel vs the plain CPU
+"""Numerics of the gfx950 batched edit-distance kernels vs the plain CPU
 Wagner-Fischer reference (ins=1, del=1, sub=2)."""
 
 import random
 
+import numpy as np
 import pytest
 
-from move2kube_amd.ops import editdistance, gpu
+from move2kube_amd.ops import editdistance, gpu, native
 
 pytestmark = pytest.mark.gpu
 
@@ -14,49 +15,75 @@ def _rand_strings(rng, n, lo, hi, alphabet="abcdefghij_-0123"):
     return ["".join(rng.choice(alphabet) for _ in range(rng.randint(lo, hi))) for _ in range(n)]
 
 
+def _ref_matrix(opts, qs):
+    return np.array([[editdistance.wagner_fischer_py(o, q) for q in qs] for o in opts], dtype=np.int32)
+
+
 def test_gpu_library_loads():
     assert gpu.gpu_host(), "no /dev/kfd on a GPU test run"
     assert gpu.available(), "libm2k_ed_hip.so must load on the GPU box"
     assert gpu.device_arch().startswith("gfx950")
 
 
-def test_ed_kernel_matches_cpu_small():
+def test_ed_matrix_matches_cpu_small():
     rng = random.Random(1)
     opts = _rand_strings(rng, 300, 0, 40) + ["", "x" * 200]
     qs = _rand_strings(rng, 37, 0, 64) + ["", "y" * 64]
     got = gpu.ed_matrix(opts, qs)
-    want = [[editdistance.wagner_fischer_py(o, q) for q in qs] for o in opts]
-    assert got == want
+    assert got.shape == (len(opts), len(qs))
+    assert np.array_equal(got, _ref_matrix(opts, qs))
 
 
-def test_ed_kernel_matches_native_large():
-    from move2kube_amd.ops import native
+def test_ed_matrix_matches_native_large():
     rng = random.Random(7)
-    opts = _rand_strings(rng, 4096, 1, 48, alphabet="abcdefghijklmnopqrstuvwxyz_")
+    opts = _rand_strings(rng, 4096 + 77, 1, 48, alphabet="abcdefghijklmnopqrstuvwxyz_")
     qs = _rand_strings(rng, 96, 1, 64, alphabet="abcdefghijklmnopqrstuvwxyz_")
     got = gpu.ed_matrix(opts, qs)
-    m = native.module()
-    assert m is not None
-    flat = m.edit_distance_batch(opts, qs, 1, 1, 2, 8)
-    want = [flat[i * len(qs):(i + 1) * len(qs)] for i in range(len(opts))]
-    assert got == want
+    want = native.module().edit_distance_batch(opts, qs, 1, 1, 2, 8)
+    assert np.array_equal(got, want)
+
+
+def test_ed_closest_matches_cpu_with_ties():
+    rng = random.Random(11)
+    # few distinct option strings -> many exact ties; the first index must win
+    base = _rand_strings(rng, 40, 1, 20, alphabet="abcd")
+    opts = [base[rng.randrange(len(base))] for _ in range(5000)]
+    qs = _rand_strings(rng, 300, 0, 64, alphabet="abcd")
+    gi, gd = gpu.ed_closest(opts, qs)
+    ci, cd = native.module().closest_batch(opts, qs, 8)
+    assert np.array_equal(gd, cd)
+    assert np.array_equal(gi, ci)
+    for j in (0, 17, 299):
+        row = [editdistance.wagner_fischer_py(o, qs[j]) for o in opts]
+        assert gd[j] == min(row) and gi[j] == row.index(min(row))
+
+
+def test_ed_closest_many_query_slabs():
+    # more than 65535 queries exercises the gridDim.y slabbing
+    rng = random.Random(5)
+    opts = _rand_strings(rng, 64, 1, 12)
+    qs = _rand_strings(rng, 70000, 0, 10)
+    gi, gd = gpu.ed_closest(opts, qs)
+    ci, cd = native.module().closest_batch(opts, qs, 8)
+    assert np.array_equal(gi, ci) and np.array_equal(gd, cd)
 
 
 def test_dispatch_uses_gpu_for_large_batches(monkeypatch):
     calls = []
-    real = gpu.ed_matrix
+    real = gpu.ed_closest
 
     def spy(o, q):
         calls.append((len(o), len(q)))
         return real(o, q)
 
-    monkeypatch.setattr(gpu, "ed_matrix", spy)
+    monkeypatch.setattr(gpu, "ed_closest", spy)
     rng = random.Random(3)
     opts = _rand_strings(rng, 2048, 1, 30)
     qs = _rand_strings(rng, 64, 1, 30)
-    m = editdistance.matrix(opts, qs)
+    idx, dist = editdistance.closest_indices(opts, qs)
     assert calls == [(2048, 64)]
-    assert m[5][7] == editdistance.wagner_fischer_py(opts[5], qs[7])
+    row = [editdistance.wagner_fischer_py(o, qs[7]) for o in opts]
+    assert dist[7] == min(row) and idx[7] == row.index(min(row))
 
 
 def test_closest_matching_strings_gpu_batch():
@@ -64,5 +91,6 @@ def test_closest_matching_strings_gpu_batch():
     opts = ["nodejs_buildpack", "java_buildpack", "python_buildpack", "go_buildpack", "ruby_buildpack"] * 1000
     names = ["node", "javaa", "pythn", "golang", "rubyy"] * 20
     got = common.get_closest_matching_strings(opts, names)
-    want = [common.get_closest_matching_string(opts, n) for n in names]
+    want = [editdistance.closest(opts, n) for n in names]
+    assert got == [opts[0], opts[1], opts[2], opts[3], opts[4]] * 20
     assert got == want

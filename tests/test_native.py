@@ -39,10 +39,10 @@ def test_hashes_match_python():
 def test_edit_distance_batch_matches_python():
     rng = random.Random(1)
     words = ["".join(rng.choice("abcde") for _ in range(rng.randint(0, 12))) for _ in range(40)]
-    flat = native.module().edit_distance_batch(words, words[:9], 1, 1, 2, 4)
+    mat = native.module().edit_distance_batch(words, words[:9], 1, 1, 2, 4)
     for i, a in enumerate(words):
         for j, b in enumerate(words[:9]):
-            assert flat[i * 9 + j] == editdistance.wagner_fischer_py(a, b)
+            assert mat[i][j] == editdistance.wagner_fischer_py(a, b)
 
 
 @needs_native
