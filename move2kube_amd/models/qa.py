@@ -269,6 +269,7 @@ class Cache:
         self.file = file
         self.problems = []
         self._lock = threading.Lock()
+        self._chunks = {}  # id(problem) -> (problem, its to_yaml(), emitted YAML of its list item)
 
     def to_yaml(self):
         d = {}
@@ -299,9 +300,33 @@ class Cache:
         for p in self.problems:
             p.resolved = True
 
+    _ITEM_PREFIX = "spec:\n  solutions:\n"
+
+    def _item_text(self, p):
+        d = p.to_yaml()
+        hit = self._chunks.get(id(p))
+        if hit is not None and hit[0] is p and hit[1] == d:
+            return hit[2]
+        text = yamlio.dump({"spec": {"solutions": [d]}})[len(self._ITEM_PREFIX):]
+        self._chunks[id(p)] = (p, d, text)
+        return text
+
+    def render(self):
+        """The cache file text.  Every solution's list item is emitted once and
+        reused (the reference re-encodes the whole cache on every answer, which
+        makes a QA session quadratic); the result is byte-identical to encoding
+        :meth:`to_yaml` in one go."""
+        if not self.problems:
+            return yamlio.dump(self.to_yaml())
+        head = {k: v for k, v in self.to_yaml().items() if k != "spec"}
+        live = {id(p) for p in self.problems}
+        for k in [k for k in self._chunks if k not in live]:
+            del self._chunks[k]
+        return yamlio.dump(head) + self._ITEM_PREFIX + "".join(self._item_text(p) for p in self.problems)
+
     def write(self):
         try:
-            common.write_text(self.file, yamlio.dump(self.to_yaml()))
+            common.write_text(self.file, self.render())
         except OSError as e:
             log.warning("Unable to write cache : %s", e)
             raise

@@ -1,0 +1,218 @@
+"""In-process evaluation of the built-in containerizer detectors.
+
+Every detector shipped in ``assets/m2kassets`` is a few lines of POSIX sh
+(``test -f``, ``find -name``, a ``*.war`` glob, ``grep -lR __main__``).  Running
+them means fork+exec of ``sh`` plus its ``find``/``wc``/``head`` children for
+every (detector x directory) pair - on a 17-service tree that is ~70% of a
+whole ``translate``.  This module evaluates the *unmodified* built-in scripts
+natively against the already-built directory index and returns exactly the
+exit status and stdout the script prints.
+
+A script is only evaluated in-process when it lives under the unpacked assets
+directory **and** its bytes hash to the packaged original; user-supplied or
+edited detectors (and everything with ``M2K_NATIVE_DETECT=0``) always run as
+real processes through :mod:`move2kube_amd.parallel.detect_pool`.
+
+Known, documented difference: with several ``__main__`` files the python
+detectors report the lexically first one, while ``grep -R`` reports the first
+in readdir order (file-system dependent in the reference too).
+"""
+
+import fnmatch
+import hashlib
+import os
+import re
+
+from ..utils import fsindex
+from ..utils.constants import settings
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ASSETS_SRC = os.path.join(os.path.dirname(_HERE), "assets", "m2kassets")
+
+
+def _exists_file(p):
+    return os.path.isfile(p)
+
+
+def _find_any(src, pattern):
+    """``find "$src"/. -name pattern -print | head -n1 | wc -l`` == 1."""
+    try:
+        idx = fsindex.get_index(src)
+    except (OSError, FileNotFoundError):
+        return False
+    root = idx.root
+    for p in idx.paths:
+        if p == root:
+            continue
+        if fnmatch.fnmatchcase(p.rsplit("/", 1)[-1], pattern):
+            return True
+    return False
+
+
+def _find_main(src):
+    """``grep -lRe __main__ "$src" | awk '/.py$/' | head -n1`` -> relative path."""
+    try:
+        idx = fsindex.get_index(src)
+    except (OSError, FileNotFoundError):
+        return ""
+    rx = re.compile(r".py$")
+    for p, k in zip(idx.paths, idx.kinds):
+        if k == fsindex.DIR:
+            continue
+        shown = src + p[len(idx.root):] if p.startswith(idx.root) else p
+        if not rx.search(shown):
+            continue
+        try:
+            with open(p, "rb") as f:
+                if b"__main__" not in f.read():
+                    continue
+        except OSError:
+            continue
+        try:
+            return os.path.relpath(os.path.realpath(shown), os.path.realpath(src))
+        except ValueError:
+            return ""
+    return ""
+
+
+def _ok(s):
+    return 0, s.encode()
+
+
+_FAIL = (1, b"")
+
+
+def _simple(marker, out):
+    def fn(src):
+        return _ok(out) if _exists_file(os.path.join(src, marker)) else _FAIL
+    return fn
+
+
+def _recursive(pattern, out):
+    def fn(src):
+        return _ok(out) if _find_any(src, pattern) else _FAIL
+    return fn
+
+
+def _war(port):
+    def fn(src):
+        try:
+            wars = sorted(n for n in os.listdir(src) if n.endswith(".war") and not n.startswith("."))
+        except OSError:
+            wars = []
+        # the script's loop exits 1 unless the first (sorted) match exists
+        if not wars or not os.path.exists(os.path.join(src, wars[0])):
+            return _FAIL
+        return _ok('{"port":%d, "war_path":"%s"}' % (port, wars[0]))
+    return fn
+
+
+_PY_MARKERS = ("requirements.txt", "setup.py", "environment.yml", "Pipfile")
+
+
+def _python_df(src):
+    for m in _PY_MARKERS:
+        if _exists_file(os.path.join(src, m)):
+            return _ok('{"main_script_rel_path": "%s", "app_name": "app", "port": 8080}' % _find_main(src))
+    return _FAIL
+
+
+def _python_s2i(src):
+    for m in _PY_MARKERS:
+        if _exists_file(os.path.join(src, m)):
+            return _ok('{"builder": "%s", "app_file": "%s", "app_name": "app", "port": 8080}'
+                       % ("registry.access.redhat.com/rhscl/python-36-rhel7:latest", _find_main(src)))
+    return _FAIL
+
+
+def _golang_s2i(src):
+    if not _exists_file(os.path.join(src, "go.mod")) and not _find_any(src, "*.go"):
+        return _FAIL
+    return _ok('{"builder": "%s", "port": 8080}\n' % "registry.access.redhat.com/ubi8/go-toolset:latest")
+
+
+def _java_s2i(src):
+    if _exists_file(os.path.join(src, "build.gradle")) or _exists_file(os.path.join(src, "build.xml")):
+        return _FAIL
+    if _exists_file(os.path.join(src, "pom.xml")):
+        return _ok('{"builder": "%s", "port": 8080}\n' % "registry.access.redhat.com/jboss-eap-6/eap64-openshift:latest")
+    if not _find_any(src, "*.java"):
+        return _FAIL
+    return _ok('{"builder": "%s", "port": 8080}\n'
+               % "registry.access.redhat.com/redhat-openjdk-18/openjdk18-openshift:latest")
+
+
+DETECTORS = {
+    ("dockerfiles/django", "m2kdfdetect.sh"): _simple("Pipfile", '{"port": 8080, "binding": "0.0.0.0:8080"}\n'),
+    ("dockerfiles/golang", "m2kdfdetect.sh"): _recursive("*.go", '{"port": 8080, "app_name": "app-bin"}\n'),
+    ("dockerfiles/java-war-jboss", "m2kdfdetect.sh"): _war(8080),
+    ("dockerfiles/java-war-liberty", "m2kdfdetect.sh"): _war(9080),
+    ("dockerfiles/java-war-tomcat", "m2kdfdetect.sh"): _war(8080),
+    ("dockerfiles/javaant", "m2kdfdetect.sh"): _simple(
+        "build.xml", '{"port": 8080, "ant_cmd": "ant all", "app_name": "simplewebapp"}\n'),
+    ("dockerfiles/javagradle", "m2kdfdetect.sh"): _simple("build.gradle", '{"port": 8080, "app_name": "simplewebapp"}\n'),
+    ("dockerfiles/javamaven", "m2kdfdetect.sh"): _simple("pom.xml", '{"port": 8080, "app_name": "app"}\n'),
+    ("dockerfiles/nodejs", "m2kdfdetect.sh"): _simple("package.json", '{"port": 8080, "app_name": "app"}\n'),
+    ("dockerfiles/php", "m2kdfdetect.sh"): _recursive(
+        "*.php", '{"port": 8080, "binding": "0.0.0.0:8080", "app_name": "app"}\n'),
+    ("dockerfiles/python", "m2kdfdetect.sh"): _python_df,
+    ("dockerfiles/ruby", "m2kdfdetect.sh"): _simple("Gemfile", '{"port": 8080, "app_name": "app"}\n'),
+    ("s2i/golang", "m2ks2idetect.sh"): _golang_s2i,
+    ("s2i/java", "m2ks2idetect.sh"): _java_s2i,
+    ("s2i/nodejs", "m2ks2idetect.sh"): _simple(
+        "package.json", '{"builder": "%s", "port": 8080}\n' % "registry.access.redhat.com/ubi8/nodejs-10"),
+    ("s2i/php", "m2ks2idetect.sh"): _recursive(
+        "*.php", '{"builder": "%s", "port": 8080}\n' % "registry.access.redhat.com/rhscl/php-72-rhel7:latest"),
+    ("s2i/python", "m2ks2idetect.sh"): _python_s2i,
+    ("s2i/ruby", "m2ks2idetect.sh"): _simple(
+        "Gemfile", '{"builder": "%s", "port": 8080}\n' % "registry.access.redhat.com/rhscl/ruby-25-rhel7:latest"),
+}
+
+
+def _sha(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+_PACKAGED = {}
+for (_rel, _script) in DETECTORS:
+    try:
+        _PACKAGED[(_rel, _script)] = _sha(os.path.join(_ASSETS_SRC, _rel, _script))
+    except OSError:
+        pass
+
+_verified = {}  # (path, mtime_ns, size) -> bool
+
+
+def enabled():
+    return os.environ.get("M2K_NATIVE_DETECT", "1") not in ("0", "")
+
+
+def lookup(script_dir, script):
+    """The in-process implementation for this detector, or None."""
+    if not enabled():
+        return None
+    assets = os.path.abspath(settings.assets_path)
+    d = os.path.abspath(script_dir)
+    if not d.startswith(assets + os.sep):
+        return None
+    rel = os.path.relpath(d, assets)
+    key = (rel, script)
+    fn = DETECTORS.get(key)
+    want = _PACKAGED.get(key)
+    if fn is None or want is None:
+        return None
+    path = os.path.join(d, script)
+    try:
+        st = os.stat(path)
+    except OSError:
+        return None
+    vk = (path, st.st_mtime_ns, st.st_size)
+    ok = _verified.get(vk)
+    if ok is None:
+        try:
+            ok = _sha(path) == want
+        except OSError:
+            ok = False
+        _verified[vk] = ok
+    return fn if ok else None

@@ -8,7 +8,8 @@ native bounded posix_spawn pool (``ops/csrc/m2k_native.cpp:run_commands``,
 GIL released) with ``settings.workers`` concurrent children, results are
 returned in submission order, and results are memoised for the lifetime of the
 enclosing ``fsindex.scope()`` so the translate phase does not re-run detectors
-the plan phase already ran in the same process.
+the plan phase already ran in the same process.  Unmodified built-in detectors
+are evaluated in-process (:mod:`.builtin_detect`) without spawning anything.
 """
 
 import os
@@ -16,6 +17,7 @@ import subprocess
 from concurrent.futures import ThreadPoolExecutor
 
 from ..ops import native
+from . import builtin_detect
 from ..utils import fsindex, log
 from ..utils.constants import settings
 
@@ -63,6 +65,21 @@ def run_detect_jobs(jobs):
         else:
             todo.append(job)
             todo_idx.append(i)
+    if todo:
+        spawn, spawn_idx = [], []
+        for k, (d, script, target) in enumerate(todo):
+            fn = builtin_detect.lookup(d, script)
+            if fn is None:
+                spawn.append(todo[k])
+                spawn_idx.append(k)
+                continue
+            code, out = fn(target)
+            r = DetectResult(code, out.decode("utf-8", "replace"))
+            results[todo_idx[k]] = r
+            if cache is not None:
+                cache[todo[k]] = r
+        todo = spawn
+        todo_idx = [todo_idx[k] for k in spawn_idx]
     if todo:
         if native.available():
             raw = native.run_commands([["/bin/sh", script, target] for (_, script, target) in todo],

@@ -317,8 +317,29 @@ def _single_quoted(s):
 PLAIN, SINGLE, DOUBLE, LITERAL = range(4)
 
 
+# strings that libyaml's analysis always allows as block plain scalars: no
+# indicators, no leading/trailing space, no breaks, printable ASCII only
+_SIMPLE_SCALAR = re.compile(r"[A-Za-z0-9_/](?:[A-Za-z0-9_./ -]*[A-Za-z0-9_./-])?\Z")
+_style_cache = {}
+
+
 def _string_style(s, key=False):
-    """Style go-yaml v3 would emit for a Go string value ``s``."""
+    """Style go-yaml v3 would emit for a Go string value ``s`` (memoised)."""
+    k = (s, key)
+    st = _style_cache.get(k)
+    if st is None:
+        if _SIMPLE_SCALAR.match(s):
+            can_plain = resolves_to_string(s) and not _BASE60.match(s) and s not in _OLD_BOOLS
+            st = PLAIN if can_plain else DOUBLE
+        else:
+            st = _string_style_slow(s, key)
+        if len(_style_cache) > 200000:
+            _style_cache.clear()
+        _style_cache[k] = st
+    return st
+
+
+def _string_style_slow(s, key=False):
     can_plain = resolves_to_string(s) and not _BASE60.match(s) and s not in _OLD_BOOLS
     if "\n" in s:
         style = LITERAL

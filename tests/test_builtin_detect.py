@@ -1,0 +1,70 @@
+"""The in-process built-in detectors must agree with running the real scripts."""
+
+import os
+import shutil
+
+import pytest
+
+from move2kube_amd.parallel import builtin_detect, detect_pool
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _make_tree(base):
+    trees = {
+        "node": {"package.json": "{}"},
+        "py": {"requirements.txt": "x", "app.py": "if __name__ == '__main__':\n  pass\n"},
+        "py_nomain": {"setup.py": "x"},
+        "gomod": {"go.mod": "module x"},
+        "gosrc": {"sub/main.go": "package main"},
+        "war": {"b.war": "x", "a.war": "y"},
+        "mvn": {"pom.xml": "<p/>"},
+        "gradle": {"build.gradle": "", "src/A.java": ""},
+        "javasrc": {"x/y/A.java": ""},
+        "php": {"deep/er/index.php": ""},
+        "ruby": {"Gemfile": ""},
+        "pipenv": {"Pipfile": ""},
+        "ant": {"build.xml": ""},
+        "empty": {},
+        "dotgo": {".hidden.go": ""},
+    }
+    for name, files in trees.items():
+        d = os.path.join(base, name)
+        os.makedirs(d, exist_ok=True)
+        for rel, content in files.items():
+            p = os.path.join(d, rel)
+            os.makedirs(os.path.dirname(p), exist_ok=True)
+            with open(p, "w") as f:
+                f.write(content)
+    return [os.path.join(base, n) for n in sorted(trees)]
+
+
+def test_builtin_matches_scripts(tmp_path, assets_dir, monkeypatch):
+    targets = _make_tree(str(tmp_path / "src"))
+    jobs = []
+    for rel, script in sorted(builtin_detect.DETECTORS):
+        for t in targets:
+            jobs.append((os.path.join(assets_dir, rel), script, t))
+    for job in jobs[:3]:
+        assert builtin_detect.lookup(job[0], job[1]) is not None
+    native_res = detect_pool.run_detect_jobs(jobs)
+    monkeypatch.setenv("M2K_NATIVE_DETECT", "0")
+    assert builtin_detect.lookup(jobs[0][0], jobs[0][1]) is None
+    script_res = detect_pool.run_detect_jobs(jobs)
+    mism = [(j, a.code, a.stdout, b.code, b.stdout) for j, a, b in zip(jobs, native_res, script_res)
+            if (a.code == 0) != (b.code == 0) or (a.code == 0 and a.stdout != b.stdout)]
+    assert mism == []
+
+
+def test_modified_detector_is_not_shortcut(tmp_path, assets_dir):
+    d = os.path.join(assets_dir, "dockerfiles", "nodejs")
+    script = os.path.join(d, "m2kdfdetect.sh")
+    with open(script, "a") as f:
+        f.write("# local edit\n")
+    assert builtin_detect.lookup(d, "m2kdfdetect.sh") is None
+
+
+def test_user_detector_outside_assets_not_shortcut(tmp_path, assets_dir):
+    d = tmp_path / "custom"
+    shutil.copytree(os.path.join(assets_dir, "dockerfiles", "nodejs"), str(d))
+    assert builtin_detect.lookup(str(d), "m2kdfdetect.sh") is None
