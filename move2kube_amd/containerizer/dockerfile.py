@@ -81,7 +81,7 @@ class DockerfileContainerizer(Containerizer):
             template = common.read_text(tpl_path)
         except OSError as e:
             log.error("Unable to read the Dockerfile template at path %r Error: %r", tpl_path, str(e))
-            raise
+            raise ContainerizerError(str(e)) from e
         srcs = service.source_artifacts.get(plantypes.SOURCE_DIRECTORY_ARTIFACT) or []
         if not srcs:
             raise ContainerizerError("Service %s has no source code directory specified" % service.service_name)
@@ -97,7 +97,7 @@ class DockerfileContainerizer(Containerizer):
             except ValueError as e:
                 log.error("Unable to unmarshal the output of the detect script at path %r Output: %r Error: %r",
                           cdir, r.stdout, str(e))
-                raise
+                raise ContainerizerError(str(e)) from e
             port = _port_from(m)
             if port is not None:
                 container.add_exposed_port(port)
@@ -130,5 +130,5 @@ class DockerfileContainerizer(Containerizer):
                 container.add_file(common.go_join(rel, name), common.read_text(f))
             except OSError as e:
                 log.error("Failed to read the file at path %r Error: %r", f, str(e))
-                raise
+                raise ContainerizerError(str(e)) from e
         return container

@@ -46,7 +46,7 @@ class S2IContainerizer(DockerfileContainerizer):
         except ValueError as e:
             log.error("Unable to unmarshal the output of the detect script at path %r Output: %r Error: %r",
                       cdir, r.stdout, str(e))
-            raise
+            raise ContainerizerError(str(e)) from e
         port = _port_from(m)
         if port is not None:
             container.add_exposed_port(port)

@@ -2,5 +2,5 @@
 an interactive CLI, or the HTTP REST API the UI drives) plus a write cache
 that checkpoints every answer."""
 
-from .engine import (add_caches, add_engine, fetch_answer, get_write_cache, reset,  # noqa: F401
+from .engine import (add_caches, add_engine, engines, fetch_answer, get_write_cache, reset,  # noqa: F401
                      set_write_cache, start_engine)
