@@ -9,7 +9,7 @@ from ..k8s import scheme
 from ..models import collection, qa
 from ..models import plan as plantypes
 from ..utils import common, log
-from ..utils.constants import DEFAULT_CLUSTER_TYPE, DEFAULT_STORAGE_CLASS_NAME
+from ..utils.constants import DEFAULT_CLUSTER_TYPE, DEFAULT_STORAGE_CLASS_NAME, settings
 
 
 class Loader:
@@ -61,8 +61,9 @@ class ClusterMDLoader(Loader):
             raise ValueError("Only one of type or path should be specified for the target cluster.")
         key = tpath if tpath else ttype
         cm = clusters.get(key)
-        if cm is None and tpath:
-            # a path target: load that file directly
+        if cm is None and tpath and settings.fixed:
+            # the reference keys clusters by name only, so a path target is never found;
+            # "fixed" compat loads that file directly
             try:
                 cm = _read_cluster_metadata(tpath)
             except Exception:  # noqa: BLE001

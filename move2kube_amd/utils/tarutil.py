@@ -61,6 +61,20 @@ def tar_as_string(path, ignore_files=()):
     return s
 
 
+def _members(tr):
+    """Iterate members, treating a missing end-of-archive trailer as EOF (the
+    reference encodes its tar before closing the writer, so its strings lack
+    the trailer and the last entry's padding)."""
+    while True:
+        try:
+            m = tr.next()
+        except tarfile.ReadError:
+            return
+        if m is None:
+            return
+        yield m
+
+
 def untar_string(tar_string, path):
     try:
         raw = base64.b64decode(tar_string, validate=True)
@@ -69,7 +83,7 @@ def untar_string(tar_string, path):
         raise TarError(str(e))
     root = os.path.abspath(path)
     with tarfile.open(fileobj=io.BytesIO(raw), mode="r:") as tr:
-        for m in tr:
+        for m in _members(tr):
             dst = os.path.abspath(os.path.join(root, m.name))
             if dst != root and not dst.startswith(root + os.sep):
                 raise TarError("tar entry %r escapes the destination" % m.name)
