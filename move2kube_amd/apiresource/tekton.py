@@ -101,7 +101,8 @@ class Pipeline(_PassThrough):
                                      "description": "registry-domain/namespace where the output image should be pushed.",
                                      "type": "string"}],
                          "workspaces": [{"name": irp["workspace_name"],
-                                         "description": "This workspace will receive the cloned git repo and be passed to the kaniko task for building the image."}],
+                                         "description": ("This workspace will receive the cloned git repo and be passed "
+                                                         "to the kaniko task for building the image.")}],
                          "tasks": tasks}}
 
 

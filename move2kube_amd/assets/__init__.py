@@ -73,7 +73,14 @@ def create_assets_data():
         assets_path = os.path.join(temp_path, ASSETS_DIR)
     except OSError:
         log.error("Unable to create temp dir. Defaulting to local path.")
-    _copy_tree(ASSETS_SRC, assets_path)
+    if os.path.isdir(ASSETS_SRC):
+        _copy_tree(ASSETS_SRC, assets_path)
+    else:
+        # single-file / zipapp distributions carry the assets as an embedded tar
+        # (``make generate``), like the reference's go:generate'd asset tar
+        from ..utils import tarutil
+        from . import _embedded_assets  # noqa: F401 - generated module
+        tarutil.untar_string(_embedded_assets.TAR, assets_path)
     return assets_path, temp_path
 
 

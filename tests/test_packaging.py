@@ -1,0 +1,37 @@
+"""Distribution build + installer (reference ``scripts/builddist.go``, ``install.sh``)."""
+
+import os
+import subprocess
+import sys
+import tarfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_builddist_and_install(tmp_path):
+    out = tmp_path / "dist"
+    subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "builddist.py"), "--version", "v0.1.0", "--out", str(out)],
+                   check=True, stdout=subprocess.PIPE)
+    archives = sorted(p for p in os.listdir(str(out)))
+    tgz = [a for a in archives if a.endswith(".tar.gz")][0]
+    assert tgz + ".sha256sum" in archives and any(a.endswith(".zip") for a in archives)
+    with tarfile.open(str(out / tgz)) as t:
+        names = t.getnames()
+    assert any(n.endswith("/bin/move2kube") for n in names)
+    assert any(n.endswith("move2kube_amd/cli/main.py") for n in names)
+    prefix = tmp_path / "prefix"
+    p = subprocess.run(["bash", os.path.join(ROOT, "scripts", "install.sh"), str(out / tgz), str(prefix)],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    assert p.returncode == 0, p.stdout.decode()
+    assert b"v0.1.0" in p.stdout
+
+
+def test_cli_version_and_help():
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    p = subprocess.run([sys.executable, "-m", "move2kube_amd", "version", "-l"], env=env, stdout=subprocess.PIPE, check=True)
+    assert b"version: v0.1.0" in p.stdout
+    p = subprocess.run([sys.executable, "-m", "move2kube_amd", "translate", "--help"], env=env, stdout=subprocess.PIPE,
+                       check=True)
+    for flag in (b"--plan", b"--curate", b"--source", b"--outpath", b"--name", b"--qacache", b"--ignoreenv"):
+        assert flag in p.stdout
+    assert b"--qaskip" not in p.stdout  # hidden like the reference
