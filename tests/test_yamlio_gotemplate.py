@@ -1,0 +1,72 @@
+"""go-yaml v3 emitter and Go text/template semantics the outputs depend on."""
+
+import pytest
+
+from move2kube_amd.utils import gotemplate, yamlio
+
+
+@pytest.mark.parametrize("value,out", [
+    ("plain", "plain"), ("true", '"true"'), ("yes", '"yes"'), ("123", '"123"'), ("1.5", '"1.5"'),
+    ("", '""'), ("a: b", "'a: b'"), ("- x", "'- x'"), ("#c", "'#c'"), (" lead", "' lead'"),
+    ("null", '"null"'), ("~", '"~"'), ("0x1F", '"0x1F"'), ("1e3", '"1e3"'), ("12:30", '"12:30"'),
+    ("2001-12-14", '"2001-12-14"'), ("it's", "it's"), ("{x}", "'{x}'"), ("a\tb", '"a\\tb"'),
+    ("{{ .Release.Name }}-{{ .Values.ingresshost }}", "'{{ .Release.Name }}-{{ .Values.ingresshost }}'"),
+])
+def test_scalar_styles(value, out):
+    assert yamlio.dump({"k": value}) == "k: %s\n" % out
+
+
+def test_literal_blocks():
+    assert yamlio.dump({"k": "a\nb\n"}) == "k: |\n  a\n  b\n"
+    assert yamlio.dump({"k": "a\nb"}) == "k: |-\n  a\n  b\n"
+    assert yamlio.dump({"k": "a\nb\n\n"}) == "k: |+\n  a\n  b\n\n"
+    assert yamlio.dump({"k": "a \nb"}) == 'k: "a \\nb"\n'
+
+
+def test_sequences_indented_and_empty_collections():
+    assert yamlio.dump({"a": [1, 2], "b": {}, "c": [], "d": None}) == "a:\n  - 1\n  - 2\nb: {}\nc: []\nd: null\n"
+
+
+def test_go_map_ordering_and_numbers():
+    d = yamlio.GoMap({"b": 1, "a": 2.5, "a10": 1e-7, "a2": 1000000.0, "A": True})
+    assert yamlio.dump(d) == "A: true\na: 2.5\na2: 1e+06\na10: 1e-07\nb: 1\n"
+
+
+def test_k8s_dump_sorts_all_maps():
+    assert yamlio.dumps_k8s({"z": 1, "a": {"x": 1, "b": 2}}) == "a:\n  b: 2\n  x: 1\nz: 1\n"
+    # go-yaml v3 quotes YAML 1.1 booleans such as "y" even as keys
+    assert yamlio.dumps_k8s({"y": 1}) == '"y": 1\n'
+
+
+def test_loader_is_yaml12ish():
+    d = yamlio.load("a: yes\nb: on\nc: 2001-12-14\nd: 0x10\ne: true\n")
+    assert d == {"a": "yes", "b": "on", "c": "2001-12-14", "d": 16, "e": True}
+
+
+@pytest.mark.parametrize("tpl,data,out", [
+    ("{{ .A }}-{{ .B }}", {"A": 1, "B": "x"}, "1-x"),
+    ("{{- if .A }} yes {{- else }} no {{- end }}", {"A": False}, " no"),
+    ("{{- if .A }} yes {{- else -}} no {{- end }}", {"A": False}, "no"),
+    ("{{ range $k, $v := . }}{{ $k }}={{ $v }};{{ end }}", {"b": 2, "a": 1}, "a=1;b=2;"),
+    ("{{ range . }}[{{ . }}]{{ else }}empty{{ end }}", [], "empty"),
+    ("{{ with .A }}{{ . }}{{ end }}", {"A": "w"}, "w"),
+    ('{{ index .M "k" }}', {"M": {"k": "v"}}, "v"),
+    ("{{ printf \"%s-%d\" .S .N }}", {"S": "s", "N": 3}, "s-3"),
+    ("{{ len .L }}", {"L": [1, 2, 3]}, "3"),
+    ("{{ if and .A (not .B) }}ok{{ end }}", {"A": 1, "B": 0}, "ok"),
+    ("{{ if eq .A \"x\" \"y\" }}ok{{ end }}", {"A": "y"}, "ok"),
+    ("{{/* comment */}}x", {}, "x"),
+    ('{{"{{ .Release.Name }}"}}', {}, "{{ .Release.Name }}"),
+    ("{{ .Missing }}", {}, "<no value>"),
+    ("{{ define \"t\" }}T{{ . }}{{ end }}{{ template \"t\" .X }}", {"X": 1}, "T1"),
+    ("{{ $x := 1 }}{{ if true }}{{ $x = 2 }}{{ end }}{{ $x }}", {}, "2"),
+])
+def test_templates(tpl, data, out):
+    assert gotemplate.render(tpl, data) == out
+
+
+def test_template_errors():
+    with pytest.raises(gotemplate.TemplateError):
+        gotemplate.render("{{ .A", {})
+    with pytest.raises(gotemplate.TemplateError):
+        gotemplate.render("{{ if }}x{{ end }}", {})
