@@ -18,6 +18,13 @@ and ``torch.cuda.synchronize()`` and the slowest rank's time is reported.
 Before timing, rank 0 checks the output of one step against the checked-in
 expected tree (``tests/golden/samples``) and reports ``manifest_diff`` (number
 of differing/missing/extra files; 0 = identical).
+
+After timing, a couple of untimed steps rerun in the reference's execution
+model (every detector forked as ``/bin/sh`` one at a time, as
+``internal/containerizer/dockerfilecontainerizer.go:76-83`` does) and report
+``reference_model_ms_per_step`` - a same-machine proxy for the Go tool, whose
+cost is dominated by those forks; the reference publishes no numbers, so
+``vs_baseline`` stays null.
 """
 
 import argparse
@@ -73,6 +80,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--src", default=SAMPLES)
     ap.add_argument("--keep", action="store_true", help="keep the output directory")
+    ap.add_argument("--reference-model-steps", type=int, default=2,
+                    help="untimed steps in the reference's serial fork-per-detector mode (0 = skip)")
     args = ap.parse_args()
 
     world, rank, local_rank = _dist_env()
@@ -123,6 +132,28 @@ def main():
                 step()
             barrier()
             elapsed = time.perf_counter() - t0
+            # Untimed ablation: the reference's execution model (every detector
+            # forked as a shell process, one at a time), same output required.
+            ref_ms = None
+            if args.reference_model_steps > 0:
+                from move2kube_amd.utils.constants import settings
+                saved = (os.environ.get("M2K_NATIVE_DETECT"), settings.workers)
+                os.environ["M2K_NATIVE_DETECT"] = "0"
+                settings.workers = 1
+                try:
+                    out_ref = step()
+                    t1 = time.perf_counter()
+                    for _ in range(args.reference_model_steps):
+                        step()
+                    ref_ms = (time.perf_counter() - t1) * 1000.0 / args.reference_model_steps
+                    if rank == 0 and diff is not None:
+                        diff += manifest_diff(out_ref, GOLDEN)
+                finally:
+                    if saved[0] is None:
+                        os.environ.pop("M2K_NATIVE_DETECT", None)
+                    else:
+                        os.environ["M2K_NATIVE_DETECT"] = saved[0]
+                    settings.workers = saved[1]
     finally:
         if not args.keep:
             shutil.rmtree(work, ignore_errors=True)
@@ -149,6 +180,8 @@ def main():
             "dtype": "n/a",
             "data": "samples/ corpus (%d services), in-process translate --qaskip, CNB disabled" % n_services,
             "manifest_diff": diff,
+            "reference_model_ms_per_step": None if ref_ms is None else round(ref_ms, 3),
+            "speedup_vs_reference_model": None if not ref_ms else round(ref_ms / ms, 2),
             "config": {"model": "move2kube translate samples/ (full tree)", "global_batch": world,
                        "seq_len": n_services, "parallelism": "dp%d" % world},
         }), flush=True)
