@@ -26,11 +26,12 @@ def main():
     ap.add_argument("--queries", type=int, default=2048)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu", action="store_true", help="also time the native CPU path")
+    ap.add_argument("--qmax", type=int, default=64, help="longest query (buildpack names are mostly <= 32)")
     a = ap.parse_args()
     rng = random.Random(0)
     opts = words(rng, a.options, 4, 40)
-    qs = words(rng, a.queries, 4, 64)
-    res = {"options": a.options, "queries": a.queries, "pairs": a.options * a.queries}
+    qs = words(rng, a.queries, 4, a.qmax)
+    res = {"options": a.options, "queries": a.queries, "qmax": a.qmax, "pairs": a.options * a.queries}
     cells = sum(len(o) for o in opts) * a.queries  # option bytes x queries = bit-parallel steps
     if gpu.available():
         gpu.ed_closest(opts[:1024], qs[:8])  # warm-up / context creation

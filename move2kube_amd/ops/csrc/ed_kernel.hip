@@ -12,25 +12,34 @@
 // bit-parallel LCS: one 64-bit word holds the DP column for a query of up to 64
 // bytes, and every character of the option costs one LDS lookup + 4 integer ops.
 //
-// Layout (CDNA4-first):
-//  * Options are sorted by length on the host and cut into panels of 256 (one
-//    workgroup = 4 wave64s).  A panel is stored transposed [panelMaxLen][256]:
-//    the k-th character load of a wave is one coalesced 64-byte read, lanes of
-//    a wave have near-equal lengths (no divergence), and padding is bounded by
-//    the length spread inside a panel instead of by the global maximum.
-//  * blockIdx.y = query; the query's 256-entry match-mask table (2 KiB) is
-//    staged once into LDS and shared by the 4 waves.
-//  * blockIdx.x walks panels, remapped so consecutive panels of one query land
-//    on the same XCD (blockIdx % 8 selects the XCD under round-robin dispatch),
-//    keeping that query's slice of the option panels in one L2.
-//  * ed_matrix kernel: results go to a query-major [nB][nA] matrix (Python
+// Layout (CDNA4-first; tuned from rocprofv3 PMC, see profiles/):
+//  * Byte remap.  The host assigns every byte value that occurs a dense code,
+//    most frequent option byte first, code 0 = padding, and (when <= 63
+//    symbols occur) stores code*4 - the byte offset into the u32 mask table -
+//    so turning a character into an LDS address is one VALU op.  M[0] = 0,
+//    so a padding code leaves the LCS column unchanged: no per-character
+//    length checks.
+//  * Width.  Queries of <= 32 bytes run a 32-bit LCS column (u32 table,
+//    `ds_read_b32`, one VALU op per and/add/sub/or): per character ~5 VALU ops
+//    instead of ~11 for the 64-bit column.  PMC of v2 showed the kernel at
+//    ~1 VALU wave-instruction per CU-cycle, i.e. VALU-bound, so this is the
+//    lever that matters.
+//  * Options are sorted by length and cut into panels of 512 (256 threads x 2
+//    options each: two independent dependency chains per lane hide the
+//    LDS-lookup -> VALU latency).  A panel is stored as 16-byte blocks
+//    [block][slot]: one `global_load_dwordx4` gives a lane its next 16
+//    characters (1 KiB per wave instruction), and the next block is prefetched
+//    while the current one is consumed (v1 waited on one byte load per char).
+//  * blockIdx.y = query; the query's 256-entry mask table (2 KiB) is staged in
+//    LDS once per workgroup.  blockIdx.x walks panels, remapped so consecutive
+//    panels of one query land on the same XCD (blockIdx % 8 picks the XCD).
+//  * ed_matrix kernel: distances go to a query-major [nB][nA] matrix (Python
 //    returns the transposed view, so no host transpose).
-//  * ed_closest kernel: the argmin over options is fused into the producer -
-//    key = (dist << 32 | original_index) is min-reduced across the wave with
-//    cross-lane shuffles, then across the 4 waves in LDS, then with one 64-bit
-//    atomicMin per workgroup - so only nB (index, dist) pairs ever leave the
-//    GPU.  Ties resolve to the lowest original index, matching the
-//    reference's strict "<" scan.
+//  * ed_closest kernel: the argmin is fused into the producer - key =
+//    (dist << 32 | original_index) is min-reduced across the wave with
+//    shuffles, across the 4 waves in LDS, then one 64-bit atomicMin per
+//    workgroup, so only nB (index, dist) pairs leave the GPU.  Ties resolve to
+//    the lowest original index, matching the reference's strict "<" scan.
 //  * queries are launched in slabs of <= 65535 rows (gridDim.y limit).
 
 #include <hip/hip_runtime.h>
@@ -43,65 +52,101 @@
 #include <vector>
 
 #define THREADS 256
+#define OPT_PER_THREAD 2
+#define SLOTS (THREADS * OPT_PER_THREAD)
 #define MAX_Y 65535
+
+typedef unsigned long long u64;
 
 namespace {
 
-struct Panels {
-  std::vector<uint8_t> data;      // concatenated transposed panels
-  std::vector<int64_t> panelOff;  // byte offset of each panel in data
-  std::vector<int> panelLen;      // max option length of each panel
-  std::vector<int> perm;          // sorted position -> original option index
+struct Prepared {
+  std::vector<uint4> data;        // panels: [block][slot] of 16 coded chars
+  std::vector<int64_t> panelOff;  // uint4 offset of each panel
+  std::vector<int> panelBlocks;   // 16-char blocks in each panel
+  std::vector<int> perm;          // sorted position -> original option index (-1 = padding slot)
   std::vector<int> lenSorted;     // option length in sorted order
+  std::vector<u64> M;             // [nB][256] match masks indexed by code
+  std::vector<int> lenB;
+  int nPanels = 0;
+  int scaled = 0;  // panel bytes hold code*4 (the byte offset into a u32 table) when <= 63 symbols
 };
 
-void build_panels(const uint8_t *opts, const int64_t *offA, int nA, Panels &P) {
-  P.perm.resize(nA);
-  std::iota(P.perm.begin(), P.perm.end(), 0);
-  std::stable_sort(P.perm.begin(), P.perm.end(),
-                   [&](int x, int y) { return (offA[x + 1] - offA[x]) < (offA[y + 1] - offA[y]); });
-  const int nPanels = (nA + THREADS - 1) / THREADS;
-  P.panelOff.resize(nPanels + 1);
-  P.panelLen.resize(nPanels);
-  P.lenSorted.assign((size_t)nPanels * THREADS, 0);
-  int64_t total = 0;
-  for (int p = 0; p < nPanels; p++) {
-    int ml = 0;
-    for (int l = 0; l < THREADS; l++) {
-      const int s = p * THREADS + l;
-      if (s >= nA) break;
-      const int o = P.perm[s];
-      const int len = (int)(offA[o + 1] - offA[o]);
-      P.lenSorted[s] = len;
-      ml = len > ml ? len : ml;
-    }
-    P.panelLen[p] = ml;
-    P.panelOff[p] = total;
-    total += (int64_t)ml * THREADS;
-  }
-  P.panelOff[nPanels] = total;
-  P.data.assign((size_t)(total > 0 ? total : 1), 0);
-  for (int p = 0; p < nPanels; p++) {
-    uint8_t *base = P.data.data() + P.panelOff[p];
-    for (int l = 0; l < THREADS; l++) {
-      const int s = p * THREADS + l;
-      if (s >= nA) break;
-      const uint8_t *src = opts + offA[P.perm[s]];
-      const int len = P.lenSorted[s];
-      for (int k = 0; k < len; k++) base[(size_t)k * THREADS + l] = src[k];
-    }
-  }
+// Dense codes ranked by option-byte frequency; 0 is reserved for padding.
+// Returns false when all 256 byte values occur (no free code for padding).
+// *nsym = number of symbols in use (codes 1..nsym).
+bool build_code_map(const uint8_t *opts, int64_t nOptBytes, const uint8_t *qs, int64_t nQBytes, uint8_t code[256],
+                    int *nsym) {
+  int64_t freq[256] = {0};
+  bool seen[256] = {false};
+  for (int64_t i = 0; i < nOptBytes; i++) freq[opts[i]]++, seen[opts[i]] = true;
+  for (int64_t i = 0; i < nQBytes; i++) seen[qs[i]] = true;
+  int order[256];
+  int n = 0;
+  for (int b = 0; b < 256; b++)
+    if (seen[b]) order[n++] = b;
+  if (n > 255) return false;
+  std::stable_sort(order, order + n, [&](int x, int y) { return freq[x] > freq[y]; });
+  memset(code, 0, 256);
+  for (int i = 0; i < n; i++) code[order[i]] = (uint8_t)(i + 1);
+  *nsym = n;
+  return true;
 }
 
-int build_masks(const uint8_t *qs, const int64_t *offB, int nB, std::vector<unsigned long long> &M,
-                std::vector<int> &lenB) {
-  M.assign((size_t)nB * 256, 0ULL);
-  lenB.resize(nB);
+int prepare(const uint8_t *opts, const int64_t *offA, int nA, const uint8_t *qs, const int64_t *offB, int nB,
+            Prepared &P) {
+  for (int j = 0; j < nB; j++) {
+    const int64_t len = offB[j + 1] - offB[j];
+    if (len < 0 || len > 64) return -2;
+  }
+  uint8_t code[256];
+  int nsym = 0;
+  if (!build_code_map(opts, offA[nA], qs, offB[nB], code, &nsym)) return -8;
+  P.scaled = nsym <= 63;
+  uint8_t stored[256];
+  for (int b = 0; b < 256; b++) stored[b] = P.scaled ? (uint8_t)(code[b] * 4) : code[b];
+
+  P.M.assign((size_t)nB * 256, 0ULL);
+  P.lenB.resize(nB);
   for (int j = 0; j < nB; j++) {
     const int len = (int)(offB[j + 1] - offB[j]);
-    if (len < 0 || len > 64) return -2;
-    lenB[j] = len;
-    for (int k = 0; k < len; k++) M[(size_t)j * 256 + qs[offB[j] + k]] |= (1ULL << k);
+    P.lenB[j] = len;
+    for (int k = 0; k < len; k++) P.M[(size_t)j * 256 + code[qs[offB[j] + k]]] |= (1ULL << k);
+  }
+
+  std::vector<int> order(nA);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int x, int y) { return (offA[x + 1] - offA[x]) < (offA[y + 1] - offA[y]); });
+  P.nPanels = (nA + SLOTS - 1) / SLOTS;
+  P.perm.assign((size_t)P.nPanels * SLOTS, -1);
+  P.lenSorted.assign((size_t)P.nPanels * SLOTS, 0);
+  P.panelOff.resize(P.nPanels + 1);
+  P.panelBlocks.resize(P.nPanels);
+  int64_t total = 0;
+  for (int p = 0; p < P.nPanels; p++) {
+    int ml = 0;
+    for (int s = 0; s < SLOTS && p * SLOTS + s < nA; s++) {
+      const int o = order[p * SLOTS + s];
+      const int len = (int)(offA[o + 1] - offA[o]);
+      P.perm[p * SLOTS + s] = o;
+      P.lenSorted[p * SLOTS + s] = len;
+      ml = len > ml ? len : ml;
+    }
+    P.panelBlocks[p] = (ml + 15) / 16;
+    P.panelOff[p] = total;
+    total += (int64_t)P.panelBlocks[p] * SLOTS;
+  }
+  P.panelOff[P.nPanels] = total;
+  P.data.assign((size_t)(total > 0 ? total : 1), make_uint4(0, 0, 0, 0));
+  for (int p = 0; p < P.nPanels; p++) {
+    uint8_t *base = reinterpret_cast<uint8_t *>(P.data.data() + P.panelOff[p]);
+    for (int s = 0; s < SLOTS && p * SLOTS + s < nA; s++) {
+      const int o = P.perm[p * SLOTS + s];
+      const uint8_t *src = opts + offA[o];
+      const int len = P.lenSorted[p * SLOTS + s];
+      for (int k = 0; k < len; k++) base[((size_t)(k / 16) * SLOTS + s) * 16 + (k % 16)] = stored[src[k]];
+    }
   }
   return 0;
 }
@@ -112,72 +157,145 @@ __device__ __forceinline__ int remap_panel(int bx, int n) {
   return (bx % 8) * per + (bx / 8);
 }
 
-__device__ __forceinline__ int lcs_dist(const uint8_t *__restrict__ col, int len, const unsigned long long *M, int lb,
-                                        unsigned long long mask) {
-  unsigned long long V = ~0ULL;
-  for (int k = 0; k < len; k++) {
-    const unsigned long long U = V & M[col[(size_t)k * THREADS]];
+// One 32-bit word = 4 coded characters.  Byte i holds either the code (SCALED=0)
+// or code*4 (SCALED=1, a ready-made byte offset into the u32 table; the u64
+// table offset is twice that), so extracting a character is one VALU op.
+template <typename W, bool SCALED>
+__device__ __forceinline__ void step4(uint32_t w, const W *M, W &V) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t c = (w >> (8 * i)) & 0xffu;
+    const uint32_t off = SCALED ? c * (uint32_t)(sizeof(W) / 4) : c * (uint32_t)sizeof(W);
+    const W m = *reinterpret_cast<const W *>(reinterpret_cast<const char *>(M) + off);
+    const W U = V & m;
     V = (V + U) | (V - U);
   }
-  return len + lb - 2 * __popcll(~V & mask);
+}
+
+// LCS columns of this lane's OPT_PER_THREAD options in panel p.
+template <typename W, bool SCALED>
+__device__ __forceinline__ void panel_lcs(const uint4 *__restrict__ panel, int blocks, const W *M,
+                                          W (&V)[OPT_PER_THREAD]) {
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < OPT_PER_THREAD; u++) V[u] = ~(W)0;
+  if (blocks == 0) return;
+  uint4 cur[OPT_PER_THREAD], nxt[OPT_PER_THREAD];
+#pragma unroll
+  for (int u = 0; u < OPT_PER_THREAD; u++) cur[u] = panel[u * THREADS + lane];
+  for (int b = 0; b < blocks; b++) {
+    if (b + 1 < blocks) {
+#pragma unroll
+      for (int u = 0; u < OPT_PER_THREAD; u++) nxt[u] = panel[(size_t)(b + 1) * SLOTS + u * THREADS + lane];
+    }
+    // interleave the two independent chains word by word
+    step4<W, SCALED>(cur[0].x, M, V[0]);
+    step4<W, SCALED>(cur[1].x, M, V[1]);
+    step4<W, SCALED>(cur[0].y, M, V[0]);
+    step4<W, SCALED>(cur[1].y, M, V[1]);
+    step4<W, SCALED>(cur[0].z, M, V[0]);
+    step4<W, SCALED>(cur[1].z, M, V[1]);
+    step4<W, SCALED>(cur[0].w, M, V[0]);
+    step4<W, SCALED>(cur[1].w, M, V[1]);
+#pragma unroll
+    for (int u = 0; u < OPT_PER_THREAD; u++) cur[u] = nxt[u];
+  }
+}
+
+// Distances of this lane's options in panel p to the query whose masks are in
+// LDS; queries of <= 32 bytes run the 32-bit column (half the VALU work).
+template <bool SCALED>
+__device__ __forceinline__ void panel_dists(const uint4 *__restrict__ panel, int blocks, const uint32_t *M32,
+                                            const u64 *M64, int lb, int (&lcs)[OPT_PER_THREAD]) {
+  if (lb <= 32) {
+    uint32_t V[OPT_PER_THREAD];
+    panel_lcs<uint32_t, SCALED>(panel, blocks, M32, V);
+    const uint32_t mask = (lb >= 32) ? ~0u : ((1u << lb) - 1u);
+#pragma unroll
+    for (int u = 0; u < OPT_PER_THREAD; u++) lcs[u] = __popc(~V[u] & mask);
+  } else {
+    u64 V[OPT_PER_THREAD];
+    panel_lcs<u64, SCALED>(panel, blocks, M64, V);
+    const u64 mask = (lb >= 64) ? ~0ULL : ((1ULL << lb) - 1ULL);
+#pragma unroll
+    for (int u = 0; u < OPT_PER_THREAD; u++) lcs[u] = __popcll(~V[u] & mask);
+  }
 }
 
 }  // namespace
 
-__global__ __launch_bounds__(THREADS) void ed_matrix_kernel(const uint8_t *__restrict__ panels,
+template <bool SCALED>
+__global__ __launch_bounds__(THREADS) void ed_matrix_kernel(const uint4 *__restrict__ panels,
                                                             const int64_t *__restrict__ panelOff,
+                                                            const int *__restrict__ panelBlocks,
                                                             const int *__restrict__ lenSorted,
-                                                            const int *__restrict__ perm,
-                                                            const unsigned long long *__restrict__ qmask,
+                                                            const int *__restrict__ perm, const u64 *__restrict__ qmask,
                                                             const int *__restrict__ lenB, int nA, int nPanels, int q0,
                                                             int *__restrict__ outT) {
-  __shared__ unsigned long long M[256];
+  __shared__ u64 M64[256];
+  __shared__ uint32_t M32[256];
   const int q = q0 + blockIdx.y;
-  for (int c = threadIdx.x; c < 256; c += THREADS) M[c] = qmask[(size_t)q * 256 + c];
+  for (int c = threadIdx.x; c < 256; c += THREADS) {
+    const u64 m = qmask[(size_t)q * 256 + c];
+    M64[c] = m;
+    M32[c] = (uint32_t)m;
+  }
   __syncthreads();
   const int lb = lenB[q];
-  const unsigned long long mask = (lb >= 64) ? ~0ULL : ((1ULL << lb) - 1ULL);
   for (int p = remap_panel(blockIdx.x, gridDim.x); p < nPanels; p += gridDim.x) {
-    const int s = p * THREADS + threadIdx.x;
-    if (s < nA) {
-      const int d = lcs_dist(panels + panelOff[p] + threadIdx.x, lenSorted[s], M, lb, mask);
-      outT[(size_t)q * nA + perm[s]] = d;
+    int lcs[OPT_PER_THREAD];
+    panel_dists<SCALED>(panels + panelOff[p], panelBlocks[p], M32, M64, lb, lcs);
+#pragma unroll
+    for (int u = 0; u < OPT_PER_THREAD; u++) {
+      const int s = p * SLOTS + u * THREADS + threadIdx.x;
+      const int o = perm[s];
+      if (o >= 0) outT[(size_t)q * nA + o] = lenSorted[s] + lb - 2 * lcs[u];
     }
   }
 }
 
-__global__ __launch_bounds__(THREADS) void ed_closest_kernel(const uint8_t *__restrict__ panels,
+template <bool SCALED>
+__global__ __launch_bounds__(THREADS) void ed_closest_kernel(const uint4 *__restrict__ panels,
                                                              const int64_t *__restrict__ panelOff,
+                                                             const int *__restrict__ panelBlocks,
                                                              const int *__restrict__ lenSorted,
                                                              const int *__restrict__ perm,
-                                                             const unsigned long long *__restrict__ qmask,
-                                                             const int *__restrict__ lenB, int nA, int nPanels, int q0,
-                                                             unsigned long long *__restrict__ best) {
-  __shared__ unsigned long long M[256];
-  __shared__ unsigned long long red[THREADS / 64];
+                                                             const u64 *__restrict__ qmask, const int *__restrict__ lenB,
+                                                             int nPanels, int q0, u64 *__restrict__ best) {
+  __shared__ u64 M64[256];
+  __shared__ uint32_t M32[256];
+  __shared__ u64 red[THREADS / 64];
   const int q = q0 + blockIdx.y;
-  for (int c = threadIdx.x; c < 256; c += THREADS) M[c] = qmask[(size_t)q * 256 + c];
+  for (int c = threadIdx.x; c < 256; c += THREADS) {
+    const u64 m = qmask[(size_t)q * 256 + c];
+    M64[c] = m;
+    M32[c] = (uint32_t)m;
+  }
   __syncthreads();
   const int lb = lenB[q];
-  const unsigned long long mask = (lb >= 64) ? ~0ULL : ((1ULL << lb) - 1ULL);
-  unsigned long long key = ~0ULL;
+  u64 key = ~0ULL;
   for (int p = remap_panel(blockIdx.x, gridDim.x); p < nPanels; p += gridDim.x) {
-    const int s = p * THREADS + threadIdx.x;
-    if (s < nA) {
-      const int d = lcs_dist(panels + panelOff[p] + threadIdx.x, lenSorted[s], M, lb, mask);
-      const unsigned long long k = ((unsigned long long)(unsigned)d << 32) | (unsigned)perm[s];
-      key = k < key ? k : key;
+    int lcs[OPT_PER_THREAD];
+    panel_dists<SCALED>(panels + panelOff[p], panelBlocks[p], M32, M64, lb, lcs);
+#pragma unroll
+    for (int u = 0; u < OPT_PER_THREAD; u++) {
+      const int s = p * SLOTS + u * THREADS + threadIdx.x;
+      const int o = perm[s];
+      if (o >= 0) {
+        const int d = lenSorted[s] + lb - 2 * lcs[u];
+        const u64 k = ((u64)(unsigned)d << 32) | (unsigned)o;
+        key = k < key ? k : key;
+      }
     }
   }
-  // wave64 min-reduction
   for (int off = 32; off > 0; off >>= 1) {
-    const unsigned long long o = __shfl_xor(key, off, 64);
+    const u64 o = __shfl_xor(key, off, 64);
     key = o < key ? o : key;
   }
   if ((threadIdx.x & 63) == 0) red[threadIdx.x / 64] = key;
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long k = red[0];
+    u64 k = red[0];
     for (int w = 1; w < THREADS / 64; w++) k = red[w] < k ? red[w] : k;
     if (k != ~0ULL) atomicMin(&best[q], k);
   }
@@ -186,13 +304,14 @@ __global__ __launch_bounds__(THREADS) void ed_closest_kernel(const uint8_t *__re
 namespace {
 
 struct Dev {
-  uint8_t *panels = nullptr;
+  uint4 *panels = nullptr;
   int64_t *panelOff = nullptr;
-  int *lenSorted = nullptr, *perm = nullptr, *lenB = nullptr;
-  unsigned long long *M = nullptr;
+  int *panelBlocks = nullptr, *lenSorted = nullptr, *perm = nullptr, *lenB = nullptr;
+  u64 *M = nullptr;
   ~Dev() {
     (void)hipFree(panels);
     (void)hipFree(panelOff);
+    (void)hipFree(panelBlocks);
     (void)hipFree(lenSorted);
     (void)hipFree(perm);
     (void)hipFree(lenB);
@@ -200,27 +319,22 @@ struct Dev {
   }
 };
 
-int upload(const Panels &P, const std::vector<unsigned long long> &M, const std::vector<int> &lenB, Dev &d) {
-  const size_t nPanels = P.panelLen.size();
-  if (hipMalloc(&d.panels, P.data.size()) != hipSuccess ||
-      hipMalloc(&d.panelOff, sizeof(int64_t) * (nPanels + 1)) != hipSuccess ||
-      hipMalloc(&d.lenSorted, sizeof(int) * P.lenSorted.size()) != hipSuccess ||
-      hipMalloc(&d.perm, sizeof(int) * P.perm.size()) != hipSuccess ||
-      hipMalloc(&d.lenB, sizeof(int) * lenB.size()) != hipSuccess ||
-      hipMalloc(&d.M, sizeof(unsigned long long) * M.size()) != hipSuccess)
-    return -4;
-  if (hipMemcpy(d.panels, P.data.data(), P.data.size(), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d.panelOff, P.panelOff.data(), sizeof(int64_t) * (nPanels + 1), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d.lenSorted, P.lenSorted.data(), sizeof(int) * P.lenSorted.size(), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d.perm, P.perm.data(), sizeof(int) * P.perm.size(), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d.lenB, lenB.data(), sizeof(int) * lenB.size(), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d.M, M.data(), sizeof(unsigned long long) * M.size(), hipMemcpyHostToDevice) != hipSuccess)
+template <class T>
+bool up(T **dst, const std::vector<T> &src) {
+  const size_t bytes = sizeof(T) * (src.empty() ? 1 : src.size());
+  if (hipMalloc(dst, bytes) != hipSuccess) return false;
+  return src.empty() || hipMemcpy(*dst, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice) == hipSuccess;
+}
+
+int upload(const Prepared &P, Dev &d) {
+  if (!up(&d.panels, P.data) || !up(&d.panelOff, P.panelOff) || !up(&d.panelBlocks, P.panelBlocks) ||
+      !up(&d.lenSorted, P.lenSorted) || !up(&d.perm, P.perm) || !up(&d.lenB, P.lenB) || !up(&d.M, P.M))
     return -4;
   return 0;
 }
 
 int grid_x(int nPanels, int nB) {
-  // >> 256 CUs worth of workgroups in total, x a multiple of 8 for the XCD remap
+  // >> 256 CUs worth of workgroups in total; x a multiple of 8 for the XCD remap
   int x = nPanels;
   const int want = (nB >= 2048) ? 8 : (nB >= 256 ? 64 : 1024);
   if (x > want) x = want;
@@ -240,23 +354,23 @@ int m2k_ed_matrix(const uint8_t *opts, const int64_t *offA, int nA, const uint8_
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -1;
   if (nA <= 0 || nB <= 0) return 0;
-  std::vector<unsigned long long> M;
-  std::vector<int> lenB;
-  int rc = build_masks(qs, offB, nB, M, lenB);
+  Prepared P;
+  int rc = prepare(opts, offA, nA, qs, offB, nB, P);
   if (rc) return rc;
-  Panels P;
-  build_panels(opts, offA, nA, P);
-  const int nPanels = (int)P.panelLen.size();
   Dev d;
   int *dOut = nullptr;
-  rc = upload(P, M, lenB, d);
+  rc = upload(P, d);
   if (rc == 0 && hipMalloc(&dOut, sizeof(int) * (size_t)nA * nB) != hipSuccess) rc = -4;
   if (rc == 0) {
-    const int gx = grid_x(nPanels, nB);
+    const int gx = grid_x(P.nPanels, nB);
     for (int q0 = 0; q0 < nB && rc == 0; q0 += MAX_Y) {
       const int rows = (nB - q0) < MAX_Y ? (nB - q0) : MAX_Y;
-      hipLaunchKernelGGL(ed_matrix_kernel, dim3(gx, rows), dim3(THREADS), 0, 0, d.panels, d.panelOff, d.lenSorted,
-                         d.perm, d.M, d.lenB, nA, nPanels, q0, dOut);
+      if (P.scaled)
+        hipLaunchKernelGGL(ed_matrix_kernel<true>, dim3(gx, rows), dim3(THREADS), 0, 0, d.panels, d.panelOff,
+                           d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, nA, P.nPanels, q0, dOut);
+      else
+        hipLaunchKernelGGL(ed_matrix_kernel<false>, dim3(gx, rows), dim3(THREADS), 0, 0, d.panels, d.panelOff,
+                           d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, nA, P.nPanels, q0, dOut);
       if (hipGetLastError() != hipSuccess) rc = -5;
     }
     if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = -6;
@@ -277,30 +391,30 @@ int m2k_ed_closest(const uint8_t *opts, const int64_t *offA, int nA, const uint8
     for (int j = 0; j < nB; j++) bestIdx[j] = -1, bestDist[j] = -1;
     return 0;
   }
-  std::vector<unsigned long long> M;
-  std::vector<int> lenB;
-  int rc = build_masks(qs, offB, nB, M, lenB);
+  Prepared P;
+  int rc = prepare(opts, offA, nA, qs, offB, nB, P);
   if (rc) return rc;
-  Panels P;
-  build_panels(opts, offA, nA, P);
-  const int nPanels = (int)P.panelLen.size();
   Dev d;
-  unsigned long long *dBest = nullptr;
-  rc = upload(P, M, lenB, d);
-  if (rc == 0 && hipMalloc(&dBest, sizeof(unsigned long long) * nB) != hipSuccess) rc = -4;
-  if (rc == 0 && hipMemset(dBest, 0xff, sizeof(unsigned long long) * nB) != hipSuccess) rc = -4;
+  u64 *dBest = nullptr;
+  rc = upload(P, d);
+  if (rc == 0 && hipMalloc(&dBest, sizeof(u64) * nB) != hipSuccess) rc = -4;
+  if (rc == 0 && hipMemset(dBest, 0xff, sizeof(u64) * nB) != hipSuccess) rc = -4;
   if (rc == 0) {
-    const int gx = grid_x(nPanels, nB);
+    const int gx = grid_x(P.nPanels, nB);
     for (int q0 = 0; q0 < nB && rc == 0; q0 += MAX_Y) {
       const int rows = (nB - q0) < MAX_Y ? (nB - q0) : MAX_Y;
-      hipLaunchKernelGGL(ed_closest_kernel, dim3(gx, rows), dim3(THREADS), 0, 0, d.panels, d.panelOff, d.lenSorted,
-                         d.perm, d.M, d.lenB, nA, nPanels, q0, dBest);
+      if (P.scaled)
+        hipLaunchKernelGGL(ed_closest_kernel<true>, dim3(gx, rows), dim3(THREADS), 0, 0, d.panels, d.panelOff,
+                           d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, P.nPanels, q0, dBest);
+      else
+        hipLaunchKernelGGL(ed_closest_kernel<false>, dim3(gx, rows), dim3(THREADS), 0, 0, d.panels, d.panelOff,
+                           d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, P.nPanels, q0, dBest);
       if (hipGetLastError() != hipSuccess) rc = -5;
     }
     if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = -6;
     if (rc == 0) {
-      std::vector<unsigned long long> h(nB);
-      if (hipMemcpy(h.data(), dBest, sizeof(unsigned long long) * nB, hipMemcpyDeviceToHost) != hipSuccess) rc = -7;
+      std::vector<u64> h(nB);
+      if (hipMemcpy(h.data(), dBest, sizeof(u64) * nB, hipMemcpyDeviceToHost) != hipSuccess) rc = -7;
       for (int j = 0; j < nB && rc == 0; j++) {
         bestIdx[j] = (int32_t)(h[j] & 0xffffffffULL);
         bestDist[j] = (int32_t)(h[j] >> 32);

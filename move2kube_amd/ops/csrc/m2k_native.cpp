@@ -436,6 +436,31 @@ py::array_t<int32_t> edit_distance_batch(const std::vector<std::string> &as, con
   return arr;
 }
 
+// Pack a list of str/bytes into one buffer + int64 offsets[n+1] (the layout the
+// GPU kernel library consumes), without building n Python bytes objects.
+std::pair<py::bytes, py::array_t<int64_t>> pack_strings(const py::list &items) {
+  const size_t n = items.size();
+  py::array_t<int64_t> off(n + 1);
+  int64_t *po = off.mutable_data();
+  std::string buf;
+  po[0] = 0;
+  for (size_t i = 0; i < n; i++) {
+    PyObject *o = items[i].ptr();
+    if (PyUnicode_Check(o)) {
+      Py_ssize_t len = 0;
+      const char *s = PyUnicode_AsUTF8AndSize(o, &len);
+      if (!s) throw py::error_already_set();
+      buf.append(s, (size_t)len);
+    } else if (PyBytes_Check(o)) {
+      buf.append(PyBytes_AS_STRING(o), (size_t)PyBytes_GET_SIZE(o));
+    } else {
+      throw py::type_error("pack_strings: items must be str or bytes");
+    }
+    po[i + 1] = (int64_t)buf.size();
+  }
+  return {py::bytes(buf), off};
+}
+
 // For every query: (first index of the minimum distance, that distance); (-1, -1) without options.
 std::pair<py::array_t<int32_t>, py::array_t<int32_t>> closest_batch(const std::vector<std::string> &as,
                                                                     const std::vector<std::string> &bs, int nthreads) {
@@ -586,6 +611,7 @@ PYBIND11_MODULE(_m2k_native, m) {
         py::arg("scost") = 2);
   m.def("edit_distance_batch", &edit_distance_batch, py::arg("as"), py::arg("bs"), py::arg("icost") = 1,
         py::arg("dcost") = 1, py::arg("scost") = 2, py::arg("nthreads") = 8);
+  m.def("pack_strings", &pack_strings, py::arg("items"));
   m.def("closest_batch", &closest_batch, py::arg("as"), py::arg("bs"), py::arg("nthreads") = 8);
   m.def("run_commands", &run_commands, py::arg("argvs"), py::arg("cwds"), py::arg("parallel") = 8,
         py::arg("timeout_s") = 0.0);

@@ -62,7 +62,11 @@ def matrix(options, queries, device="auto"):
     device: "auto" | "cpu" | "gpu"."""
     na, nb = len(options), len(queries)
     if _use_gpu(na * nb, device, queries):
-        return gpu.ed_matrix(options, queries)
+        try:
+            return gpu.ed_matrix(options, queries)
+        except gpu.GpuUnsupportedInput:
+            if device == "gpu":
+                raise
     m = native.module()
     if m is not None:
         return m.edit_distance_batch(list(options), list(queries), 1, 1, 2, _threads())
@@ -77,7 +81,11 @@ def closest_indices(options, queries, device="auto"):
     if na == 0 or nb == 0:
         return np.full(nb, -1, dtype=np.int32), np.full(nb, -1, dtype=np.int32)
     if _use_gpu(na * nb, device, queries):
-        return gpu.ed_closest(options, queries)
+        try:
+            return gpu.ed_closest(options, queries)
+        except gpu.GpuUnsupportedInput:
+            if device == "gpu":
+                raise
     m = native.module()
     if m is not None:
         return m.closest_batch(list(options), list(queries), _threads())

@@ -22,6 +22,13 @@ class GpuUnavailable(RuntimeError):
     pass
 
 
+class GpuUnsupportedInput(GpuUnavailable):
+    """The kernel cannot take this input (query > 64 bytes, all 256 byte values used)."""
+
+
+_RC_UNSUPPORTED = (-2, -8)
+
+
 def gpu_host():
     """True on a host exposing an AMD GPU to this process."""
     if os.environ.get("M2K_FORCE_CPU"):
@@ -68,6 +75,11 @@ def device_arch():
 
 def _pack(strings):
     """(packed bytes, int64 offsets[n+1], max length)."""
+    from . import native
+    m = native.module()
+    if m is not None and isinstance(strings, list):
+        data, off = m.pack_strings(strings)
+        return data, off, int(np.diff(off).max()) if len(strings) else 0
     bs = [s.encode() if isinstance(s, str) else bytes(s) for s in strings]
     lens = np.fromiter((len(b) for b in bs), dtype=np.int64, count=len(bs))
     off = np.zeros(len(bs) + 1, dtype=np.int64)
@@ -96,10 +108,12 @@ def ed_matrix(options, queries):
     a, offa, _ = _pack(options)
     q, offb, qmax = _pack(queries)
     if qmax > 64:
-        raise GpuUnavailable("queries longer than 64 bytes are not supported on the GPU path")
+        raise GpuUnsupportedInput("queries longer than 64 bytes are not supported on the GPU path")
     outT = np.empty((nb, na), dtype=np.int32)
     rc = lib.m2k_ed_matrix(a, _ptr(offa, ctypes.c_int64), na, q, _ptr(offb, ctypes.c_int64), nb,
                            _ptr(outT, ctypes.c_int32))
+    if rc in _RC_UNSUPPORTED:
+        raise GpuUnsupportedInput("m2k_ed_matrix cannot take this input (code %d)" % rc)
     if rc != 0:
         raise GpuUnavailable("m2k_ed_matrix failed with code %d" % rc)
     return outT.T
@@ -117,9 +131,11 @@ def ed_closest(options, queries):
     a, offa, _ = _pack(options)
     q, offb, qmax = _pack(queries)
     if qmax > 64:
-        raise GpuUnavailable("queries longer than 64 bytes are not supported on the GPU path")
+        raise GpuUnsupportedInput("queries longer than 64 bytes are not supported on the GPU path")
     rc = lib.m2k_ed_closest(a, _ptr(offa, ctypes.c_int64), na, q, _ptr(offb, ctypes.c_int64), nb,
                             _ptr(idx, ctypes.c_int32), _ptr(dist, ctypes.c_int32))
+    if rc in _RC_UNSUPPORTED:
+        raise GpuUnsupportedInput("m2k_ed_closest cannot take this input (code %d)" % rc)
     if rc != 0:
         raise GpuUnavailable("m2k_ed_closest failed with code %d" % rc)
     return idx, dist

@@ -94,3 +94,28 @@ def test_closest_matching_strings_gpu_batch():
     want = [editdistance.closest(opts, n) for n in names]
     assert got == [opts[0], opts[1], opts[2], opts[3], opts[4]] * 20
     assert got == want
+
+
+def test_all_byte_values_fall_back_to_cpu():
+    # every byte value in use leaves no code for padding: the kernel refuses and
+    # the dispatcher answers on the CPU
+    base = [bytes(range(i, min(256, i + 32))) for i in range(0, 256, 32)]
+    opts = base * 3000
+    qs = [bytes([1, 2, 3]), bytes([250, 251])] * 20
+    with pytest.raises(gpu.GpuUnsupportedInput):
+        gpu.ed_closest(opts, qs)
+    idx, dist = editdistance.closest_indices(opts, qs)
+    for j in (0, 1):
+        row = [editdistance.wagner_fischer_py(o, qs[j]) for o in base]
+        assert dist[j] == min(row) and idx[j] == row.index(min(row))
+
+
+def test_uneven_lengths_and_padding_slots():
+    # nA not a multiple of the 512-option panel, lengths spanning many 16-byte blocks
+    rng = random.Random(9)
+    opts = _rand_strings(rng, 1537, 0, 200, alphabet="ab")
+    qs = _rand_strings(rng, 33, 0, 64, alphabet="abc")
+    assert np.array_equal(gpu.ed_matrix(opts, qs), _ref_matrix(opts, qs))
+    gi, gd = gpu.ed_closest(opts, qs)
+    ci, cd = native.module().closest_batch(opts, qs, 8)
+    assert np.array_equal(gi, ci) and np.array_equal(gd, cd)
