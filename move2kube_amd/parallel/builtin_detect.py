@@ -18,7 +18,6 @@ detectors report the lexically first one, while ``grep -R`` reports the first
 in readdir order (file-system dependent in the reference too).
 """
 
-import fnmatch
 import hashlib
 import os
 import re
@@ -40,13 +39,7 @@ def _find_any(src, pattern):
         idx = fsindex.get_index(src)
     except (OSError, FileNotFoundError):
         return False
-    root = idx.root
-    for p in idx.paths:
-        if p == root:
-            continue
-        if fnmatch.fnmatchcase(p.rsplit("/", 1)[-1], pattern):
-            return True
-    return False
+    return idx.has_match(pattern)
 
 
 def _find_main(src):

@@ -67,8 +67,11 @@ def run_detect_jobs(jobs):
             todo_idx.append(i)
     if todo:
         spawn, spawn_idx = [], []
+        fns = {}
         for k, (d, script, target) in enumerate(todo):
-            fn = builtin_detect.lookup(d, script)
+            if (d, script) not in fns:
+                fns[(d, script)] = builtin_detect.lookup(d, script)
+            fn = fns[(d, script)]
             if fn is None:
                 spawn.append(todo[k])
                 spawn_idx.append(k)

@@ -64,15 +64,51 @@ def scoped_cache(name):
 
 
 class FileIndex:
-    """The result of one ``filepath.Walk``-equivalent traversal."""
+    """The result of one ``filepath.Walk``-equivalent traversal.
 
-    __slots__ = ("root", "paths", "kinds", "errors")
+    Walk order is depth-first pre-order with sorted names, so every
+    directory's subtree is one contiguous range of ``paths``.  Sub-indexes are
+    sliced out of that range (no rescans) and remember their offset in the
+    base index, which lets recursive "any entry named like X below here?"
+    queries use one precomputed position list per pattern (``has_match``).
+    """
 
-    def __init__(self, root, paths, kinds, errors):
+    __slots__ = ("root", "paths", "kinds", "errors", "base", "lo", "_pos", "_end", "_match", "_by_ext", "_by_name")
+
+    def __init__(self, root, paths, kinds, errors, base=None, lo=0):
         self.root = root
         self.paths = paths
         self.kinds = kinds
         self.errors = errors
+        self.base = base
+        self.lo = lo
+        self._pos = None
+        self._end = None
+        self._match = None
+        self._by_ext = None
+        self._by_name = None
+
+    def _file_maps(self):
+        """ext -> [positions], basename -> [positions] of non-directories (one pass)."""
+        if self._by_ext is None:
+            by_ext, by_name = {}, {}
+            for i, (p, k) in enumerate(zip(self.paths, self.kinds)):
+                if k == DIR:
+                    continue
+                base = p.rsplit("/", 1)[-1]
+                j = base.rfind(".")
+                by_ext.setdefault(base[j:] if j >= 0 else "", []).append(i)
+                by_name.setdefault(base, []).append(i)
+            self._by_ext, self._by_name = by_ext, by_name
+        return self._by_ext, self._by_name
+
+    def _select(self, table, keys):
+        pos = []
+        for key in keys:
+            pos.extend(table.get(key, ()))
+        if len(keys) > 1:
+            pos.sort()
+        return [self.paths[i] for i in pos]
 
     def files(self):
         return [p for p, k in zip(self.paths, self.kinds) if k != DIR]
@@ -81,41 +117,62 @@ class FileIndex:
         return [p for p, k in zip(self.paths, self.kinds) if k == DIR]
 
     def files_by_ext(self, exts):
-        exts = list(exts)
-        out = []
-        for p, k in zip(self.paths, self.kinds):
-            if k == DIR:
-                continue
-            base = p.rsplit("/", 1)[-1]
-            i = base.rfind(".")
-            ext = base[i:] if i >= 0 else ""
-            for e in exts:
-                if ext == e:
-                    out.append(p)
-        return out
+        """Non-directories whose extension (Go ``filepath.Ext``) is in ``exts``, in walk order."""
+        return self._select(self._file_maps()[0], list(dict.fromkeys(exts)))
 
     def files_by_name(self, names):
-        names = list(names)
-        out = []
-        for p, k in zip(self.paths, self.kinds):
-            if k == DIR:
-                continue
-            base = p.rsplit("/", 1)[-1]
-            for n in names:
-                if base == n:
-                    out.append(p)
-        return out
+        """Non-directories whose base name is in ``names``, in walk order."""
+        return self._select(self._file_maps()[1], list(dict.fromkeys(names)))
+
+    # -- subtree ranges -------------------------------------------------------
+    def _positions(self):
+        if self._pos is None:
+            self._pos = {p: i for i, p in enumerate(self.paths)}
+        return self._pos
+
+    def _ends(self):
+        """end[i] = one past the last descendant of entry i."""
+        if self._end is None:
+            n = len(self.paths)
+            end = list(range(1, n + 1))
+            stack = []  # (prefix, index) of open directories
+            for i, (p, k) in enumerate(zip(self.paths, self.kinds)):
+                while stack and not p.startswith(stack[-1][0]):
+                    end[stack.pop()[1]] = i
+                if k == DIR:
+                    stack.append((p.rstrip("/") + "/", i))
+            for _, j in stack:
+                end[j] = n
+            self._end = end
+        return self._end
 
     def sub_index(self, sub_root):
         """Listing of a sub-directory derived from this index (no new walk)."""
+        i = self._positions().get(sub_root)
+        if i is None:
+            return FileIndex(sub_root, [], [], [], self.base or self, self.lo)
+        j = self._ends()[i]
         prefix = sub_root.rstrip("/") + "/"
-        paths, kinds = [], []
-        for p, k in zip(self.paths, self.kinds):
-            if p == sub_root or p.startswith(prefix):
-                paths.append(p)
-                kinds.append(k)
         errors = [e for e in self.errors if e[0] == sub_root or e[0].startswith(prefix)]
-        return FileIndex(sub_root, paths, kinds, errors)
+        return FileIndex(sub_root, self.paths[i:j], self.kinds[i:j], errors, self.base or self, self.lo + i)
+
+    def has_match(self, pattern, include_root=False):
+        """True if some entry of this index (other than its root unless asked)
+        has a basename matching the shell ``pattern`` (``find -name``)."""
+        import bisect
+        import fnmatch
+        base = self.base or self
+        if base._match is None:
+            base._match = {}
+        pos = base._match.get(pattern)
+        if pos is None:
+            rx = __import__("re").compile(fnmatch.translate(pattern))
+            pos = [i for i, p in enumerate(base.paths) if rx.match(p.rsplit("/", 1)[-1])]
+            base._match[pattern] = pos
+        lo = self.lo if include_root else self.lo + 1
+        hi = self.lo + len(self.paths)
+        k = bisect.bisect_left(pos, lo)
+        return k < len(pos) and pos[k] < hi
 
 
 def _walk_py(root):
@@ -184,8 +241,15 @@ def get_index(root):
     idx = cache.get(root)
     if idx is not None:
         return idx
-    for r, parent in cache.items():
-        if root.startswith(r.rstrip("/") + "/"):
+    # nearest cached ancestor (O(depth) lookups instead of scanning the cache)
+    anc = root
+    while True:
+        parent_dir = os.path.dirname(anc)
+        if parent_dir == anc:
+            break
+        anc = parent_dir
+        parent = cache.get(anc)
+        if parent is not None:
             idx = parent.sub_index(root)
             cache[root] = idx
             return idx
