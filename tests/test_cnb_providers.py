@@ -1,0 +1,132 @@
+"""CNB provider chain against fakes: a Docker Engine API served on a unix
+socket, and stub podman / pack executables."""
+
+import json
+import os
+import socketserver
+import threading
+from http.server import BaseHTTPRequestHandler
+
+import pytest
+
+from move2kube_amd.containerizer.cnb import providers
+
+STUBS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "stubbin")
+LABEL = json.dumps([{"group": [{"id": "google.nodejs.runtime"}, {"id": "google.go.runtime"}]}])
+
+
+class _FakeDockerd(BaseHTTPRequestHandler):
+    state = {}
+
+    def log_message(self, *a):
+        pass
+
+    def _json(self, code, obj):
+        data = json.dumps(obj).encode()
+        self.send_response(code)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(data)))
+        self.end_headers()
+        self.wfile.write(data)
+
+    def do_POST(self):  # noqa: N802
+        n = int(self.headers.get("Content-Length") or 0)
+        body = self.rfile.read(n) if n else b""
+        if self.path.startswith("/images/create"):
+            return self._json(200, {"status": "pulled"})
+        if self.path == "/containers/create":
+            cfg = json.loads(body or b"{}")
+            cid = "c%d" % len(self.state)
+            mounts = (cfg.get("HostConfig") or {}).get("Mounts") or []
+            src = mounts[0]["Source"] if mounts else ""
+            self.state[cid] = 0 if (cfg.get("Image") == "hello-world" or os.path.exists(os.path.join(src, "package.json"))) else 1
+            return self._json(201, {"Id": cid})
+        if self.path.endswith("/start"):
+            return self._json(204, {})
+        if "/wait" in self.path:
+            cid = self.path.split("/")[2]
+            return self._json(200, {"StatusCode": self.state.get(cid, 1)})
+        return self._json(404, {"message": "no"})
+
+    def do_GET(self):  # noqa: N802
+        if "/logs" in self.path:
+            return self._json(200, "detected")
+        if self.path.startswith("/images/") and self.path.endswith("/json"):
+            return self._json(200, {"Config": {"Labels": {providers.ORDER_LABEL: LABEL}}})
+        return self._json(404, {"message": "no"})
+
+    def do_DELETE(self):  # noqa: N802
+        return self._json(204, {})
+
+
+class _UnixServer(socketserver.ThreadingMixIn, socketserver.UnixStreamServer):
+    daemon_threads = True
+
+    def get_request(self):
+        req, _ = super().get_request()
+        return req, ("local", 0)
+
+
+@pytest.fixture
+def fake_dockerd(tmp_path, monkeypatch):
+    sock = str(tmp_path / "docker.sock")
+    srv = _UnixServer(sock, _FakeDockerd)
+    t = threading.Thread(target=srv.serve_forever, daemon=True)
+    t.start()
+    monkeypatch.setenv("DOCKER_HOST", "unix://" + sock)
+    yield sock
+    srv.shutdown()
+    srv.server_close()
+
+
+def test_docker_api_provider(fake_dockerd, tmp_path):
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "package.json").write_text("{}")
+    other = tmp_path / "other"
+    other.mkdir()
+    p = providers.DockerAPIProvider()
+    assert p.is_sock_accessible()
+    assert p.is_builder_supported(str(app), "gcr.io/buildpacks/builder") is True
+    assert p.is_builder_supported(str(other), "gcr.io/buildpacks/builder") is False
+    assert p.get_all_buildpacks(["gcr.io/buildpacks/builder"]) == {
+        "gcr.io/buildpacks/builder": ["google.nodejs.runtime", "google.go.runtime"]}
+
+
+def test_podman_provider(monkeypatch, tmp_path):
+    monkeypatch.setenv("PATH", STUBS + os.pathsep + "/usr/bin:/bin")
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "package.json").write_text("{}")
+    p = providers.ContainerRuntimeProvider()
+    assert p.get_runtime() == "podman"
+    assert p.is_builder_supported(str(app), "b") is True
+    assert p.is_builder_supported(str(tmp_path), "b") is False
+    assert p.get_all_buildpacks(["b"]) == {"b": ["org.cloudfoundry.nodejs", "org.cloudfoundry.go"]}
+
+
+def test_pack_provider(monkeypatch, tmp_path):
+    monkeypatch.setenv("PATH", STUBS + os.pathsep + "/usr/bin:/bin")
+    monkeypatch.setattr(providers, "DOCKER_SOCK", str(tmp_path / "sock"))
+    (tmp_path / "sock").write_text("")
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "package.json").write_text("{}")
+    p = providers.PackProvider()
+    assert p.is_builder_supported(str(app), "b") is True
+    assert p.is_builder_supported(str(tmp_path), "b") is False
+    assert p.get_all_buildpacks(["b"]) == {"b": ["paketo-buildpacks/nodejs", "paketo-buildpacks/java"]}
+
+
+def test_chain_falls_through_to_first_working_provider(monkeypatch, tmp_path):
+    monkeypatch.delenv("M2K_DISABLE_CNB", raising=False)
+    monkeypatch.setenv("DOCKER_HOST", "unix://" + str(tmp_path / "missing.sock"))
+    monkeypatch.setenv("PATH", STUBS + os.pathsep + "/usr/bin:/bin")
+    providers.reset_providers()
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "package.json").write_text("{}")
+    try:
+        assert providers.is_builder_supported(str(app), "b") is True  # docker API fails -> podman answers
+    finally:
+        providers.reset_providers()
