@@ -110,8 +110,9 @@ def get_missing_variables(path):
     doc = _load(path)
     names = set()
     _var_names(doc, names)
-    # an interpolated document must still decode as a manifest
-    _decode_manifest(_evaluate(doc, {n: "" for n in names}))
+    if not names:
+        # interpolation succeeded, so the manifest itself must decode
+        _decode_manifest(doc)
     return sorted(names)
 
 
