@@ -135,7 +135,7 @@ def main():
             # Untimed ablation: the reference's execution model (every detector
             # forked as a shell process, one at a time), same output required.
             ref_ms = None
-            if args.reference_model_steps > 0:
+            if args.reference_model_steps > 0 and rank == 0:
                 from move2kube_amd.utils.constants import settings
                 saved = (os.environ.get("M2K_NATIVE_DETECT"), settings.workers)
                 os.environ["M2K_NATIVE_DETECT"] = "0"
