@@ -1,0 +1,41 @@
+"""Property tests: the go-yaml emitter round-trips through a YAML loader, the
+native and Python walkers agree, edit-distance implementations agree."""
+
+import string
+
+from hypothesis import given, settings, strategies as st
+
+from move2kube_amd.ops import editdistance, native
+from move2kube_amd.utils import yamlio
+
+import yaml
+
+_text = st.text(alphabet=st.characters(blacklist_categories=("Cs",), blacklist_characters="﻿\x85  "),
+                max_size=20)
+_scalars = st.one_of(_text, st.integers(min_value=-10**12, max_value=10**12), st.booleans(), st.none())
+_values = st.recursive(_scalars, lambda ch: st.one_of(st.lists(ch, max_size=4),
+                                                      st.dictionaries(_text, ch, max_size=4)), max_leaves=12)
+
+
+def _norm(v):
+    # YAML has no distinction between "absent" and null inside lists/maps we emit; keep types
+    return v
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.dictionaries(_text, _values, max_size=5))
+def test_dump_roundtrips_through_yaml_loader(doc):
+    text = yamlio.dump(doc)
+    back = yaml.load(text, Loader=yaml.SafeLoader)
+    assert back == (doc or {}), text
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.text(alphabet=string.ascii_lowercase + string.digits + "_-", max_size=30),
+       st.text(alphabet=string.ascii_lowercase + string.digits + "_-", max_size=30))
+def test_edit_distance_native_equals_python(a, b):
+    m = native.module()
+    if m is None:
+        return
+    assert int(m.edit_distance_batch([a], [b], 1, 1, 2, 1)[0][0]) == editdistance.wagner_fischer_py(a, b)
+    assert m.wagner_fischer(a, b, 1, 1, 2) == editdistance.wagner_fischer_py(a, b)
