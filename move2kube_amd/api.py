@@ -8,7 +8,7 @@ from . import assets, move2kube, qaengine
 from .containerizer import cnb
 from .containerizer.cnb import providers
 from .models import plan as plantypes
-from .utils import sshkeys
+from .utils import sshkeys, yamlio
 from .utils.constants import QA_CACHE_FILE, settings
 
 
@@ -45,12 +45,17 @@ class Session:
 
     def plan(self, src, name="myproject"):
         self._start()
-        return move2kube.create_plan(os.path.abspath(src), name)
+        with yamlio.parse_cache():
+            return move2kube.create_plan(os.path.abspath(src), name)
 
     def translate(self, src, outdir, name="myproject", plan=None, curate=True):
         """``move2kube translate -s src -o outdir -n name`` (new plan unless one is
         given).  Returns the project output directory."""
         self._start()
+        with yamlio.parse_cache():
+            return self._translate(src, outdir, name, plan, curate)
+
+    def _translate(self, src, outdir, name, plan, curate):
         if plan is None:
             p = move2kube.create_plan(os.path.abspath(src), name)
         else:

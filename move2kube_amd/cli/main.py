@@ -11,7 +11,7 @@ import sys
 
 from .. import assets, move2kube, qaengine
 from ..models import plan as plantypes
-from ..utils import log
+from ..utils import log, yamlio
 from ..utils.constants import (APP_NAME_SHORT, DEFAULT_DIRECTORY_PERMISSION, DEFAULT_PLAN_FILE, DEFAULT_PROJECT_NAME,
                                QA_CACHE_FILE, settings)
 
@@ -203,7 +203,8 @@ def main(argv=None):
         log.error("Unable to create the assets directory. Error: %r", str(e))
         return 1
     try:
-        a.func(a)
+        with yamlio.parse_cache():  # one command = one parse of each YAML document
+            a.func(a)
     except log.FatalError:
         return 1
     finally:

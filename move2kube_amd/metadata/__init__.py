@@ -2,7 +2,6 @@
 (built-in profiles + collected ClusterMetadata), Kubernetes YAMLs to carry over
 as cached objects, and QA caches found in the source tree."""
 
-import copy
 
 from .. import assets, qaengine
 from ..k8s import scheme
@@ -77,8 +76,9 @@ class ClusterMDLoader(Loader):
         clusters = {}
         for name, prof in assets.builtin_clusters().items():
             cm = collection.ClusterMetadata(name)
+            # kind -> [group/version]: a one-level copy is a full copy
             cm.spec = collection.ClusterMetadataSpec(list(prof["storageClasses"]),
-                                                     copy.deepcopy(prof["apiKindVersionMap"]))
+                                                     {k: list(v) for k, v in prof["apiKindVersionMap"].items()})
             if not cm.spec.storage_classes:
                 cm.spec.storage_classes = [DEFAULT_STORAGE_CLASS_NAME]
             clusters[cm.name] = cm

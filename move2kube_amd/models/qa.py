@@ -270,6 +270,11 @@ class Cache:
         self.problems = []
         self._lock = threading.Lock()
         self._chunks = {}  # id(problem) -> (problem, its to_yaml(), emitted YAML of its list item)
+        # write-behind: answers are persisted at the engine chain's flush points
+        # (before a blocking prompt, when the command ends) instead of one full
+        # rewrite per answer
+        self.write_behind = False
+        self.dirty = False
 
     def to_yaml(self):
         d = {}
@@ -346,11 +351,31 @@ class Cache:
                     break
             else:
                 self.problems.append(p.copy())
+            if self.write_behind:
+                self.dirty = True
+            else:
+                try:
+                    self.write()
+                except OSError as e:
+                    log.error("Unable to persist cache : %s", e)
+        return True
+
+    def flush(self):
+        """Write pending answers (write-behind mode)."""
+        with self._lock:
+            if not self.dirty:
+                return
+            self.dirty = False
             try:
                 self.write()
             except OSError as e:
                 log.error("Unable to persist cache : %s", e)
-        return True
+
+    def discard_pending(self):
+        """The file is about to be deleted: pending answers need no write (the
+        reference's writes of them would be deleted with it)."""
+        with self._lock:
+            self.dirty = False
 
     def get_solution(self, p):
         if p.resolved:

@@ -139,6 +139,13 @@ def translate(p, outpath, qadisablecli=False):
     optimize -> compose output -> customize -> (helm) parameterize -> CI/CD
     -> k8s/knative output."""
     try:
+        _translate(p, outpath, qadisablecli)
+    finally:
+        qaengine.flush_write_cache()
+
+
+def _translate(p, outpath, qadisablecli):
+    try:
         ir = source_translator.translate(p)
     except Exception as e:  # noqa: BLE001
         if isinstance(e, log.FatalError):
@@ -165,6 +172,7 @@ def translate(p, outpath, qadisablecli=False):
     log.debug("Total services optimized : %d", len(ir.services))
 
     if os.path.lexists(outpath):
+        qaengine.before_remove(outpath)
         try:
             if os.path.isdir(outpath) and not os.path.islink(outpath):
                 shutil.rmtree(outpath)

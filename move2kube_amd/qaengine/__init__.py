@@ -2,5 +2,5 @@
 an interactive CLI, or the HTTP REST API the UI drives) plus a write cache
 that checkpoints every answer."""
 
-from .engine import (add_caches, add_engine, engines, fetch_answer, get_write_cache, reset,  # noqa: F401
-                     set_write_cache, start_engine)
+from .engine import (add_caches, add_engine, before_remove, engines, fetch_answer,  # noqa: F401
+                     flush_write_cache, get_write_cache, reset, set_write_cache, start_engine)

@@ -15,6 +15,8 @@ from .engine import Engine
 
 
 class CliEngine(Engine):
+    interactive = True  # may block on a person: the write cache is flushed first
+
     def __init__(self, stdin=None, stdout=None):
         self.stdin = stdin
         self.stdout = stdout

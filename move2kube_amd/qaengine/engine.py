@@ -3,8 +3,16 @@
 Engines are consulted in order until one resolves a problem; cache engines
 added with :func:`add_caches` are *prepended* (highest priority).  Every
 resolved answer is appended to the write cache (``<out>/m2kqacache.yaml``),
-which is rewritten on each answer - the resumable checkpoint of an
-interactive session.  Passwords are never cached.
+the resumable checkpoint of an interactive session.  Passwords are never
+cached.
+
+The reference rewrites the whole cache file on every answer.  Here the cache
+is write-behind: it is flushed before any interactive engine (CLI prompt,
+REST UI) can block waiting for a person, when the command ends (also on
+errors and at interpreter exit), and pending answers are dropped when the
+output directory holding the file is about to be removed - so the file on
+disk at every point a user could interrupt is the one the reference would
+have written.
 
 Difference from the reference: when no engine resolves a problem the
 reference loops forever on the last engine; here the last
@@ -12,6 +20,7 @@ engine is retried a bounded number of times and then the problem's default is
 used (or an error raised when it has none).
 """
 
+import atexit
 import os
 import threading
 
@@ -39,6 +48,7 @@ class Engine:
 def reset():
     """Drop all engines and the write cache (tests / in-process reuse)."""
     global _engines, _write_cache
+    flush_write_cache()
     with _lock:
         _engines = []
         _write_cache = None
@@ -97,6 +107,8 @@ def fetch_answer(prob):
         from .default_engine import DefaultEngine
         chain = [DefaultEngine()]
     for e in chain:
+        if getattr(e, "interactive", False):
+            flush_write_cache()
         try:
             ans = e.fetch_answer(prob.copy())
             err = None
@@ -129,15 +141,40 @@ def fetch_answer(prob):
     return ans
 
 
-def set_write_cache(cache_file):
+def set_write_cache(cache_file, write_behind=True):
     global _write_cache
+    flush_write_cache()
     d = os.path.dirname(cache_file)
     if d:
         os.makedirs(d, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
     c = qa.Cache(cache_file)
     c.write()
+    c.write_behind = write_behind
     _write_cache = c
     return c
+
+
+def flush_write_cache():
+    c = _write_cache
+    if c is not None:
+        c.flush()
+
+
+def before_remove(path):
+    """``path`` is about to be deleted: drop pending answers if the write cache
+    lives under it, otherwise persist them."""
+    c = _write_cache
+    if c is None:
+        return
+    cf = os.path.abspath(c.file)
+    root = os.path.abspath(path)
+    if cf == root or cf.startswith(root.rstrip(os.sep) + os.sep):
+        c.discard_pending()
+    else:
+        c.flush()
+
+
+atexit.register(flush_write_cache)
 
 
 def get_write_cache():

@@ -35,6 +35,8 @@ def free_port():
 
 
 class HTTPRESTEngine(Engine):
+    interactive = True  # may block on a person: the write cache is flushed first
+
     def __init__(self, port=0, host=""):
         self.port = port
         self.host = host

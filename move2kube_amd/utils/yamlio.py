@@ -18,9 +18,12 @@ field order) unless ``sort_maps=True``; a :class:`GoMap` is always sorted with
 the go-yaml key comparator (Go maps).
 """
 
+import contextlib
+import copy
 import functools
 import math
 import re
+import threading
 
 import yaml
 
@@ -586,15 +589,81 @@ for _tag in ("tag:yaml.org,2002:int", "tag:yaml.org,2002:float", "tag:yaml.org,2
     _RawLoader.add_constructor(_tag, _construct_raw_scalar)
 
 
+# Command-scoped parse memo.  Every planner/loader of the reference decodes
+# every YAML file of the source tree on its own (compose v3, compose v1/v2, CF
+# manifest, knative, kube, k8s-files, QA-cache and cluster loaders: 8-10
+# parses of each file per translate).  Inside ``parse_cache()`` each distinct
+# (loader, text) pair is parsed once and callers get private copies.  Keyed by
+# content, so it can never serve a stale document.
+_memo = None
+_memo_depth = 0
+_memo_lock = threading.Lock()
+
+
+@contextlib.contextmanager
+def parse_cache():
+    """Memoize YAML parses for the duration of one command (nestable)."""
+    global _memo, _memo_depth
+    with _memo_lock:
+        if _memo_depth == 0:
+            _memo = {}
+        _memo_depth += 1
+    try:
+        yield
+    finally:
+        with _memo_lock:
+            _memo_depth -= 1
+            if _memo_depth == 0:
+                _memo = None
+
+
+_ATOMS = (str, int, float, bool, type(None))
+
+
+def _tree_copy(o):
+    t = type(o)
+    if t is dict:
+        return {k: (v if type(v) in _ATOMS else _tree_copy(v)) for k, v in o.items()}
+    if t is list:
+        return [v if type(v) in _ATOMS else _tree_copy(v) for v in o]
+    if t in _ATOMS:
+        return o
+    return copy.deepcopy(o)
+
+
+def _memoized(kind, text, parse):
+    memo = _memo
+    if memo is None or not isinstance(text, str):
+        return parse(text)
+    key = (kind, text)
+    hit = memo.get(key, _MISS)
+    if hit is _MISS:
+        try:
+            hit = (True, parse(text))
+        except yaml.YAMLError as e:
+            hit = (False, e)
+        memo[key] = hit
+    ok, val = hit
+    if not ok:
+        raise val.with_traceback(None)
+    try:
+        return _tree_copy(val)
+    except RecursionError:  # self-referencing aliases
+        return copy.deepcopy(val)
+
+
+_MISS = object()
+
+
 def load(text):
     """Decode like go-yaml v3 into ``interface{}``."""
-    return yaml.load(text, Loader=_TypedLoader)
+    return _memoized("typed", text, lambda t: yaml.load(t, Loader=_TypedLoader))
 
 
 def load_all(text):
-    return list(yaml.load_all(text, Loader=_TypedLoader))
+    return _memoized("typed*", text, lambda t: list(yaml.load_all(t, Loader=_TypedLoader)))
 
 
 def load_raw(text):
     """Decode keeping scalars as raw strings (for typed struct decoding)."""
-    return yaml.load(text, Loader=_RawLoader)
+    return _memoized("raw", text, lambda t: yaml.load(t, Loader=_RawLoader))

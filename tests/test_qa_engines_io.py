@@ -72,3 +72,55 @@ def test_cli_engine_select_confirm_input_multiselect():
     assert ms.get_slice_answer() == ["x", "z"]
     assert e.fetch_answer(qa.new_input_problem("i2", [], "dflt")).get_string_answer() == "dflt"
     assert "Hints:" in out.getvalue()
+
+
+def _cache_answers(path):
+    from move2kube_amd.utils import yamlio
+    with open(path) as f:
+        d = yamlio.load(f.read())
+    return [s["description"] for s in (d.get("spec") or {}).get("solutions") or []]
+
+
+def test_write_cache_is_flushed_before_an_interactive_prompt(tmp_path):
+    """Answers from non-interactive engines are written behind; the file is
+    complete before any engine that may block on a person is consulted."""
+    from move2kube_amd.qaengine.default_engine import DefaultEngine
+    cache = str(tmp_path / "m2kqacache.yaml")
+    qaengine.add_engine(DefaultEngine())
+    qaengine.set_write_cache(cache)
+    qaengine.fetch_answer(qa.new_input_problem("first", [], "a"))
+    assert _cache_answers(cache) == []          # written behind
+
+    seen = {}
+
+    class Prompt(CliEngine):
+        def fetch_answer(self, prob):
+            seen["on_disk"] = _cache_answers(cache)
+            prob.set_answer(["typed"])
+            return prob
+    qaengine.reset()
+    qaengine.add_engine(Prompt())
+    qaengine.set_write_cache(cache)
+    qaengine.fetch_answer(qa.new_input_problem("first", [], "a"))  # pending
+    qaengine.fetch_answer(qa.new_input_problem("second", [], "b"))
+    assert seen["on_disk"] == ["first"]
+    qaengine.flush_write_cache()
+    assert _cache_answers(cache) == ["first", "second"]
+
+
+def test_pending_answers_dropped_when_output_is_removed(tmp_path):
+    from move2kube_amd.qaengine.default_engine import DefaultEngine
+    out = tmp_path / "out"
+    cache = str(out / "m2kqacache.yaml")
+    qaengine.add_engine(DefaultEngine())
+    qaengine.set_write_cache(cache)
+    qaengine.fetch_answer(qa.new_input_problem("q1", [], "a"))
+    qaengine.before_remove(str(out))
+    import shutil
+    shutil.rmtree(str(out))
+    qaengine.flush_write_cache()
+    assert not out.exists()           # like the reference: nothing rewrites it
+    out.mkdir()
+    qaengine.fetch_answer(qa.new_input_problem("q2", [], "b"))
+    qaengine.flush_write_cache()
+    assert _cache_answers(cache) == ["q1", "q2"]

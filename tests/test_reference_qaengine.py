@@ -55,6 +55,7 @@ def test_cache_multiselect_and_write_cache(cache_engine):
                                    ["MultiSelect input problem test context"], d,
                                    ["Option A", "Option B", "Option C", "Option D"])
     assert qaengine.fetch_answer(p).get_slice_answer() == d
+    qaengine.flush_write_cache()
     written = yamlio.load(cache_engine.read_text())
     assert written["kind"] == "QACache"
     sol = written["spec"]["solutions"][0]
@@ -102,5 +103,6 @@ def test_passwords_not_cached(tmp_path):
     qaengine.set_write_cache(str(tmp_path / "w.yaml"))
     qaengine.fetch_answer(qa.new_password_problem("pw", []))
     qaengine.fetch_answer(qa.new_input_problem("user", [], "u"))
+    qaengine.flush_write_cache()
     data = yamlio.load((tmp_path / "w.yaml").read_text())
     assert [s["description"] for s in data["spec"]["solutions"]] == ["user"]

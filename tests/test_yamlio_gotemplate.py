@@ -70,3 +70,24 @@ def test_template_errors():
         gotemplate.render("{{ .A", {})
     with pytest.raises(gotemplate.TemplateError):
         gotemplate.render("{{ if }}x{{ end }}", {})
+
+
+def test_parse_cache_returns_private_copies_and_reraises():
+    from move2kube_amd.utils import yamlio as y
+    text = "a:\n  b: [1, 2]\n"
+    bad = "a: [\n"
+    with y.parse_cache():
+        d1 = y.load(text)
+        d1["a"]["b"].append(3)
+        d2 = y.load(text)
+        assert d2 == {"a": {"b": [1, 2]}}
+        assert y.load_raw("x: 1\n") == {"x": "1"}      # loaders are cached separately
+        assert y.load("x: 1\n") == {"x": 1}
+        for _ in range(2):
+            try:
+                y.load(bad)
+            except y.YAMLError:
+                pass
+            else:
+                raise AssertionError("expected a YAML error")
+    assert y._memo is None
