@@ -42,14 +42,14 @@ def _run(cmd):
 
 def build_native(force=False):
     import pybind11
-    src = os.path.join(CSRC, "m2k_native.cpp")
+    srcs = [os.path.join(CSRC, "m2k_native.cpp"), os.path.join(CSRC, "yaml_emit.cpp")]
     out = native_target()
-    if not force and not _stale(out, [src]):
+    if not force and not _stale(out, srcs):
         return out
     inc = sysconfig.get_paths()["include"]
     cxx = os.environ.get("CXX", "g++")
     _run([cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall",
-          "-I" + pybind11.get_include(), "-I" + inc, src, "-o", out + ".tmp", "-lpthread"])
+          "-I" + pybind11.get_include(), "-I" + inc] + srcs + ["-o", out + ".tmp", "-lpthread"])
     os.replace(out + ".tmp", out)
     return out
 

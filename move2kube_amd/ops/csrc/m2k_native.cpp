@@ -20,6 +20,7 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <stdexcept>
 #include <atomic>
 #include <cerrno>
 #include <cstdint>
@@ -601,6 +602,68 @@ std::vector<std::pair<int, py::bytes>> run_commands(const std::vector<std::vecto
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// Batched output writes: open(O_TRUNC) + write + fchmod(mode) per file, spread
+// over threads with the GIL released.  Returns errno per file (0 = ok).  A path
+// listed twice keeps its last content (written once, like sequential writes).
+// ---------------------------------------------------------------------------
+static int write_one(const std::string &path, const std::string &data, int mode) {
+  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+  if (fd < 0) return errno;
+  const char *p = data.data();
+  size_t left = data.size();
+  while (left) {
+    ssize_t w = ::write(fd, p, left);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      int e = errno;
+      ::close(fd);
+      return e;
+    }
+    p += w;
+    left -= static_cast<size_t>(w);
+  }
+  (void)::fchmod(fd, static_cast<mode_t>(mode));  // best effort, like os.chmod after write
+  if (::close(fd) != 0) return errno;
+  return 0;
+}
+
+std::vector<int> write_files(const std::vector<std::string> &paths, const std::vector<py::bytes> &datas,
+                             const std::vector<int> &modes, int nthreads) {
+  const size_t n = paths.size();
+  if (datas.size() != n || modes.size() != n) throw std::invalid_argument("paths, datas and modes differ in length");
+  std::vector<std::string> bufs(n);
+  for (size_t i = 0; i < n; i++) bufs[i] = static_cast<std::string>(datas[i]);
+  std::vector<int> err(n, 0);
+  std::vector<char> skip(n, 0);  // superseded by a later write to the same path
+  {
+    std::vector<size_t> order(n);
+    for (size_t i = 0; i < n; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return paths[a] < paths[b]; });
+    for (size_t k = 0; k + 1 < n; k++)
+      if (paths[order[k]] == paths[order[k + 1]]) skip[order[k]] = 1;
+  }
+  {
+    py::gil_scoped_release nogil;
+    parallel_for(n, nthreads, 16, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; i++)
+        if (!skip[i]) err[i] = write_one(paths[i], bufs[i], modes[i]);
+    });
+  }
+  return err;
+}
+
+// yaml_emit.cpp
+extern "C" PyObject* m2k_yaml_dump(PyObject* data, int sort_maps, PyObject* gomap, PyObject* scalar_fn,
+                                   PyObject* style_fn, PyObject* sort_fn);
+
+static py::str yaml_dump(py::object data, bool sort_maps, py::object gomap, py::object scalar_fn, py::object style_fn,
+                         py::object sort_fn) {
+  PyObject* r = m2k_yaml_dump(data.ptr(), sort_maps ? 1 : 0, gomap.ptr(), scalar_fn.ptr(), style_fn.ptr(), sort_fn.ptr());
+  if (!r) throw py::error_already_set();
+  return py::reinterpret_steal<py::str>(r);
+}
+
 PYBIND11_MODULE(_m2k_native, m) {
   m.doc() = "move2kube_amd native runtime (walk, sniff, spawn pool, hashes, edit distance)";
   m.def("walk", &walk, py::arg("root"));
@@ -613,6 +676,9 @@ PYBIND11_MODULE(_m2k_native, m) {
         py::arg("dcost") = 1, py::arg("scost") = 2, py::arg("nthreads") = 8);
   m.def("pack_strings", &pack_strings, py::arg("items"));
   m.def("closest_batch", &closest_batch, py::arg("as"), py::arg("bs"), py::arg("nthreads") = 8);
+  m.def("write_files", &write_files, py::arg("paths"), py::arg("datas"), py::arg("modes"), py::arg("nthreads") = 8);
+  m.def("yaml_dump", &yaml_dump, py::arg("data"), py::arg("sort_maps"), py::arg("gomap"), py::arg("scalar_fn"),
+        py::arg("style_fn"), py::arg("sort_fn"));
   m.def("run_commands", &run_commands, py::arg("argvs"), py::arg("cwds"), py::arg("parallel") = 8,
         py::arg("timeout_s") = 0.0);
 }

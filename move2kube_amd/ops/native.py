@@ -65,6 +65,30 @@ def sniff_dockerfiles(paths, nthreads=8):
     return [sniff_first_from(p) for p in paths]
 
 
+def write_files(items, nthreads=8):
+    """Write ``[(path, text_or_bytes, mode)]``; returns ``[OSError or None]`` per
+    item.  Native: parallel, GIL released; a repeated path keeps its last content."""
+    datas = [d.encode("utf-8", errors="surrogateescape") if isinstance(d, str) else bytes(d) for _, d, _ in items]
+    m = _load()
+    if m is not None:
+        paths = [p for p, _, _ in items]
+        errs = m.write_files(paths, datas, [int(md) for _, _, md in items], nthreads)
+        return [OSError(e, os.strerror(e), p) if e else None for p, e in zip(paths, errs)]
+    out = []
+    for (p, _, md), data in zip(items, datas):
+        try:
+            with open(p, "wb") as f:
+                f.write(data)
+            try:
+                os.chmod(p, md)
+            except OSError:
+                pass
+            out.append(None)
+        except OSError as e:
+            out.append(e)
+    return out
+
+
 def run_commands(argvs, cwds, parallel=8, timeout_s=0.0):
     m = _load()
     if m is not None:

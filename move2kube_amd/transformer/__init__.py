@@ -21,6 +21,7 @@ from .. import assets
 from ..apiresource.base import GOTYPE
 from ..apiresourceset import K8sAPIResourceSet, KnativeAPIResourceSet, TektonAPIResourceSet
 from ..k8s import convert, schema
+from ..ops import native
 from ..models import plan as plantypes
 from ..utils import common, log, yamlio
 from ..utils.constants import (DEFAULT_DIRECTORY_PERMISSION, DEFAULT_EXECUTABLE_PERMISSION, DEFAULT_FILE_PERMISSION,
@@ -44,6 +45,7 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
         log.error("Unable to create directory %s : %s", cpath, e)
     log.debug("Total number of containers : %d", len(containers))
     buildscripts, dockerimages, manualimages = [], [], []
+    batch = []
     for c in containers:
         if not c.new:
             continue
@@ -62,10 +64,10 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
             if common.go_ext(wp) == ".sh":
                 mode = DEFAULT_EXECUTABLE_PERMISSION
                 buildscripts.append(os.path.join(CONTAINERS_DIR, rel))
-            try:
-                common.write_text(wp, c.new_files[rel], mode)
-            except OSError as e:
-                log.warning("Error writing file at %s : %s", wp, e)
+            batch.append((wp, c.new_files[rel], mode))
+    for (wp, _, _), err in zip(batch, native.write_files(batch)):
+        if err is not None:
+            log.warning("Error writing file at %s : %s", wp, err)
     if manualimages:
         wp = os.path.join(outpath, "Manualimages.md")
         if settings.fixed:
@@ -113,6 +115,7 @@ def write_transformed_objects(path, objs):
     except OSError as e:
         log.error("Unable to create directory %s : %s", path, e)
         raise
+    batch, kinds = [], []
     for obj in objs:
         try:
             data = serialize_object(obj)
@@ -120,11 +123,13 @@ def write_transformed_objects(path, objs):
             log.error("Error while Encoding object : %s", e)
             continue
         name = (obj.get("metadata") or {}).get("name", "")
-        f = os.path.join(path, "%s-%s.yaml" % (name, obj.get("kind", "").lower()))
-        try:
-            common.write_text(f, data, DEFAULT_FILE_PERMISSION)
-        except OSError as e:
-            log.error("Failed to write %r Error: %r", obj.get("kind"), str(e))
+        batch.append((os.path.join(path, "%s-%s.yaml" % (name, obj.get("kind", "").lower())), data,
+                      DEFAULT_FILE_PERMISSION))
+        kinds.append(obj.get("kind"))
+    # one batched, parallel write (ops/csrc/m2k_native.cpp:write_files)
+    for (f, _, _), kind, err in zip(batch, kinds, native.write_files(batch)):
+        if err is not None:
+            log.error("Failed to write %r Error: %r", kind, str(err))
             continue
         written.append(f)
         log.debug("%r created", f)

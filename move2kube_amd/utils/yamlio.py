@@ -538,8 +538,33 @@ class _Emitter:
         return "\n".join(self.out) + "\n"
 
 
+def dump_py(data, sort_maps=False):
+    """The pure-Python emitter: the executable specification of the native one."""
+    return _Emitter(sort_maps).document(data)
+
+
+_scalar_lines = _Emitter(False).scalar
+_native_dump = None
+
+
+def _native():
+    global _native_dump
+    if _native_dump is None:
+        from ..ops import native
+        m = native.module()
+        _native_dump = getattr(m, "yaml_dump", None) or False
+    return _native_dump
+
+
 def dump(data, sort_maps=False):
-    """Encode ``data`` like go-yaml v3 ``Encoder`` with ``SetIndent(2)``."""
+    """Encode ``data`` like go-yaml v3 ``Encoder`` with ``SetIndent(2)``.
+
+    Runs the native emitter (``ops/csrc/yaml_emit.cpp``) when the extension is
+    built; it defers floats, non-ASCII text and numeric-looking strings to the
+    Python helpers below, so both paths emit identical bytes."""
+    nd = _native()
+    if nd:
+        return nd(data, sort_maps, GoMap, _scalar_lines, _string_style, go_key_sorted)
     return _Emitter(sort_maps).document(data)
 
 

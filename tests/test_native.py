@@ -74,3 +74,22 @@ def test_python_fallback_distance_is_weighted():
     assert editdistance.wagner_fischer_py("ab", "ac") == 2
     assert editdistance.wagner_fischer_py("", "abc") == 3
     assert editdistance.wagner_fischer_py("kitten", "sitting") == 5
+
+
+def test_write_files_batch(tmp_path, monkeypatch):
+    from move2kube_amd.ops import native as nat
+    d = tmp_path / "o"
+    d.mkdir()
+    items = [(str(d / "a.yaml"), "x: 1\n", 0o644), (str(d / "b.sh"), b"#!/bin/sh\n", 0o744),
+             (str(d / "a.yaml"), "x: 2\n", 0o600), (str(tmp_path / "missing" / "c"), "z", 0o644)]
+    errs = nat.write_files(items)
+    assert errs[:3] == [None, None, None]
+    assert isinstance(errs[3], OSError) and errs[3].errno == 2 and str(tmp_path / "missing" / "c") in str(errs[3])
+    assert (d / "a.yaml").read_text() == "x: 2\n"               # last write wins
+    assert (d / "a.yaml").stat().st_mode & 0o777 == 0o600
+    assert (d / "b.sh").stat().st_mode & 0o777 == 0o744
+    # the pure-Python fallback behaves the same
+    monkeypatch.setattr(nat, "_load", lambda: None)
+    errs2 = nat.write_files(items)
+    assert [type(e) for e in errs2] == [type(e) for e in errs]
+    assert (d / "a.yaml").read_text() == "x: 2\n"

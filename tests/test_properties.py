@@ -1,6 +1,7 @@
 """Property tests: the go-yaml emitter round-trips through a YAML loader, the
 native and Python walkers agree, edit-distance implementations agree."""
 
+import os
 import string
 
 from hypothesis import given, settings, strategies as st
@@ -39,3 +40,28 @@ def test_edit_distance_native_equals_python(a, b):
         return
     assert int(m.edit_distance_batch([a], [b], 1, 1, 2, 1)[0][0]) == editdistance.wagner_fischer_py(a, b)
     assert m.wagner_fischer(a, b, 1, 1, 2) == editdistance.wagner_fischer_py(a, b)
+
+
+# strings biased towards what decides libyaml scalar styles: indicators,
+# whitespace/breaks, control characters, numbers, YAML 1.1 keywords
+_tricky_atoms = st.sampled_from(["-", "--", "---", "...", ":", ": ", " #", "#", "?", "'", '"', "\\", "|", ">",
+                                 "\n", "\r", "\t", " ", "  ", "\x00", "\x7f", "\x1b", "y", "no", "null", "~",
+                                 "true", "0x1F", "1_000", "1e3", ".5", "-.inf", "12:30", "2001-12-14", "+1",
+                                 "007", "<<", "é", " ", "[", "{", ",", "%", "@", "`", "&a", "*a", "!t"])
+_tricky = st.lists(st.one_of(_tricky_atoms, st.text(alphabet=string.printable, max_size=4)),
+                   max_size=5).map("".join)
+_keys = st.one_of(_tricky, st.integers(min_value=-5, max_value=120), st.sampled_from(["b10", "b9", "b09", "a0", "A"]))
+_leaf = st.one_of(_tricky, st.integers(min_value=-2**70, max_value=2**70), st.floats(allow_nan=True),
+                  st.booleans(), st.none())
+_tree = st.recursive(_leaf, lambda ch: st.one_of(
+    st.lists(ch, max_size=4), st.lists(ch, max_size=3).map(tuple),
+    st.dictionaries(_keys, ch, max_size=4),
+    st.dictionaries(_keys, ch, max_size=4).map(yamlio.GoMap)), max_leaves=16)
+
+
+@settings(max_examples=int(os.environ.get("M2K_PROP_EXAMPLES", "600")), deadline=None)
+@given(_tree, st.booleans())
+def test_native_emitter_matches_python_specification(doc, sort_maps):
+    if not yamlio._native():
+        return
+    assert yamlio.dump(doc, sort_maps) == yamlio.dump_py(doc, sort_maps)
