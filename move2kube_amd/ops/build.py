@@ -40,16 +40,25 @@ def _run(cmd):
     subprocess.run(cmd, check=True)
 
 
-def build_native(force=False):
+NATIVE_SOURCES = [os.path.join(CSRC, "m2k_native.cpp"), os.path.join(CSRC, "yaml_emit.cpp")]
+SANITIZERS = {"address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"],
+              "thread": ["-fsanitize=thread"]}
+
+
+def build_native(force=False, out=None, sanitize=None):
+    """Build ``_m2k_native``.  ``sanitize`` ("address" = ASan+UBSan, "thread" =
+    TSan) builds an instrumented copy at ``out`` for the sanitizer test
+    (``tests/test_sanitizers.py``); run it with the runtime ``LD_PRELOAD``-ed."""
     import pybind11
-    srcs = [os.path.join(CSRC, "m2k_native.cpp"), os.path.join(CSRC, "yaml_emit.cpp")]
-    out = native_target()
+    srcs = NATIVE_SOURCES
+    out = out or native_target()
     if not force and not _stale(out, srcs):
         return out
     inc = sysconfig.get_paths()["include"]
     cxx = os.environ.get("CXX", "g++")
-    _run([cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall",
-          "-I" + pybind11.get_include(), "-I" + inc] + srcs + ["-o", out + ".tmp", "-lpthread"])
+    opt = ["-O3"] if not sanitize else ["-O1", "-g"] + SANITIZERS[sanitize]
+    _run([cxx] + opt + ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall",
+                        "-I" + pybind11.get_include(), "-I" + inc] + srcs + ["-o", out + ".tmp", "-lpthread"])
     os.replace(out + ".tmp", out)
     return out
 
