@@ -110,6 +110,7 @@ def main():
 
     work = tempfile.mkdtemp(prefix="m2k-bench-r%d-" % rank)
     n_services = 0
+    phase_ms = None
     try:
         # private copy outside any git checkout, so output is location independent
         src = os.path.join(work, "samples")
@@ -132,6 +133,16 @@ def main():
                 step()
             barrier()
             elapsed = time.perf_counter() - t0
+            # Untimed: one traced step for the per-phase breakdown (utils/trace.py)
+            phase_ms = None
+            if rank == 0:
+                from move2kube_amd.utils import trace
+                trace.enable("")
+                try:
+                    step()
+                    phase_ms = {k: round(v, 3) for k, v in list(trace.summary().items())[:12]}
+                finally:
+                    trace._events = None
             # Untimed ablation: the reference's execution model (every detector
             # forked as a shell process, one at a time), same output required.
             ref_ms = None
@@ -182,6 +193,7 @@ def main():
             "manifest_diff": diff,
             "reference_model_ms_per_step": None if ref_ms is None else round(ref_ms, 3),
             "speedup_vs_reference_model": None if not ref_ms else round(ref_ms / ms, 2),
+            "phase_ms_one_step": phase_ms,
             "config": {"model": "move2kube translate samples/ (full tree)", "global_batch": world,
                        "seq_len": n_services, "parallelism": "dp%d" % world},
         }), flush=True)

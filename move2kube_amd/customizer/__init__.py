@@ -10,7 +10,7 @@ import urllib.parse
 from .. import qaengine
 from ..models import ir as irtypes
 from ..models import qa
-from ..utils import common, log
+from ..utils import common, log, trace
 from ..utils.constants import DEFAULT_PVC_SIZE, DEFAULT_REGISTRY_URL, IMAGE_PULL_SECRET_PREFIX, settings
 
 OTHER_REGISTRY = "Other"
@@ -270,7 +270,8 @@ def customize(ir):
     for c in get_customizers():
         log.debug("[%s] Begin Customization", type(c).__name__)
         try:
-            c.customize(ir)
+            with trace.span(type(c).__name__, "customizer"):
+                c.customize(ir)
         except Exception as e:  # noqa: BLE001
             if isinstance(e, log.FatalError):
                 raise

@@ -344,25 +344,61 @@ def _marshal_value(v, typ):
     return v
 
 
+_SKIP = object()
+_EMPTY_STRUCT = object()
+_plans = {}
+_empty = {}
+
+
+def _plan(typ):
+    """Per struct type: (json name, field type, omitempty, value when absent)."""
+    pl = _plans.get(typ)
+    if pl is None:
+        pl = []
+        for jname, ftype, omit in _STRUCTS[typ]:
+            if jname == "inline":
+                absent = None
+            elif ftype in _STRUCTS:
+                absent = _EMPTY_STRUCT
+            elif ftype == "Time":
+                absent = None
+            elif omit:
+                absent = _SKIP
+            elif ftype.startswith("*") or ftype.startswith("[]") or ftype.startswith("map") or ftype in ("any", "bytes"):
+                absent = None
+            else:
+                absent = _zero(ftype)
+            pl.append((jname, ftype, omit, absent))
+        pl = _plans[typ] = tuple(pl)
+    return pl
+
+
+def _empty_struct(typ):
+    # shared and read-only: marshal output only feeds the serializer
+    e = _empty.get(typ)
+    if e is None:
+        e = _empty[typ] = _marshal_fields({}, typ)
+    return e
+
+
 def _marshal_struct(d, typ):
+    if not d:
+        return _empty_struct(typ)
+    return _marshal_fields(d, typ)
+
+
+def _marshal_fields(d, typ):
     out = {}
-    for jname, ftype, omit in _STRUCTS[typ]:
+    get = d.get
+    for jname, ftype, omit, absent in _plan(typ):
         if jname == "inline":
             out.update(_marshal_struct(d, ftype))
             continue
-        present = jname in d
-        v = d.get(jname)
-        if not present or v is None:
-            if ftype in _STRUCTS:
-                out[jname] = _marshal_struct({}, ftype)
-            elif ftype == "Time":
-                out[jname] = None
-            elif omit:
+        v = get(jname)
+        if v is None:
+            if absent is _SKIP:
                 continue
-            elif ftype.startswith("*") or ftype.startswith("[]") or ftype.startswith("map") or ftype in ("any", "bytes"):
-                out[jname] = None
-            else:
-                out[jname] = _zero(ftype)
+            out[jname] = _empty_struct(ftype) if absent is _EMPTY_STRUCT else absent
             continue
         if omit and _is_empty(v, ftype):
             continue

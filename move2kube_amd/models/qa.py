@@ -7,6 +7,7 @@ empty multi-selects, default checks), answer validation and cache matching
 so that caches written by either tool replay in the other.
 """
 
+import functools
 import re
 import threading
 
@@ -163,14 +164,23 @@ class Problem:
         return "Problem(%r)" % (self.to_json(),)
 
 
-def _match_string(s1, s2):
-    if s1.casefold() == s2.casefold():
-        return True
+@functools.lru_cache(maxsize=4096)
+def _matcher(s1):
+    """(casefolded s1, compiled regex or None) - cache lookups compare every
+    new problem against every cached one, so both are computed once."""
     try:
-        return re.search(_go_regex(s1), s2) is not None
+        rx = re.compile(_go_regex(s1))
     except re.error as e:
         log.debug("Unable to compile string %s : %s", s1, e)
-        return False
+        rx = None
+    return s1.casefold(), rx
+
+
+def _match_string(s1, s2):
+    folded, rx = _matcher(s1)
+    if folded == s2.casefold():
+        return True
+    return rx is not None and rx.search(s2) is not None
 
 
 def _go_regex(p):

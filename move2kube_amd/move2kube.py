@@ -8,7 +8,7 @@ from . import collector, customizer, metadata, optimizer, parameterizer, qaengin
 from .models import info, qa
 from .models import plan as plantypes
 from .source import translator as source_translator
-from .utils import common, fsindex, log, yamlio
+from .utils import common, fsindex, log, trace, yamlio
 from .utils.constants import DEFAULT_CLUSTER_TYPE
 
 
@@ -24,12 +24,13 @@ def create_plan(input_path, project_name):
     p = plantypes.new_plan()
     p.name = project_name
     p.root_dir = input_path
-    with fsindex.scope():
+    with fsindex.scope(), trace.span("plan", "command"):
         log.info("Planning Translation")
         for t in source_translator.get_source_loaders():
             log.info("[%r] Planning translation", t)
             try:
-                services = t.get_service_options(input_path, p)
+                with trace.span(type(t).__name__, "plan"):
+                    services = t.get_service_options(input_path, p)
             except Exception as e:  # noqa: BLE001
                 if isinstance(e, log.FatalError):
                     raise
@@ -42,7 +43,8 @@ def create_plan(input_path, project_name):
         for loader in metadata.get_loaders():
             log.info("[%r] Planning metadata", loader)
             try:
-                loader.update_plan(input_path, p)
+                with trace.span(type(loader).__name__, "plan-metadata"):
+                    loader.update_plan(input_path, p)
             except Exception as e:  # noqa: BLE001
                 if isinstance(e, log.FatalError):
                     raise
@@ -139,12 +141,24 @@ def translate(p, outpath, qadisablecli=False):
     optimize -> compose output -> customize -> (helm) parameterize -> CI/CD
     -> k8s/knative output."""
     try:
-        _translate(p, outpath, qadisablecli)
+        with trace.span("translate", "command", services=len(p.services)):
+            _translate(p, outpath, qadisablecli)
     finally:
         qaengine.flush_write_cache()
+        trace.flush()
 
 
 def _translate(p, outpath, qadisablecli):
+    # source -> IR and metadata loading only read the source tree: one shared
+    # directory index for all translators/containerizers of this stage
+    with fsindex.scope():
+        ir = _to_ir(p)
+    ir = optimizer.optimize(ir)
+    log.debug("Total services optimized : %d", len(ir.services))
+    _emit(p, ir, outpath, qadisablecli)
+
+
+def _to_ir(p):
     try:
         ir = source_translator.translate(p)
     except Exception as e:  # noqa: BLE001
@@ -157,7 +171,8 @@ def _translate(p, outpath, qadisablecli):
     for loader in metadata.get_loaders():
         log.debug("[%r] Begin metadata loading", loader)
         try:
-            loader.load_to_ir(p, ir)
+            with trace.span(type(loader).__name__, "metadata"):
+                loader.load_to_ir(p, ir)
         except Exception as e:  # noqa: BLE001
             if isinstance(e, log.FatalError):
                 raise
@@ -167,10 +182,10 @@ def _translate(p, outpath, qadisablecli):
     log.info("Metadata loading done")
     log.debug("Total services loaded : %d", len(ir.services))
     log.debug("Total containers loaded : %d", len(ir.containers))
+    return ir
 
-    ir = optimizer.optimize(ir)
-    log.debug("Total services optimized : %d", len(ir.services))
 
+def _emit(p, ir, outpath, qadisablecli):
     if os.path.lexists(outpath):
         qaengine.before_remove(outpath)
         try:
@@ -184,8 +199,9 @@ def _translate(p, outpath, qadisablecli):
 
     dct = transformer.ComposeTransformer()
     try:
-        dct.transform(ir)
-        dct.write_objects(outpath)
+        with trace.span("ComposeTransformer", "transform"):
+            dct.transform(ir)
+            dct.write_objects(outpath)
     except Exception as e:  # noqa: BLE001
         if isinstance(e, log.FatalError):
             raise
@@ -199,8 +215,9 @@ def _translate(p, outpath, qadisablecli):
     if any(c.new for c in ir.containers):
         cicd = transformer.CICDTransformer()
         try:
-            cicd.transform(ir)
-            cicd.write_objects(outpath)
+            with trace.span("CICDTransformer", "transform"):
+                cicd.transform(ir)
+                cicd.write_objects(outpath)
         except Exception as e:  # noqa: BLE001
             if isinstance(e, log.FatalError):
                 raise
@@ -209,13 +226,15 @@ def _translate(p, outpath, qadisablecli):
     ir.add_copy_sources_warning = qadisablecli
     t = transformer.get_transformer(ir)
     try:
-        t.transform(ir)
+        with trace.span(type(t).__name__ + ".transform", "transform"):
+            t.transform(ir)
     except Exception as e:  # noqa: BLE001
         if isinstance(e, log.FatalError):
             raise
         log.fatal("Error during translate. Error: %r", str(e))
     try:
-        t.write_objects(outpath)
+        with trace.span(type(t).__name__ + ".write_objects", "transform"):
+            t.write_objects(outpath)
     except Exception as e:  # noqa: BLE001
         if isinstance(e, log.FatalError):
             raise

@@ -7,7 +7,7 @@ import re
 from .. import qaengine
 from ..models import ir as irtypes
 from ..models import qa
-from ..utils import common, log
+from ..utils import common, log, trace
 from ..utils.constants import ANNOTATION_LABEL_VALUE, DEFAULT_SERVICE_PORT, EXPOSE_SELECTOR
 
 MIN_REPLICAS = 2
@@ -163,7 +163,8 @@ def optimize(ir):
     for o in get_optimizers():
         log.debug("[%s] Begin Optimization", type(o).__name__)
         try:
-            ir = o.optimize(ir)
+            with trace.span(type(o).__name__, "optimizer"):
+                ir = o.optimize(ir)
         except Exception as e:  # noqa: BLE001
             if isinstance(e, log.FatalError):
                 raise

@@ -18,7 +18,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 from ..ops import native
 from . import builtin_detect
-from ..utils import fsindex, log
+from ..utils import fsindex, log, trace
 from ..utils.constants import settings
 
 DETECT_TIMEOUT_S = float(os.environ.get("M2K_DETECT_TIMEOUT", "300"))
@@ -56,6 +56,11 @@ def run_detect_jobs(jobs):
     """Run [(script_dir, script_name, target_dir), ...]; returns DetectResults in order."""
     if not jobs:
         return []
+    with trace.span("detect-batch", "detect", jobs=len(jobs)):
+        return _run_detect_jobs(jobs)
+
+
+def _run_detect_jobs(jobs):
     cache = fsindex.scoped_cache("detect")
     todo, todo_idx = [], []
     results = [None] * len(jobs)

@@ -5,7 +5,7 @@ images, a shared storage class -> ``{{ .Values.storageclass }}``, ingress host -
 
 from ..models import ir as irtypes
 from ..models.output import CONTAINERS_TAG, IMAGE_TAG_TAG, PARAMETER_REGISTRY_PREFIX, SERVICES_TAG
-from ..utils import common, log
+from ..utils import common, log, trace
 from ..utils.constants import settings
 
 
@@ -73,7 +73,8 @@ def parameterize(ir):
     for p in get_parameterizers():
         log.debug("[%s] Begin Parameterization", type(p).__name__)
         try:
-            p.parameterize(ir)
+            with trace.span(type(p).__name__, "parameterizer"):
+                p.parameterize(ir)
         except Exception as e:  # noqa: BLE001
             log.warning("[%s] Failed : %s", type(p).__name__, e)
         else:

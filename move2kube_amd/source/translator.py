@@ -6,7 +6,7 @@ translator of its ``translationType`` and merges the resulting IRs.
 """
 
 from ..models import ir as irtypes
-from ..utils import log
+from ..utils import log, trace
 
 
 class Translator:
@@ -48,7 +48,8 @@ def translate(plan):
                 valid.append(options[0])
         log.debug("Services to translate : %d", len(valid))
         try:
-            cur = t.translate(valid, plan)
+            with trace.span(type(t).__name__, "translate", services=len(valid)):
+                cur = t.translate(valid, plan)
         except Exception as e:  # noqa: BLE001
             log.warning("[%r] Failed : %s", t, e)
             continue

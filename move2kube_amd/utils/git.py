@@ -10,6 +10,8 @@ import os
 import re
 import urllib.parse
 
+from . import fsindex
+
 
 class GitError(Exception):
     pass
@@ -18,13 +20,22 @@ class GitError(Exception):
 def find_repo(path):
     """Walk up from ``path`` to the directory containing ``.git``.
 
-    Returns (worktree_root, git_dir)."""
+    Returns (worktree_root, git_dir).  Inside an ``fsindex.scope()`` every
+    directory visited remembers the answer, so the per-service lookups of one
+    command share their walks up the tree."""
+    cache = fsindex.scoped_cache("git-find")
     p = os.path.abspath(path)
+    visited = []
     while True:
+        if cache is not None and p in cache:
+            result = cache[p]
+            break
+        visited.append(p)
         dotgit = os.path.join(p, ".git")
         if os.path.isdir(dotgit):
             if os.path.exists(os.path.join(dotgit, "HEAD")):
-                return p, dotgit
+                result = (p, dotgit)
+                break
         elif os.path.isfile(dotgit):
             try:
                 with open(dotgit) as f:
@@ -35,11 +46,19 @@ def find_repo(path):
                 gd = line[len("gitdir:"):].strip()
                 if not os.path.isabs(gd):
                     gd = os.path.normpath(os.path.join(p, gd))
-                return p, gd
+                result = (p, gd)
+                break
         parent = os.path.dirname(p)
         if parent == p:
-            raise GitError("repository does not exist")
+            result = None
+            break
         p = parent
+    if cache is not None:
+        for v in visited:
+            cache[v] = result
+    if result is None:
+        raise GitError("repository does not exist")
+    return result
 
 
 _REMOTE_RE = re.compile(r'^remote\s+"(.*)"$')
