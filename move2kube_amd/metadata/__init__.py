@@ -76,9 +76,9 @@ class ClusterMDLoader(Loader):
         clusters = {}
         for name, prof in assets.builtin_clusters().items():
             cm = collection.ClusterMetadata(name)
-            # kind -> [group/version]: a one-level copy is a full copy
-            cm.spec = collection.ClusterMetadataSpec(list(prof["storageClasses"]),
-                                                     {k: list(v) for k, v in prof["apiKindVersionMap"].items()})
+            # version lists are shared with the packaged profile: consumers only
+            # read them, and load_to_ir takes a deep copy (cm.spec.copy())
+            cm.spec = collection.ClusterMetadataSpec(prof["storageClasses"], prof["apiKindVersionMap"])
             if not cm.spec.storage_classes:
                 cm.spec.storage_classes = [DEFAULT_STORAGE_CLASS_NAME]
             clusters[cm.name] = cm

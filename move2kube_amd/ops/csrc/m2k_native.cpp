@@ -20,6 +20,7 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <map>
 #include <stdexcept>
 #include <atomic>
 #include <cerrno>
@@ -603,8 +604,8 @@ std::vector<std::pair<int, py::bytes>> run_commands(const std::vector<std::vecto
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Batched output writes: open(O_TRUNC) + write + fchmod(mode) per file, spread
-// over threads with the GIL released.  Returns errno per file (0 = ok).  A path
+// Batched output writes: open(O_TRUNC) + write + fchmod(mode) per file, with
+// the GIL released; different directories are written by different threads.  Returns errno per file (0 = ok).  A path
 // listed twice keeps its last content (written once, like sequential writes).
 // ---------------------------------------------------------------------------
 static int write_one(const std::string &path, const std::string &data, int mode) {
@@ -643,11 +644,18 @@ std::vector<int> write_files(const std::vector<std::string> &paths, const std::v
     for (size_t k = 0; k + 1 < n; k++)
       if (paths[order[k]] == paths[order[k + 1]]) skip[order[k]] = 1;
   }
+  // Creating entries in one directory serialises on that directory's inode
+  // lock (threads only add contention), so work is split by parent directory.
+  std::map<std::string, std::vector<size_t>> by_dir;
+  for (size_t i = 0; i < n; i++)
+    if (!skip[i]) by_dir[paths[i].substr(0, paths[i].rfind('/') + 1)].push_back(i);
+  std::vector<const std::vector<size_t> *> groups;
+  for (auto &kv : by_dir) groups.push_back(&kv.second);
   {
     py::gil_scoped_release nogil;
-    parallel_for(n, nthreads, 16, [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; i++)
-        if (!skip[i]) err[i] = write_one(paths[i], bufs[i], modes[i]);
+    parallel_for(groups.size(), std::min<int>(nthreads, static_cast<int>(groups.size())), 2, [&](size_t lo, size_t hi) {
+      for (size_t g = lo; g < hi; g++)
+        for (size_t i : *groups[g]) err[i] = write_one(paths[i], bufs[i], modes[i]);
     });
   }
   return err;

@@ -27,31 +27,31 @@ def tar_as_string(path, ignore_files=()):
     err = None
     with tarfile.open(fileobj=buf, mode="w", format=tarfile.PAX_FORMAT) as tw:
         def add(cur):
+            """Add one entry; True if it is a directory to descend into.  Like
+            the reference's Walk callback, an ignored name is left out of the
+            archive but an ignored directory's contents are still walked."""
             rel = os.path.relpath(cur, path)
-            if rel in ignore:
-                return False
             info = tw.gettarinfo(cur, arcname=rel)
-            if info.isdir():
-                tw.addfile(info)
-                return True
-            if info.isreg():
-                with open(cur, "rb") as f:
-                    tw.addfile(info, f)
-            else:
-                tw.addfile(info)
-            return False
+            if rel not in ignore:
+                if info.isreg():
+                    with open(cur, "rb") as f:
+                        tw.addfile(info, f)
+                else:
+                    tw.addfile(info)
+            return info.isdir()
+
+        def walk(d):
+            # filepath.Walk order: lexical, depth first, parent before children
+            for name in sorted(os.listdir(d)):
+                p = os.path.join(d, name)
+                if add(p):
+                    walk(p)
 
         try:
             if not os.path.lexists(path):
                 raise FileNotFoundError("lstat %s: no such file or directory" % path)
             if add(path):
-                stack = [path]
-                while stack:
-                    d = stack.pop()
-                    for name in sorted(os.listdir(d), reverse=True):
-                        p = os.path.join(d, name)
-                        if add(p) and not os.path.islink(p):
-                            stack.append(p)
+                walk(path)
         except OSError as e:
             err = e
             log.warning("Failed to create tar string: %s : %s", path, e)
