@@ -42,6 +42,7 @@ def main():
                 r = fn(opts, qs)
                 t.append(time.perf_counter() - t0)
             res["gpu_%s_s" % name] = min(t)
+            res["gpu_%s_breakdown" % name] = gpu.last_timings()
             res["gpu_%s_gsteps_per_s" % name] = cells / min(t) / 1e9
         res["arch"] = gpu.device_arch()
         gi, gd = gpu.ed_closest(opts, qs)

@@ -48,7 +48,13 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <mutex>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #define THREADS 256
@@ -59,97 +65,6 @@
 typedef unsigned long long u64;
 
 namespace {
-
-struct Prepared {
-  std::vector<uint4> data;        // panels: [block][slot] of 16 coded chars
-  std::vector<int64_t> panelOff;  // uint4 offset of each panel
-  std::vector<int> panelBlocks;   // 16-char blocks in each panel
-  std::vector<int> perm;          // sorted position -> original option index (-1 = padding slot)
-  std::vector<int> lenSorted;     // option length in sorted order
-  std::vector<u64> M;             // [nB][256] match masks indexed by code
-  std::vector<int> lenB;
-  int nPanels = 0;
-  int scaled = 0;  // panel bytes hold code*4 (the byte offset into a u32 table) when <= 63 symbols
-};
-
-// Dense codes ranked by option-byte frequency; 0 is reserved for padding.
-// Returns false when all 256 byte values occur (no free code for padding).
-// *nsym = number of symbols in use (codes 1..nsym).
-bool build_code_map(const uint8_t *opts, int64_t nOptBytes, const uint8_t *qs, int64_t nQBytes, uint8_t code[256],
-                    int *nsym) {
-  int64_t freq[256] = {0};
-  bool seen[256] = {false};
-  for (int64_t i = 0; i < nOptBytes; i++) freq[opts[i]]++, seen[opts[i]] = true;
-  for (int64_t i = 0; i < nQBytes; i++) seen[qs[i]] = true;
-  int order[256];
-  int n = 0;
-  for (int b = 0; b < 256; b++)
-    if (seen[b]) order[n++] = b;
-  if (n > 255) return false;
-  std::stable_sort(order, order + n, [&](int x, int y) { return freq[x] > freq[y]; });
-  memset(code, 0, 256);
-  for (int i = 0; i < n; i++) code[order[i]] = (uint8_t)(i + 1);
-  *nsym = n;
-  return true;
-}
-
-int prepare(const uint8_t *opts, const int64_t *offA, int nA, const uint8_t *qs, const int64_t *offB, int nB,
-            Prepared &P) {
-  for (int j = 0; j < nB; j++) {
-    const int64_t len = offB[j + 1] - offB[j];
-    if (len < 0 || len > 64) return -2;
-  }
-  uint8_t code[256];
-  int nsym = 0;
-  if (!build_code_map(opts, offA[nA], qs, offB[nB], code, &nsym)) return -8;
-  P.scaled = nsym <= 63;
-  uint8_t stored[256];
-  for (int b = 0; b < 256; b++) stored[b] = P.scaled ? (uint8_t)(code[b] * 4) : code[b];
-
-  P.M.assign((size_t)nB * 256, 0ULL);
-  P.lenB.resize(nB);
-  for (int j = 0; j < nB; j++) {
-    const int len = (int)(offB[j + 1] - offB[j]);
-    P.lenB[j] = len;
-    for (int k = 0; k < len; k++) P.M[(size_t)j * 256 + code[qs[offB[j] + k]]] |= (1ULL << k);
-  }
-
-  std::vector<int> order(nA);
-  std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(),
-                   [&](int x, int y) { return (offA[x + 1] - offA[x]) < (offA[y + 1] - offA[y]); });
-  P.nPanels = (nA + SLOTS - 1) / SLOTS;
-  P.perm.assign((size_t)P.nPanels * SLOTS, -1);
-  P.lenSorted.assign((size_t)P.nPanels * SLOTS, 0);
-  P.panelOff.resize(P.nPanels + 1);
-  P.panelBlocks.resize(P.nPanels);
-  int64_t total = 0;
-  for (int p = 0; p < P.nPanels; p++) {
-    int ml = 0;
-    for (int s = 0; s < SLOTS && p * SLOTS + s < nA; s++) {
-      const int o = order[p * SLOTS + s];
-      const int len = (int)(offA[o + 1] - offA[o]);
-      P.perm[p * SLOTS + s] = o;
-      P.lenSorted[p * SLOTS + s] = len;
-      ml = len > ml ? len : ml;
-    }
-    P.panelBlocks[p] = (ml + 15) / 16;
-    P.panelOff[p] = total;
-    total += (int64_t)P.panelBlocks[p] * SLOTS;
-  }
-  P.panelOff[P.nPanels] = total;
-  P.data.assign((size_t)(total > 0 ? total : 1), make_uint4(0, 0, 0, 0));
-  for (int p = 0; p < P.nPanels; p++) {
-    uint8_t *base = reinterpret_cast<uint8_t *>(P.data.data() + P.panelOff[p]);
-    for (int s = 0; s < SLOTS && p * SLOTS + s < nA; s++) {
-      const int o = P.perm[p * SLOTS + s];
-      const uint8_t *src = opts + offA[o];
-      const int len = P.lenSorted[p * SLOTS + s];
-      for (int k = 0; k < len; k++) base[((size_t)(k / 16) * SLOTS + s) * 16 + (k % 16)] = stored[src[k]];
-    }
-  }
-  return 0;
-}
 
 __device__ __forceinline__ int remap_panel(int bx, int n) {
   if (n % 8 != 0) return bx;
@@ -301,35 +216,237 @@ __global__ __launch_bounds__(THREADS) void ed_closest_kernel(const uint4 *__rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// Host side.  One request = code map + length sort + panel fill, written
+// straight into a pinned staging buffer that is laid out exactly like the
+// device buffer, then ONE async H2D copy, the kernels and the D2H of the
+// results on one stream.  Staging/device buffers and the stream live in a
+// grow-only per-process arena (no hipMalloc/hipFree/hipHostMalloc per call;
+// hipFree would also serialise the device).  The fill runs on host threads.
+// ---------------------------------------------------------------------------
 namespace {
 
-struct Dev {
-  uint4 *panels = nullptr;
-  int64_t *panelOff = nullptr;
-  int *panelBlocks = nullptr, *lenSorted = nullptr, *perm = nullptr, *lenB = nullptr;
-  u64 *M = nullptr;
-  ~Dev() {
-    (void)hipFree(panels);
-    (void)hipFree(panelOff);
-    (void)hipFree(panelBlocks);
-    (void)hipFree(lenSorted);
-    (void)hipFree(perm);
-    (void)hipFree(lenB);
-    (void)hipFree(M);
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int host_threads() {
+  unsigned h = std::thread::hardware_concurrency();
+  int t = h ? (int)h : 4;
+  if (const char *e = getenv("M2K_ED_THREADS")) t = atoi(e);
+  return std::max(1, std::min(t, 32));
+}
+
+// f(lo, hi) over [0, n) in nt contiguous chunks
+template <class F>
+void par_for(int64_t n, int nt, int64_t grain, F f) {
+  if (n <= 0) return;
+  if (nt <= 1 || n < 2 * grain) {
+    f(0, n);
+    return;
+  }
+  nt = (int)std::min<int64_t>(nt, (n + grain - 1) / grain);
+  std::vector<std::thread> pool;
+  const int64_t chunk = (n + nt - 1) / nt;
+  for (int t = 1; t < nt; t++) {
+    const int64_t lo = t * chunk, hi = std::min(n, lo + chunk);
+    if (lo < hi) pool.emplace_back(f, lo, hi);
+  }
+  f(0, std::min(n, chunk));
+  for (auto &th : pool) th.join();
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Layout {
+  int nA = 0, nB = 0, nPanels = 0, scaled = 0;
+  int64_t totalU4 = 0;
+  size_t oPanels = 0, oPanelOff = 0, oPanelBlocks = 0, oLenSorted = 0, oPerm = 0, oLenB = 0, oM = 0;
+  size_t h2dBytes = 0, oBest = 0, bytes = 0;
+};
+
+struct Arena {
+  std::mutex mu;
+  char *host = nullptr;  // pinned staging, same layout as dev
+  char *dev = nullptr;
+  size_t cap = 0;
+  int *out = nullptr;  // ed_matrix output
+  size_t outCap = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double last[4] = {0, 0, 0, 0};  // prep, h2d, kernel, d2h (ms)
+
+  int ensure(size_t bytes) {
+    if (!stream) {
+      if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return -4;
+      for (auto &e : ev)
+        if (hipEventCreate(&e) != hipSuccess) return -4;
+    }
+    if (bytes <= cap) return 0;
+    const size_t want = std::max(bytes, cap + cap / 2);
+    if (host) (void)hipHostFree(host);
+    if (dev) (void)hipFree(dev);
+    host = dev = nullptr;
+    cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void **>(&host), want, hipHostMallocDefault) != hipSuccess) return -4;
+    if (hipMalloc(reinterpret_cast<void **>(&dev), want) != hipSuccess) return -4;
+    cap = want;
+    return 0;
+  }
+  int ensure_out(size_t bytes) {
+    if (bytes <= outCap) return 0;
+    if (out) (void)hipFree(out);
+    out = nullptr;
+    outCap = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&out), bytes) != hipSuccess) return -4;
+    outCap = bytes;
+    return 0;
   }
 };
 
-template <class T>
-bool up(T **dst, const std::vector<T> &src) {
-  const size_t bytes = sizeof(T) * (src.empty() ? 1 : src.size());
-  if (hipMalloc(dst, bytes) != hipSuccess) return false;
-  return src.empty() || hipMemcpy(*dst, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice) == hipSuccess;
+// Process lifetime on purpose: destroying HIP objects from a static destructor
+// races the runtime's own teardown.
+Arena &arena() {
+  static Arena *a = new Arena();
+  return *a;
 }
 
-int upload(const Prepared &P, Dev &d) {
-  if (!up(&d.panels, P.data) || !up(&d.panelOff, P.panelOff) || !up(&d.panelBlocks, P.panelBlocks) ||
-      !up(&d.lenSorted, P.lenSorted) || !up(&d.perm, P.perm) || !up(&d.lenB, P.lenB) || !up(&d.M, P.M))
-    return -4;
+// Dense codes ranked by option-byte frequency; 0 is reserved for padding.
+// Returns false when all 256 byte values occur (no free code for padding).
+bool build_code_map(const uint8_t *opts, int64_t nOptBytes, const uint8_t *qs, int64_t nQBytes, int nt,
+                    uint8_t code[256], int *nsym) {
+  std::vector<std::array<int64_t, 256>> part(std::max(1, nt));
+  for (auto &p : part) p.fill(0);
+  std::atomic<int> slot{0};
+  par_for(nOptBytes, nt, 1 << 20, [&](int64_t lo, int64_t hi) {
+    auto &f = part[slot.fetch_add(1)];
+    for (int64_t i = lo; i < hi; i++) f[opts[i]]++;
+  });
+  int64_t freq[256] = {0};
+  bool seen[256] = {false};
+  for (auto &p : part)
+    for (int b = 0; b < 256; b++) freq[b] += p[b];
+  for (int b = 0; b < 256; b++) seen[b] = freq[b] > 0;
+  for (int64_t i = 0; i < nQBytes; i++) seen[qs[i]] = true;
+  int order[256];
+  int n = 0;
+  for (int b = 0; b < 256; b++)
+    if (seen[b]) order[n++] = b;
+  if (n > 255) return false;
+  std::stable_sort(order, order + n, [&](int x, int y) { return freq[x] > freq[y]; });
+  memset(code, 0, 256);
+  for (int i = 0; i < n; i++) code[order[i]] = (uint8_t)(i + 1);
+  *nsym = n;
+  return true;
+}
+
+// Everything up to (not including) the H2D copy.  Returns 0 or an error code.
+int prepare(const uint8_t *opts, const int64_t *offA, int nA, const uint8_t *qs, const int64_t *offB, int nB,
+            Arena &ar, Layout &L) {
+  for (int j = 0; j < nB; j++) {
+    const int64_t len = offB[j + 1] - offB[j];
+    if (len < 0 || len > 64) return -2;
+  }
+  const int nt = host_threads();
+  uint8_t code[256];
+  int nsym = 0;
+  if (!build_code_map(opts, offA[nA], qs, offB[nB], nt, code, &nsym)) return -8;
+  L.nA = nA;
+  L.nB = nB;
+  L.scaled = nsym <= 63;
+  uint8_t stored[256];
+  for (int b = 0; b < 256; b++) stored[b] = L.scaled ? (uint8_t)(code[b] * 4) : code[b];
+
+  // stable counting sort of the options by length
+  int maxLen = 0;
+  for (int i = 0; i < nA; i++) maxLen = std::max(maxLen, (int)(offA[i + 1] - offA[i]));
+  std::vector<int> order(nA);
+  if (maxLen <= (1 << 20)) {
+    std::vector<int> start(maxLen + 2, 0);
+    for (int i = 0; i < nA; i++) start[(int)(offA[i + 1] - offA[i]) + 1]++;
+    for (int l = 0; l <= maxLen; l++) start[l + 1] += start[l];
+    for (int i = 0; i < nA; i++) order[start[(int)(offA[i + 1] - offA[i])]++] = i;
+  } else {
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int x, int y) { return (offA[x + 1] - offA[x]) < (offA[y + 1] - offA[y]); });
+  }
+  L.nPanels = (nA + SLOTS - 1) / SLOTS;
+  std::vector<int> blocks(L.nPanels);
+  std::vector<int64_t> poff(L.nPanels + 1);
+  int64_t total = 0;
+  for (int p = 0; p < L.nPanels; p++) {
+    const int last = std::min(nA, (p + 1) * SLOTS) - 1;  // sorted: the panel's longest option
+    const int o = order[last];
+    blocks[p] = (int)((offA[o + 1] - offA[o] + 15) / 16);
+    poff[p] = total;
+    total += (int64_t)blocks[p] * SLOTS;
+  }
+  poff[L.nPanels] = total;
+  L.totalU4 = total;
+
+  size_t o = 0;
+  L.oPanels = o;
+  o = align256(o + sizeof(uint4) * (size_t)std::max<int64_t>(total, 1));
+  L.oPanelOff = o;
+  o = align256(o + sizeof(int64_t) * (size_t)(L.nPanels + 1));
+  L.oPanelBlocks = o;
+  o = align256(o + sizeof(int) * (size_t)L.nPanels);
+  L.oLenSorted = o;
+  o = align256(o + sizeof(int) * (size_t)L.nPanels * SLOTS);
+  L.oPerm = o;
+  o = align256(o + sizeof(int) * (size_t)L.nPanels * SLOTS);
+  L.oLenB = o;
+  o = align256(o + sizeof(int) * (size_t)nB);
+  L.oM = o;
+  o = align256(o + sizeof(u64) * (size_t)nB * 256);
+  L.h2dBytes = o;
+  L.oBest = o;
+  o = align256(o + sizeof(u64) * (size_t)nB);
+  L.bytes = o;
+  if (int rc = ar.ensure(L.bytes)) return rc;
+
+  char *h = ar.host;
+  memcpy(h + L.oPanelOff, poff.data(), sizeof(int64_t) * poff.size());
+  memcpy(h + L.oPanelBlocks, blocks.data(), sizeof(int) * blocks.size());
+  int *lenSorted = reinterpret_cast<int *>(h + L.oLenSorted);
+  int *perm = reinterpret_cast<int *>(h + L.oPerm);
+  uint4 *panels = reinterpret_cast<uint4 *>(h + L.oPanels);
+  par_for(L.nPanels, nt, 4, [&](int64_t plo, int64_t phi) {
+    for (int64_t p = plo; p < phi; p++) {
+      uint8_t *base = reinterpret_cast<uint8_t *>(panels + poff[p]);
+      memset(base, 0, sizeof(uint4) * (size_t)blocks[p] * SLOTS);
+      for (int s = 0; s < SLOTS; s++) {
+        const int64_t k = p * SLOTS + s;
+        if (k >= nA) {
+          perm[k] = -1;
+          lenSorted[k] = 0;
+          continue;
+        }
+        const int opt = order[k];
+        const uint8_t *src = opts + offA[opt];
+        const int len = (int)(offA[opt + 1] - offA[opt]);
+        perm[k] = opt;
+        lenSorted[k] = len;
+        for (int b = 0; b * 16 < len; b++) {
+          uint8_t *dst = base + ((size_t)b * SLOTS + s) * 16;
+          const int n = std::min(16, len - b * 16);
+          for (int t = 0; t < n; t++) dst[t] = stored[src[b * 16 + t]];
+        }
+      }
+    }
+  });
+  int *lenB = reinterpret_cast<int *>(h + L.oLenB);
+  u64 *M = reinterpret_cast<u64 *>(h + L.oM);
+  par_for(nB, nt, 256, [&](int64_t lo, int64_t hi) {
+    for (int64_t j = lo; j < hi; j++) {
+      const int len = (int)(offB[j + 1] - offB[j]);
+      lenB[j] = len;
+      u64 *mj = M + (size_t)j * 256;
+      memset(mj, 0, sizeof(u64) * 256);
+      for (int k = 0; k < len; k++) mj[code[qs[offB[j] + k]]] |= (1ULL << k);
+    }
+  });
   return 0;
 }
 
@@ -340,6 +457,35 @@ int grid_x(int nPanels, int nB) {
   if (x > want) x = want;
   if (x >= 8) x = (x / 8) * 8;
   return x < 1 ? 1 : x;
+}
+
+struct DevPtrs {
+  const uint4 *panels;
+  const int64_t *panelOff;
+  const int *panelBlocks, *lenSorted, *perm, *lenB;
+  const u64 *M;
+  u64 *best;
+};
+
+DevPtrs dev_ptrs(const Arena &ar, const Layout &L) {
+  char *d = ar.dev;
+  return {reinterpret_cast<const uint4 *>(d + L.oPanels), reinterpret_cast<const int64_t *>(d + L.oPanelOff),
+          reinterpret_cast<const int *>(d + L.oPanelBlocks), reinterpret_cast<const int *>(d + L.oLenSorted),
+          reinterpret_cast<const int *>(d + L.oPerm),        reinterpret_cast<const int *>(d + L.oLenB),
+          reinterpret_cast<const u64 *>(d + L.oM),            reinterpret_cast<u64 *>(d + L.oBest)};
+}
+
+void record_times(Arena &ar, double prep) {
+  float a = 0, b = 0, c = 0;
+  (void)hipEventElapsedTime(&a, ar.ev[0], ar.ev[1]);
+  (void)hipEventElapsedTime(&b, ar.ev[1], ar.ev[2]);
+  (void)hipEventElapsedTime(&c, ar.ev[2], ar.ev[3]);
+  ar.last[0] = prep;
+  ar.last[1] = a;
+  ar.last[2] = b;
+  ar.last[3] = c;
+  if (getenv("M2K_ED_PROFILE"))
+    fprintf(stderr, "[m2k_ed] prep %.3f ms  h2d %.3f ms  kernel %.3f ms  d2h %.3f ms\n", prep, a, b, c);
 }
 
 }  // namespace
@@ -354,29 +500,36 @@ int m2k_ed_matrix(const uint8_t *opts, const int64_t *offA, int nA, const uint8_
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return -1;
   if (nA <= 0 || nB <= 0) return 0;
-  Prepared P;
-  int rc = prepare(opts, offA, nA, qs, offB, nB, P);
+  Arena &ar = arena();
+  std::lock_guard<std::mutex> lock(ar.mu);
+  const double t0 = now_ms();
+  Layout L;
+  int rc = prepare(opts, offA, nA, qs, offB, nB, ar, L);
   if (rc) return rc;
-  Dev d;
-  int *dOut = nullptr;
-  rc = upload(P, d);
-  if (rc == 0 && hipMalloc(&dOut, sizeof(int) * (size_t)nA * nB) != hipSuccess) rc = -4;
-  if (rc == 0) {
-    const int gx = grid_x(P.nPanels, nB);
-    for (int q0 = 0; q0 < nB && rc == 0; q0 += MAX_Y) {
-      const int rows = (nB - q0) < MAX_Y ? (nB - q0) : MAX_Y;
-      if (P.scaled)
-        hipLaunchKernelGGL(ed_matrix_kernel<true>, dim3(gx, rows), dim3(THREADS), 0, 0, d.panels, d.panelOff,
-                           d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, nA, P.nPanels, q0, dOut);
-      else
-        hipLaunchKernelGGL(ed_matrix_kernel<false>, dim3(gx, rows), dim3(THREADS), 0, 0, d.panels, d.panelOff,
-                           d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, nA, P.nPanels, q0, dOut);
-      if (hipGetLastError() != hipSuccess) rc = -5;
-    }
-    if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = -6;
-    if (rc == 0 && hipMemcpy(outT, dOut, sizeof(int) * (size_t)nA * nB, hipMemcpyDeviceToHost) != hipSuccess) rc = -7;
+  if ((rc = ar.ensure_out(sizeof(int) * (size_t)nA * nB))) return rc;
+  const double prep = now_ms() - t0;
+  const DevPtrs d = dev_ptrs(ar, L);
+  hipStream_t s = ar.stream;
+  (void)hipEventRecord(ar.ev[0], s);
+  if (hipMemcpyAsync(ar.dev, ar.host, L.h2dBytes, hipMemcpyHostToDevice, s) != hipSuccess) return -7;
+  (void)hipEventRecord(ar.ev[1], s);
+  const int gx = grid_x(L.nPanels, nB);
+  for (int q0 = 0; q0 < nB && rc == 0; q0 += MAX_Y) {
+    const int rows = (nB - q0) < MAX_Y ? (nB - q0) : MAX_Y;
+    if (L.scaled)
+      hipLaunchKernelGGL(ed_matrix_kernel<true>, dim3(gx, rows), dim3(THREADS), 0, s, d.panels, d.panelOff,
+                         d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, nA, L.nPanels, q0, ar.out);
+    else
+      hipLaunchKernelGGL(ed_matrix_kernel<false>, dim3(gx, rows), dim3(THREADS), 0, s, d.panels, d.panelOff,
+                         d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, nA, L.nPanels, q0, ar.out);
+    if (hipGetLastError() != hipSuccess) rc = -5;
   }
-  (void)hipFree(dOut);
+  (void)hipEventRecord(ar.ev[2], s);
+  if (rc == 0 && hipMemcpyAsync(outT, ar.out, sizeof(int) * (size_t)nA * nB, hipMemcpyDeviceToHost, s) != hipSuccess)
+    rc = -7;
+  (void)hipEventRecord(ar.ev[3], s);
+  if (hipStreamSynchronize(s) != hipSuccess && rc == 0) rc = -6;
+  if (rc == 0) record_times(ar, prep);
   return rc;
 }
 
@@ -391,38 +544,50 @@ int m2k_ed_closest(const uint8_t *opts, const int64_t *offA, int nA, const uint8
     for (int j = 0; j < nB; j++) bestIdx[j] = -1, bestDist[j] = -1;
     return 0;
   }
-  Prepared P;
-  int rc = prepare(opts, offA, nA, qs, offB, nB, P);
+  Arena &ar = arena();
+  std::lock_guard<std::mutex> lock(ar.mu);
+  const double t0 = now_ms();
+  Layout L;
+  int rc = prepare(opts, offA, nA, qs, offB, nB, ar, L);
   if (rc) return rc;
-  Dev d;
-  u64 *dBest = nullptr;
-  rc = upload(P, d);
-  if (rc == 0 && hipMalloc(&dBest, sizeof(u64) * nB) != hipSuccess) rc = -4;
-  if (rc == 0 && hipMemset(dBest, 0xff, sizeof(u64) * nB) != hipSuccess) rc = -4;
-  if (rc == 0) {
-    const int gx = grid_x(P.nPanels, nB);
-    for (int q0 = 0; q0 < nB && rc == 0; q0 += MAX_Y) {
-      const int rows = (nB - q0) < MAX_Y ? (nB - q0) : MAX_Y;
-      if (P.scaled)
-        hipLaunchKernelGGL(ed_closest_kernel<true>, dim3(gx, rows), dim3(THREADS), 0, 0, d.panels, d.panelOff,
-                           d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, P.nPanels, q0, dBest);
-      else
-        hipLaunchKernelGGL(ed_closest_kernel<false>, dim3(gx, rows), dim3(THREADS), 0, 0, d.panels, d.panelOff,
-                           d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, P.nPanels, q0, dBest);
-      if (hipGetLastError() != hipSuccess) rc = -5;
-    }
-    if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = -6;
-    if (rc == 0) {
-      std::vector<u64> h(nB);
-      if (hipMemcpy(h.data(), dBest, sizeof(u64) * nB, hipMemcpyDeviceToHost) != hipSuccess) rc = -7;
-      for (int j = 0; j < nB && rc == 0; j++) {
-        bestIdx[j] = (int32_t)(h[j] & 0xffffffffULL);
-        bestDist[j] = (int32_t)(h[j] >> 32);
-      }
-    }
+  const double prep = now_ms() - t0;
+  const DevPtrs d = dev_ptrs(ar, L);
+  hipStream_t s = ar.stream;
+  (void)hipEventRecord(ar.ev[0], s);
+  if (hipMemcpyAsync(ar.dev, ar.host, L.h2dBytes, hipMemcpyHostToDevice, s) != hipSuccess) return -7;
+  if (hipMemsetAsync(d.best, 0xff, sizeof(u64) * nB, s) != hipSuccess) return -4;
+  (void)hipEventRecord(ar.ev[1], s);
+  const int gx = grid_x(L.nPanels, nB);
+  for (int q0 = 0; q0 < nB && rc == 0; q0 += MAX_Y) {
+    const int rows = (nB - q0) < MAX_Y ? (nB - q0) : MAX_Y;
+    if (L.scaled)
+      hipLaunchKernelGGL(ed_closest_kernel<true>, dim3(gx, rows), dim3(THREADS), 0, s, d.panels, d.panelOff,
+                         d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, L.nPanels, q0, d.best);
+    else
+      hipLaunchKernelGGL(ed_closest_kernel<false>, dim3(gx, rows), dim3(THREADS), 0, s, d.panels, d.panelOff,
+                         d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, L.nPanels, q0, d.best);
+    if (hipGetLastError() != hipSuccess) rc = -5;
   }
-  (void)hipFree(dBest);
+  (void)hipEventRecord(ar.ev[2], s);
+  u64 *hBest = reinterpret_cast<u64 *>(ar.host + L.oBest);
+  if (rc == 0 && hipMemcpyAsync(hBest, d.best, sizeof(u64) * nB, hipMemcpyDeviceToHost, s) != hipSuccess) rc = -7;
+  (void)hipEventRecord(ar.ev[3], s);
+  if (hipStreamSynchronize(s) != hipSuccess && rc == 0) rc = -6;
+  if (rc == 0) {
+    for (int j = 0; j < nB; j++) {
+      bestIdx[j] = (int32_t)(hBest[j] & 0xffffffffULL);
+      bestDist[j] = (int32_t)(hBest[j] >> 32);
+    }
+    record_times(ar, prep);
+  }
   return rc;
+}
+
+// prep / H2D / kernel / D2H milliseconds of the last successful call
+void m2k_ed_last_timings(double *out4) {
+  Arena &ar = arena();
+  std::lock_guard<std::mutex> lock(ar.mu);
+  for (int i = 0; i < 4; i++) out4[i] = ar.last[i];
 }
 
 int m2k_gpu_device_count() {

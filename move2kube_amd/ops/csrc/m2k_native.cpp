@@ -440,27 +440,38 @@ py::array_t<int32_t> edit_distance_batch(const std::vector<std::string> &as, con
 
 // Pack a list of str/bytes into one buffer + int64 offsets[n+1] (the layout the
 // GPU kernel library consumes), without building n Python bytes objects.
-std::pair<py::bytes, py::array_t<int64_t>> pack_strings(const py::list &items) {
-  const size_t n = items.size();
+// Pack str/bytes items back to back: (bytes, int64 offsets[n+1], max length).
+// Two passes over borrowed list items; the result bytes object is filled in place.
+std::tuple<py::bytes, py::array_t<int64_t>, int64_t> pack_strings(const py::list &items) {
+  PyObject *lst = items.ptr();
+  const Py_ssize_t n = PyList_GET_SIZE(lst);
   py::array_t<int64_t> off(n + 1);
   int64_t *po = off.mutable_data();
-  std::string buf;
+  std::vector<const char *> ptrs((size_t)n);
   po[0] = 0;
-  for (size_t i = 0; i < n; i++) {
-    PyObject *o = items[i].ptr();
+  int64_t maxlen = 0;
+  for (Py_ssize_t i = 0; i < n; i++) {
+    PyObject *o = PyList_GET_ITEM(lst, i);
+    Py_ssize_t len = 0;
+    const char *s;
     if (PyUnicode_Check(o)) {
-      Py_ssize_t len = 0;
-      const char *s = PyUnicode_AsUTF8AndSize(o, &len);
+      s = PyUnicode_AsUTF8AndSize(o, &len);  // O(1) for ASCII strings
       if (!s) throw py::error_already_set();
-      buf.append(s, (size_t)len);
     } else if (PyBytes_Check(o)) {
-      buf.append(PyBytes_AS_STRING(o), (size_t)PyBytes_GET_SIZE(o));
+      s = PyBytes_AS_STRING(o);
+      len = PyBytes_GET_SIZE(o);
     } else {
       throw py::type_error("pack_strings: items must be str or bytes");
     }
-    po[i + 1] = (int64_t)buf.size();
+    ptrs[(size_t)i] = s;
+    po[i + 1] = po[i] + (int64_t)len;
+    if (len > maxlen) maxlen = len;
   }
-  return {py::bytes(buf), off};
+  PyObject *b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)po[n]);
+  if (!b) throw py::error_already_set();
+  char *dst = PyBytes_AS_STRING(b);
+  for (Py_ssize_t i = 0; i < n; i++) memcpy(dst + po[i], ptrs[(size_t)i], (size_t)(po[i + 1] - po[i]));
+  return std::make_tuple(py::reinterpret_steal<py::bytes>(b), off, maxlen);
 }
 
 // For every query: (first index of the minimum distance, that distance); (-1, -1) without options.

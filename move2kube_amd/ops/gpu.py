@@ -53,6 +53,8 @@ def _load():
     lib.m2k_ed_matrix.argtypes = [ctypes.c_char_p, i64p, ctypes.c_int, ctypes.c_char_p, i64p, ctypes.c_int, i32p]
     lib.m2k_ed_closest.argtypes = [ctypes.c_char_p, i64p, ctypes.c_int, ctypes.c_char_p, i64p, ctypes.c_int, i32p,
                                    i32p]
+    lib.m2k_ed_last_timings.restype = None
+    lib.m2k_ed_last_timings.argtypes = [ctypes.POINTER(ctypes.c_double)]
     lib.m2k_gpu_device_count.restype = ctypes.c_int
     lib.m2k_gpu_arch.restype = ctypes.c_char_p
     _lib = lib
@@ -68,6 +70,14 @@ def available():
     return lib is not None and lib.m2k_gpu_device_count() > 0
 
 
+def last_timings():
+    """{prep, h2d, kernel, d2h} milliseconds of the last ed_matrix/ed_closest call."""
+    lib = _lib_or_raise()
+    buf = (ctypes.c_double * 4)()
+    lib.m2k_ed_last_timings(buf)
+    return dict(zip(("prep_ms", "h2d_ms", "kernel_ms", "d2h_ms"), (round(x, 3) for x in buf)))
+
+
 def device_arch():
     lib = _load()
     return lib.m2k_gpu_arch().decode() if lib is not None else ""
@@ -78,8 +88,8 @@ def _pack(strings):
     from . import native
     m = native.module()
     if m is not None and isinstance(strings, list):
-        data, off = m.pack_strings(strings)
-        return data, off, int(np.diff(off).max()) if len(strings) else 0
+        data, off, maxlen = m.pack_strings(strings)
+        return data, off, int(maxlen)
     bs = [s.encode() if isinstance(s, str) else bytes(s) for s in strings]
     lens = np.fromiter((len(b) for b in bs), dtype=np.int64, count=len(bs))
     off = np.zeros(len(bs) + 1, dtype=np.int64)

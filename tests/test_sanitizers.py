@@ -44,7 +44,8 @@ DRIVER = textwrap.dedent(r'''
     assert mat.shape == (40, 500)
     idx, dist = m.closest_batch(opts, qs, 8)
     assert len(idx) == len(qs)
-    buf, offs = m.pack_strings(opts)
+    buf, offs, mx = m.pack_strings(opts)
+    assert mx == max(len(o) for o in opts)
     assert len(offs) == len(opts) + 1
     out = os.path.join(work, "o")
     os.makedirs(out)
