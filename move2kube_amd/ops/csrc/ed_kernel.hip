@@ -9,38 +9,38 @@
 //
 // With substitution cost == insertion + deletion the weighted distance is
 // exactly  |a| + |b| - 2 * LCS(a, b),  so each pair reduces to Hyyro's
-// bit-parallel LCS: one 64-bit word holds the DP column for a query of up to 64
-// bytes, and every character of the option costs one LDS lookup + 4 integer ops.
+// bit-parallel LCS over a DP column of |query| <= 64 bits.
 //
-// Layout (CDNA4-first; tuned from rocprofv3 PMC, see profiles/):
+// Layout (CDNA4-first; every step below was kept or dropped on rocprofv3
+// numbers, see profiles/r01_ed_kernel*):
 //  * Byte remap.  The host assigns every byte value that occurs a dense code,
-//    most frequent option byte first, code 0 = padding, and (when <= 63
-//    symbols occur) stores code*4 - the byte offset into the u32 mask table -
-//    so turning a character into an LDS address is one VALU op.  M[0] = 0,
-//    so a padding code leaves the LCS column unchanged: no per-character
-//    length checks.
-//  * Width.  Queries of <= 32 bytes run a 32-bit LCS column (u32 table,
-//    `ds_read_b32`, one VALU op per and/add/sub/or): per character ~5 VALU ops
-//    instead of ~11 for the 64-bit column.  PMC of v2 showed the kernel at
-//    ~1 VALU wave-instruction per CU-cycle, i.e. VALU-bound, so this is the
-//    lever that matters.
+//    most frequent option byte first, code 0 = padding, and (<= 63 symbols)
+//    stores code*4 so the LDS byte address of a character is one VALU op.
+//    Masks of code 0 are 0, so padding leaves a column unchanged: no
+//    per-character length checks.
+//  * Query tiles.  Queries are sorted by length and grouped so one pass over
+//    the option characters serves several queries: 8 queries <= 16 bytes
+//    (two per 32-bit word, v_pk_add_u16 keeps the halves independent),
+//    4 <= 32 bytes (one per word) or 2 <= 64 bytes (one u64 each).
+//    blockIdx.y = tile; its 4 KiB of masks are staged in LDS as two u64
+//    sub-tables, so a character costs two conflict-free ds_read_b64
+//    (banked mod 64 over 32-lane groups) whatever the tile kind.
+//  * LCS step.  U = V & M; V' = (V + U) | (V & ~M)  (V - U never borrows
+//    because U is a subset of V) = and + add + one v_bitop3_b32 per word.
 //  * Options are sorted by length and cut into panels of 512 (256 threads x 2
-//    options each: two independent dependency chains per lane hide the
-//    LDS-lookup -> VALU latency).  A panel is stored as 16-byte blocks
-//    [block][slot]: one `global_load_dwordx4` gives a lane its next 16
-//    characters (1 KiB per wave instruction), and the next block is prefetched
-//    while the current one is consumed (v1 waited on one byte load per char).
-//  * blockIdx.y = query; the query's 256-entry mask table (2 KiB) is staged in
-//    LDS once per workgroup.  blockIdx.x walks panels, remapped so consecutive
-//    panels of one query land on the same XCD (blockIdx % 8 picks the XCD).
-//  * ed_matrix kernel: distances go to a query-major [nB][nA] matrix (Python
-//    returns the transposed view, so no host transpose).
-//  * ed_closest kernel: the argmin is fused into the producer - key =
-//    (dist << 32 | original_index) is min-reduced across the wave with
-//    shuffles, across the 4 waves in LDS, then one 64-bit atomicMin per
-//    workgroup, so only nB (index, dist) pairs leave the GPU.  Ties resolve to
-//    the lowest original index, matching the reference's strict "<" scan.
-//  * queries are launched in slabs of <= 65535 rows (gridDim.y limit).
+//    options each: two independent chains per lane).  A panel is stored as
+//    16-byte blocks [block][slot]: one global_load_dwordx4 gives a lane its
+//    next 16 characters, and the next block is prefetched while the current
+//    one is consumed.  blockIdx.x walks panels, remapped XCD-aware
+//    (consecutive panels of one tile on one XCD's L2).
+//  * ed_closest fuses the argmin: key = (dist << 32 | original index), min
+//    over the wave by shuffles, over the 4 waves in LDS, then one 64-bit
+//    atomicMin per query per workgroup, so only (index, dist) pairs leave
+//    the GPU.  Ties resolve to the lowest index, like the reference's scan.
+//  * ed_matrix writes a query-major [nB][nA] matrix (Python returns the
+//    transposed view); it is bound by the scattered int32 stores and, end to
+//    end, by the device-to-host copy of the matrix itself.
+//  * Tiles are launched in slabs of <= 65535 (gridDim.y limit).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -72,28 +72,88 @@ __device__ __forceinline__ int remap_panel(int bx, int n) {
   return (bx % 8) * per + (bx / 8);
 }
 
-// One 32-bit word = 4 coded characters.  Byte i holds either the code (SCALED=0)
-// or code*4 (SCALED=1, a ready-made byte offset into the u32 table; the u64
-// table offset is twice that), so extracting a character is one VALU op.
-template <typename W, bool SCALED>
-__device__ __forceinline__ void step4(uint32_t w, const W *M, W &V) {
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t c = (w >> (8 * i)) & 0xffu;
-    const uint32_t off = SCALED ? c * (uint32_t)(sizeof(W) / 4) : c * (uint32_t)sizeof(W);
-    const W m = *reinterpret_cast<const W *>(reinterpret_cast<const char *>(M) + off);
-    const W U = V & m;
-    V = (V + U) | (V - U);
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Tile kinds: how many queries share one pass over the option characters.
+//   K16: 8 queries <= 16 bytes, two per 32-bit word (v_pk_add_u16/v_pk_sub_u16
+//        keep the halves independent, exactly two 16-bit LCS columns)
+//   K32: 4 queries <= 32 bytes, one per 32-bit word
+//   K64: 2 queries <= 64 bytes, one per 64-bit word
+enum { K16 = 0, K32 = 1, K64 = 2 };
+template <int KIND> struct TileT;
+template <> struct TileT<K16> { typedef uint32_t W; enum { NW = 4, NQ = 8 }; };
+template <> struct TileT<K32> { typedef uint32_t W; enum { NW = 4, NQ = 4 }; };
+template <> struct TileT<K64> { typedef u64 W; enum { NW = 2, NQ = 2 }; };
+
+// One LCS step of a column word against its match mask.  Hyyro's
+// V' = (V + U) | (V - U) with U = V & M; U's bits are a subset of V's, so
+// V - U borrows nowhere and equals V & ~M:  V' = (V + U) | (V & ~M) - an and,
+// an add and one 3-input v_bitop3_b32 per 32-bit word (v2 spent ~4.4 ops).
+// f(A, V, M) = A | (V & ~M) as one v_bitop3_b32 (truth table 0xF4, operand
+// bits indexing it as A*4 + V*2 + M); spelled out because the compiler emits
+// v_bfi + v_or for the 64-bit halves.
+__device__ __forceinline__ uint32_t or_andn(uint32_t a, uint32_t v, uint32_t m) {
+  return __builtin_amdgcn_bitop3_b32(a, v, m, 0xF4);
+}
+
+template <int KIND>
+__device__ __forceinline__ void lcs_step(typename TileT<KIND>::W &V, typename TileT<KIND>::W m) {
+  typedef typename TileT<KIND>::W W;
+  const W U = V & m;
+  if constexpr (KIND == K16) {
+    const uint32_t A = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, V) + __builtin_bit_cast(u16x2, U));
+    V = or_andn(A, V, m);
+  } else if constexpr (KIND == K32) {
+    V = or_andn(V + U, V, m);
+  } else {
+    const W A = V + U;
+    V = ((W)or_andn((uint32_t)(A >> 32), (uint32_t)(V >> 32), (uint32_t)(m >> 32)) << 32) |
+        or_andn((uint32_t)A, (uint32_t)V, (uint32_t)m);
   }
 }
 
-// LCS columns of this lane's OPT_PER_THREAD options in panel p.
-template <typename W, bool SCALED>
-__device__ __forceinline__ void panel_lcs(const uint4 *__restrict__ panel, int blocks, const W *M,
-                                          W (&V)[OPT_PER_THREAD]) {
+// Four coded characters of one option against every word of the tile.
+//
+// LDS layout (4 KiB per tile): two sub-tables of 256 u64 entries, sub-table h
+// at byte 2048*h.  K16/K32: entry c of sub-table h = words 2h (low half) and
+// 2h+1 (high half) of the code's masks; K64: entry c of sub-table h = query h.
+// Each character costs two `ds_read_b64` (bank = (addr/4) mod 64 over 32-lane
+// groups, so the <= 32 most frequent codes never conflict; 2 LDS cycles each).
+// The second address goes through an empty asm so the compiler cannot fuse
+// the pair into `ds_read2st64_b64` - that form banks mod 32 in 16-lane groups
+// and cost 8 cycles + ~7 conflict cycles per instruction in PMC (v5).
+template <int KIND, bool SCALED>
+__device__ __forceinline__ void step4(uint32_t w, const char *T, typename TileT<KIND>::W (&V)[TileT<KIND>::NW]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t c = (w >> (8 * i)) & 0xffu;
+    const uint32_t off = SCALED ? c * 2u : c * 8u;  // byte offset of entry c in a u64 table
+    uint32_t off1 = off + 2048u;
+    __asm__ volatile("" : "+v"(off1));
+    const u64 m0 = *reinterpret_cast<const u64 *>(T + off);
+    const u64 m1 = *reinterpret_cast<const u64 *>(T + off1);
+    if constexpr (KIND == K64) {
+      lcs_step<KIND>(V[0], m0);
+      lcs_step<KIND>(V[1], m1);
+    } else {
+      lcs_step<KIND>(V[0], (uint32_t)m0);
+      lcs_step<KIND>(V[1], (uint32_t)(m0 >> 32));
+      lcs_step<KIND>(V[2], (uint32_t)m1);
+      lcs_step<KIND>(V[3], (uint32_t)(m1 >> 32));
+    }
+  }
+}
+
+// LCS columns of this lane's OPT_PER_THREAD options in one panel against the tile.
+template <int KIND, bool SCALED>
+__device__ __forceinline__ void panel_lcs(const uint4 *__restrict__ panel, int blocks, const char *T,
+                                          typename TileT<KIND>::W (&V)[OPT_PER_THREAD][TileT<KIND>::NW]) {
+  typedef typename TileT<KIND>::W W;
   const int lane = threadIdx.x;
 #pragma unroll
-  for (int u = 0; u < OPT_PER_THREAD; u++) V[u] = ~(W)0;
+  for (int u = 0; u < OPT_PER_THREAD; u++)
+#pragma unroll
+    for (int k = 0; k < TileT<KIND>::NW; k++) V[u][k] = ~(W)0;
   if (blocks == 0) return;
   uint4 cur[OPT_PER_THREAD], nxt[OPT_PER_THREAD];
 #pragma unroll
@@ -103,116 +163,122 @@ __device__ __forceinline__ void panel_lcs(const uint4 *__restrict__ panel, int b
 #pragma unroll
       for (int u = 0; u < OPT_PER_THREAD; u++) nxt[u] = panel[(size_t)(b + 1) * SLOTS + u * THREADS + lane];
     }
-    // interleave the two independent chains word by word
-    step4<W, SCALED>(cur[0].x, M, V[0]);
-    step4<W, SCALED>(cur[1].x, M, V[1]);
-    step4<W, SCALED>(cur[0].y, M, V[0]);
-    step4<W, SCALED>(cur[1].y, M, V[1]);
-    step4<W, SCALED>(cur[0].z, M, V[0]);
-    step4<W, SCALED>(cur[1].z, M, V[1]);
-    step4<W, SCALED>(cur[0].w, M, V[0]);
-    step4<W, SCALED>(cur[1].w, M, V[1]);
+    // the two options' chains interleave word by word
+    step4<KIND, SCALED>(cur[0].x, T, V[0]);
+    step4<KIND, SCALED>(cur[1].x, T, V[1]);
+    step4<KIND, SCALED>(cur[0].y, T, V[0]);
+    step4<KIND, SCALED>(cur[1].y, T, V[1]);
+    step4<KIND, SCALED>(cur[0].z, T, V[0]);
+    step4<KIND, SCALED>(cur[1].z, T, V[1]);
+    step4<KIND, SCALED>(cur[0].w, T, V[0]);
+    step4<KIND, SCALED>(cur[1].w, T, V[1]);
 #pragma unroll
     for (int u = 0; u < OPT_PER_THREAD; u++) cur[u] = nxt[u];
   }
 }
 
-// Distances of this lane's options in panel p to the query whose masks are in
-// LDS; queries of <= 32 bytes run the 32-bit column (half the VALU work).
-template <bool SCALED>
-__device__ __forceinline__ void panel_dists(const uint4 *__restrict__ panel, int blocks, const uint32_t *M32,
-                                            const u64 *M64, int lb, int (&lcs)[OPT_PER_THREAD]) {
-  if (lb <= 32) {
-    uint32_t V[OPT_PER_THREAD];
-    panel_lcs<uint32_t, SCALED>(panel, blocks, M32, V);
-    const uint32_t mask = (lb >= 32) ? ~0u : ((1u << lb) - 1u);
-#pragma unroll
-    for (int u = 0; u < OPT_PER_THREAD; u++) lcs[u] = __popc(~V[u] & mask);
+// LCS length of tile query j from the final column words.
+template <int KIND>
+__device__ __forceinline__ int query_lcs(const typename TileT<KIND>::W (&V)[TileT<KIND>::NW], int j, int len) {
+  if constexpr (KIND == K16) {
+    const uint32_t bits = (~V[j >> 1] >> (16 * (j & 1))) & ((1u << len) - 1u);  // len <= 16
+    return __popc(bits);
+  } else if constexpr (KIND == K32) {
+    const uint32_t mask = len >= 32 ? ~0u : ((1u << len) - 1u);
+    return __popc(~V[j] & mask);
   } else {
-    u64 V[OPT_PER_THREAD];
-    panel_lcs<u64, SCALED>(panel, blocks, M64, V);
-    const u64 mask = (lb >= 64) ? ~0ULL : ((1ULL << lb) - 1ULL);
-#pragma unroll
-    for (int u = 0; u < OPT_PER_THREAD; u++) lcs[u] = __popcll(~V[u] & mask);
+    const u64 mask = len >= 64 ? ~0ULL : ((1ULL << len) - 1ULL);
+    return __popcll(~V[j] & mask);
   }
+}
+
+// Stage the tile's mask tables (4 KiB) in LDS.
+__device__ __forceinline__ void load_tile(const uint4 *__restrict__ tileM, int tile, uint4 *T) {
+  const uint4 *src = tileM + (size_t)tile * 256;
+  for (int i = threadIdx.x; i < 256; i += THREADS) T[i] = src[i];
+  __syncthreads();
 }
 
 }  // namespace
 
-template <bool SCALED>
-__global__ __launch_bounds__(THREADS) void ed_matrix_kernel(const uint4 *__restrict__ panels,
-                                                            const int64_t *__restrict__ panelOff,
-                                                            const int *__restrict__ panelBlocks,
-                                                            const int *__restrict__ lenSorted,
-                                                            const int *__restrict__ perm, const u64 *__restrict__ qmask,
-                                                            const int *__restrict__ lenB, int nA, int nPanels, int q0,
-                                                            int *__restrict__ outT) {
-  __shared__ u64 M64[256];
-  __shared__ uint32_t M32[256];
-  const int q = q0 + blockIdx.y;
-  for (int c = threadIdx.x; c < 256; c += THREADS) {
-    const u64 m = qmask[(size_t)q * 256 + c];
-    M64[c] = m;
-    M32[c] = (uint32_t)m;
-  }
-  __syncthreads();
-  const int lb = lenB[q];
+// Tile metadata: tileQ[t][8] = query index (-1 = empty), tileLen[t][8] = its length.
+template <int KIND, bool SCALED>
+__global__ __launch_bounds__(THREADS) void ed_matrix_kernel(
+    const uint4 *__restrict__ panels, const int64_t *__restrict__ panelOff, const int *__restrict__ panelBlocks,
+    const int *__restrict__ lenSorted, const int *__restrict__ perm, const uint4 *__restrict__ tileM,
+    const int *__restrict__ tileQ, const int *__restrict__ tileLen, int nA, int nPanels, int tile0,
+    int *__restrict__ outT) {
+  typedef TileT<KIND> TT;
+  __shared__ uint4 T[256];
+  const int tile = tile0 + blockIdx.y;
+  load_tile(tileM, tile, T);
+  int qid[TT::NQ], qlen[TT::NQ];
+#pragma unroll
+  for (int j = 0; j < TT::NQ; j++) qid[j] = tileQ[tile * 8 + j], qlen[j] = tileLen[tile * 8 + j];
   for (int p = remap_panel(blockIdx.x, gridDim.x); p < nPanels; p += gridDim.x) {
-    int lcs[OPT_PER_THREAD];
-    panel_dists<SCALED>(panels + panelOff[p], panelBlocks[p], M32, M64, lb, lcs);
+    typename TT::W V[OPT_PER_THREAD][TT::NW];
+    panel_lcs<KIND, SCALED>(panels + panelOff[p], panelBlocks[p], reinterpret_cast<const char *>(T), V);
 #pragma unroll
     for (int u = 0; u < OPT_PER_THREAD; u++) {
       const int s = p * SLOTS + u * THREADS + threadIdx.x;
       const int o = perm[s];
-      if (o >= 0) outT[(size_t)q * nA + o] = lenSorted[s] + lb - 2 * lcs[u];
+      if (o < 0) continue;
+      const int la = lenSorted[s];
+#pragma unroll
+      for (int j = 0; j < TT::NQ; j++)
+        if (qid[j] >= 0) outT[(size_t)qid[j] * nA + o] = la + qlen[j] - 2 * query_lcs<KIND>(V[u], j, qlen[j]);
     }
   }
 }
 
-template <bool SCALED>
-__global__ __launch_bounds__(THREADS) void ed_closest_kernel(const uint4 *__restrict__ panels,
-                                                             const int64_t *__restrict__ panelOff,
-                                                             const int *__restrict__ panelBlocks,
-                                                             const int *__restrict__ lenSorted,
-                                                             const int *__restrict__ perm,
-                                                             const u64 *__restrict__ qmask, const int *__restrict__ lenB,
-                                                             int nPanels, int q0, u64 *__restrict__ best) {
-  __shared__ u64 M64[256];
-  __shared__ uint32_t M32[256];
-  __shared__ u64 red[THREADS / 64];
-  const int q = q0 + blockIdx.y;
-  for (int c = threadIdx.x; c < 256; c += THREADS) {
-    const u64 m = qmask[(size_t)q * 256 + c];
-    M64[c] = m;
-    M32[c] = (uint32_t)m;
-  }
-  __syncthreads();
-  const int lb = lenB[q];
-  u64 key = ~0ULL;
+template <int KIND, bool SCALED>
+__global__ __launch_bounds__(THREADS) void ed_closest_kernel(
+    const uint4 *__restrict__ panels, const int64_t *__restrict__ panelOff, const int *__restrict__ panelBlocks,
+    const int *__restrict__ lenSorted, const int *__restrict__ perm, const uint4 *__restrict__ tileM,
+    const int *__restrict__ tileQ, const int *__restrict__ tileLen, int nPanels, int tile0, u64 *__restrict__ best) {
+  typedef TileT<KIND> TT;
+  __shared__ uint4 T[256];
+  __shared__ u64 red[THREADS / 64][TT::NQ];
+  const int tile = tile0 + blockIdx.y;
+  load_tile(tileM, tile, T);
+  int qid[TT::NQ], qlen[TT::NQ];
+  u64 key[TT::NQ];
+#pragma unroll
+  for (int j = 0; j < TT::NQ; j++) qid[j] = tileQ[tile * 8 + j], qlen[j] = tileLen[tile * 8 + j], key[j] = ~0ULL;
   for (int p = remap_panel(blockIdx.x, gridDim.x); p < nPanels; p += gridDim.x) {
-    int lcs[OPT_PER_THREAD];
-    panel_dists<SCALED>(panels + panelOff[p], panelBlocks[p], M32, M64, lb, lcs);
+    typename TT::W V[OPT_PER_THREAD][TT::NW];
+    panel_lcs<KIND, SCALED>(panels + panelOff[p], panelBlocks[p], reinterpret_cast<const char *>(T), V);
 #pragma unroll
     for (int u = 0; u < OPT_PER_THREAD; u++) {
       const int s = p * SLOTS + u * THREADS + threadIdx.x;
       const int o = perm[s];
-      if (o >= 0) {
-        const int d = lenSorted[s] + lb - 2 * lcs[u];
+      if (o < 0) continue;
+      const int la = lenSorted[s];
+#pragma unroll
+      for (int j = 0; j < TT::NQ; j++) {
+        const int d = la + qlen[j] - 2 * query_lcs<KIND>(V[u], j, qlen[j]);
         const u64 k = ((u64)(unsigned)d << 32) | (unsigned)o;
-        key = k < key ? k : key;
+        key[j] = k < key[j] ? k : key[j];
       }
     }
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    const u64 o = __shfl_xor(key, off, 64);
-    key = o < key ? o : key;
+  // argmin per query: wave shuffles, then the 4 waves through LDS, one atomic each
+#pragma unroll
+  for (int j = 0; j < TT::NQ; j++) {
+    u64 k = key[j];
+    for (int off = 32; off > 0; off >>= 1) {
+      const u64 o = __shfl_xor(k, off, 64);
+      k = o < k ? o : k;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x / 64][j] = k;
   }
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x / 64] = key;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    u64 k = red[0];
-    for (int w = 1; w < THREADS / 64; w++) k = red[w] < k ? red[w] : k;
-    if (k != ~0ULL) atomicMin(&best[q], k);
+  if (threadIdx.x < TT::NQ) {
+    const int j = threadIdx.x;
+    const int q = tileQ[tile * 8 + j];  // (not qid[j]: a dynamic index would spill the array)
+    u64 k = red[0][j];
+    for (int w = 1; w < THREADS / 64; w++) k = red[w][j] < k ? red[w][j] : k;
+    if (q >= 0 && k != ~0ULL) atomicMin(&best[q], k);
   }
 }
 
@@ -260,8 +326,10 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct Layout {
   int nA = 0, nB = 0, nPanels = 0, scaled = 0;
+  int nTiles = 0, kindStart[3] = {0, 0, 0}, kindCount[3] = {0, 0, 0};
   int64_t totalU4 = 0;
-  size_t oPanels = 0, oPanelOff = 0, oPanelBlocks = 0, oLenSorted = 0, oPerm = 0, oLenB = 0, oM = 0;
+  size_t oPanels = 0, oPanelOff = 0, oPanelBlocks = 0, oLenSorted = 0, oPerm = 0;
+  size_t oTileM = 0, oTileQ = 0, oTileLen = 0;
   size_t h2dBytes = 0, oBest = 0, bytes = 0;
 };
 
@@ -385,6 +453,35 @@ int prepare(const uint8_t *opts, const int64_t *offA, int nA, const uint8_t *qs,
   poff[L.nPanels] = total;
   L.totalU4 = total;
 
+  // Query tiles, by length class: 8 x <=16 B (16-bit halves), 4 x <=32 B, 2 x <=64 B.
+  std::vector<int> qorder(nB);
+  {
+    int start[66] = {0};
+    for (int j = 0; j < nB; j++) start[(int)(offB[j + 1] - offB[j]) + 1]++;
+    for (int l = 0; l <= 64; l++) start[l + 1] += start[l];
+    for (int j = 0; j < nB; j++) qorder[start[(int)(offB[j + 1] - offB[j])]++] = j;
+  }
+  std::vector<int> tileQ, tileLen;
+  int kindOfPrev = -1, fill = 0;
+  for (int r = 0; r < nB; r++) {
+    const int j = qorder[r];
+    const int len = (int)(offB[j + 1] - offB[j]);
+    const int kind = len <= 16 ? K16 : (len <= 32 ? K32 : K64);
+    const int cap = 8 >> kind;
+    if (kind != kindOfPrev || fill == cap) {
+      if (kind != kindOfPrev) L.kindStart[kind] = (int)(tileQ.size() / 8);
+      tileQ.insert(tileQ.end(), 8, -1);
+      tileLen.insert(tileLen.end(), 8, 0);
+      L.kindCount[kind]++;
+      kindOfPrev = kind;
+      fill = 0;
+    }
+    tileQ[tileQ.size() - 8 + fill] = j;
+    tileLen[tileLen.size() - 8 + fill] = len;
+    fill++;
+  }
+  L.nTiles = (int)(tileQ.size() / 8);
+
   size_t o = 0;
   L.oPanels = o;
   o = align256(o + sizeof(uint4) * (size_t)std::max<int64_t>(total, 1));
@@ -396,10 +493,12 @@ int prepare(const uint8_t *opts, const int64_t *offA, int nA, const uint8_t *qs,
   o = align256(o + sizeof(int) * (size_t)L.nPanels * SLOTS);
   L.oPerm = o;
   o = align256(o + sizeof(int) * (size_t)L.nPanels * SLOTS);
-  L.oLenB = o;
-  o = align256(o + sizeof(int) * (size_t)nB);
-  L.oM = o;
-  o = align256(o + sizeof(u64) * (size_t)nB * 256);
+  L.oTileQ = o;
+  o = align256(o + sizeof(int) * (size_t)L.nTiles * 8);
+  L.oTileLen = o;
+  o = align256(o + sizeof(int) * (size_t)L.nTiles * 8);
+  L.oTileM = o;
+  o = align256(o + (size_t)4096 * L.nTiles);
   L.h2dBytes = o;
   L.oBest = o;
   o = align256(o + sizeof(u64) * (size_t)nB);
@@ -436,25 +535,48 @@ int prepare(const uint8_t *opts, const int64_t *offA, int nA, const uint8_t *qs,
       }
     }
   });
-  int *lenB = reinterpret_cast<int *>(h + L.oLenB);
-  u64 *M = reinterpret_cast<u64 *>(h + L.oM);
-  par_for(nB, nt, 256, [&](int64_t lo, int64_t hi) {
-    for (int64_t j = lo; j < hi; j++) {
-      const int len = (int)(offB[j + 1] - offB[j]);
-      lenB[j] = len;
-      u64 *mj = M + (size_t)j * 256;
-      memset(mj, 0, sizeof(u64) * 256);
-      for (int k = 0; k < len; k++) mj[code[qs[offB[j] + k]]] |= (1ULL << k);
+  memcpy(h + L.oTileQ, tileQ.data(), sizeof(int) * tileQ.size());
+  memcpy(h + L.oTileLen, tileLen.data(), sizeof(int) * tileLen.size());
+  char *tm = h + L.oTileM;
+  par_for(L.nTiles, nt, 32, [&](int64_t lo, int64_t hi) {
+    for (int64_t t = lo; t < hi; t++) {
+      char *T = tm + (size_t)t * 4096;
+      memset(T, 0, 4096);
+      const int kind = t >= L.kindStart[K64] && L.kindCount[K64] && t < L.kindStart[K64] + L.kindCount[K64]
+                           ? K64
+                           : (t >= L.kindStart[K32] && L.kindCount[K32] && t < L.kindStart[K32] + L.kindCount[K32]
+                                  ? K32
+                                  : K16);
+      for (int slot = 0; slot < (8 >> kind); slot++) {
+        const int j = tileQ[t * 8 + slot];
+        if (j < 0) continue;
+        const int len = tileLen[t * 8 + slot];
+        for (int k = 0; k < len; k++) {
+          const int c = code[qs[offB[j] + k]];
+          // word = the 32-bit column word holding this query; sub-table word/2, half word%2
+          u64 *T64 = reinterpret_cast<u64 *>(T);
+          if (kind == K64) {
+            T64[slot * 256 + c] |= 1ULL << k;
+          } else {
+            const int word = kind == K32 ? slot : (slot >> 1);
+            const int bit = kind == K32 ? k : k + 16 * (slot & 1);
+            T64[(word >> 1) * 256 + c] |= (u64)(1u << bit) << (32 * (word & 1));
+          }
+        }
+      }
     }
   });
   return 0;
 }
 
-int grid_x(int nPanels, int nB) {
-  // >> 256 CUs worth of workgroups in total; x a multiple of 8 for the XCD remap
-  int x = nPanels;
-  const int want = (nB >= 2048) ? 8 : (nB >= 256 ? 64 : 1024);
-  if (x > want) x = want;
+int grid_x(int nPanels, int tiles) {
+  // ~4k workgroups per launch: ~2 rounds of the 256 CUs x 7 resident 256-thread
+  // groups, each walking enough panels to amortise staging its 4 KiB tile table
+  // and the per-query reductions (16k tiny groups measured 3x slower for K16).
+  // x is a multiple of 8 for the XCD remap.
+  int want = (4096 + tiles - 1) / tiles;
+  want = std::max(8, std::min(want, 1024));
+  int x = std::min(nPanels, want);
   if (x >= 8) x = (x / 8) * 8;
   return x < 1 ? 1 : x;
 }
@@ -462,8 +584,8 @@ int grid_x(int nPanels, int nB) {
 struct DevPtrs {
   const uint4 *panels;
   const int64_t *panelOff;
-  const int *panelBlocks, *lenSorted, *perm, *lenB;
-  const u64 *M;
+  const int *panelBlocks, *lenSorted, *perm, *tileQ, *tileLen;
+  const uint4 *tileM;
   u64 *best;
 };
 
@@ -471,8 +593,45 @@ DevPtrs dev_ptrs(const Arena &ar, const Layout &L) {
   char *d = ar.dev;
   return {reinterpret_cast<const uint4 *>(d + L.oPanels), reinterpret_cast<const int64_t *>(d + L.oPanelOff),
           reinterpret_cast<const int *>(d + L.oPanelBlocks), reinterpret_cast<const int *>(d + L.oLenSorted),
-          reinterpret_cast<const int *>(d + L.oPerm),        reinterpret_cast<const int *>(d + L.oLenB),
-          reinterpret_cast<const u64 *>(d + L.oM),            reinterpret_cast<u64 *>(d + L.oBest)};
+          reinterpret_cast<const int *>(d + L.oPerm),        reinterpret_cast<const int *>(d + L.oTileQ),
+          reinterpret_cast<const int *>(d + L.oTileLen),     reinterpret_cast<const uint4 *>(d + L.oTileM),
+          reinterpret_cast<u64 *>(d + L.oBest)};
+}
+
+template <int KIND, bool SCALED>
+int launch_kind(const Layout &L, const DevPtrs &d, int nA, int *out, hipStream_t s) {
+  const int count = L.kindCount[KIND];
+  if (count == 0) return 0;
+  const int gx = grid_x(L.nPanels, count);
+  for (int t = 0; t < count; t += MAX_Y) {
+    const int rows = std::min(MAX_Y, count - t);
+    const int tile0 = L.kindStart[KIND] + t;
+    if (out)
+      hipLaunchKernelGGL((ed_matrix_kernel<KIND, SCALED>), dim3(gx, rows), dim3(THREADS), 0, s, d.panels, d.panelOff,
+                         d.panelBlocks, d.lenSorted, d.perm, d.tileM, d.tileQ, d.tileLen, nA, L.nPanels, tile0, out);
+    else
+      hipLaunchKernelGGL((ed_closest_kernel<KIND, SCALED>), dim3(gx, rows), dim3(THREADS), 0, s, d.panels,
+                         d.panelOff, d.panelBlocks, d.lenSorted, d.perm, d.tileM, d.tileQ, d.tileLen, L.nPanels, tile0,
+                         d.best);
+    if (hipGetLastError() != hipSuccess) return -5;
+  }
+  return 0;
+}
+
+template <bool SCALED>
+int launch_all(const Layout &L, const DevPtrs &d, int nA, int *out, hipStream_t s) {
+  int rc = launch_kind<K16, SCALED>(L, d, nA, out, s);
+  if (rc == 0) rc = launch_kind<K32, SCALED>(L, d, nA, out, s);
+  if (rc == 0) rc = launch_kind<K64, SCALED>(L, d, nA, out, s);
+  return rc;
+}
+
+int launch_matrix(const Layout &L, const DevPtrs &d, int nA, int *out, hipStream_t s) {
+  return L.scaled ? launch_all<true>(L, d, nA, out, s) : launch_all<false>(L, d, nA, out, s);
+}
+
+int launch_closest(const Layout &L, const DevPtrs &d, hipStream_t s) {
+  return L.scaled ? launch_all<true>(L, d, 0, nullptr, s) : launch_all<false>(L, d, 0, nullptr, s);
 }
 
 void record_times(Arena &ar, double prep) {
@@ -513,17 +672,7 @@ int m2k_ed_matrix(const uint8_t *opts, const int64_t *offA, int nA, const uint8_
   (void)hipEventRecord(ar.ev[0], s);
   if (hipMemcpyAsync(ar.dev, ar.host, L.h2dBytes, hipMemcpyHostToDevice, s) != hipSuccess) return -7;
   (void)hipEventRecord(ar.ev[1], s);
-  const int gx = grid_x(L.nPanels, nB);
-  for (int q0 = 0; q0 < nB && rc == 0; q0 += MAX_Y) {
-    const int rows = (nB - q0) < MAX_Y ? (nB - q0) : MAX_Y;
-    if (L.scaled)
-      hipLaunchKernelGGL(ed_matrix_kernel<true>, dim3(gx, rows), dim3(THREADS), 0, s, d.panels, d.panelOff,
-                         d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, nA, L.nPanels, q0, ar.out);
-    else
-      hipLaunchKernelGGL(ed_matrix_kernel<false>, dim3(gx, rows), dim3(THREADS), 0, s, d.panels, d.panelOff,
-                         d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, nA, L.nPanels, q0, ar.out);
-    if (hipGetLastError() != hipSuccess) rc = -5;
-  }
+  rc = launch_matrix(L, d, nA, ar.out, s);
   (void)hipEventRecord(ar.ev[2], s);
   if (rc == 0 && hipMemcpyAsync(outT, ar.out, sizeof(int) * (size_t)nA * nB, hipMemcpyDeviceToHost, s) != hipSuccess)
     rc = -7;
@@ -557,17 +706,7 @@ int m2k_ed_closest(const uint8_t *opts, const int64_t *offA, int nA, const uint8
   if (hipMemcpyAsync(ar.dev, ar.host, L.h2dBytes, hipMemcpyHostToDevice, s) != hipSuccess) return -7;
   if (hipMemsetAsync(d.best, 0xff, sizeof(u64) * nB, s) != hipSuccess) return -4;
   (void)hipEventRecord(ar.ev[1], s);
-  const int gx = grid_x(L.nPanels, nB);
-  for (int q0 = 0; q0 < nB && rc == 0; q0 += MAX_Y) {
-    const int rows = (nB - q0) < MAX_Y ? (nB - q0) : MAX_Y;
-    if (L.scaled)
-      hipLaunchKernelGGL(ed_closest_kernel<true>, dim3(gx, rows), dim3(THREADS), 0, s, d.panels, d.panelOff,
-                         d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, L.nPanels, q0, d.best);
-    else
-      hipLaunchKernelGGL(ed_closest_kernel<false>, dim3(gx, rows), dim3(THREADS), 0, s, d.panels, d.panelOff,
-                         d.panelBlocks, d.lenSorted, d.perm, d.M, d.lenB, L.nPanels, q0, d.best);
-    if (hipGetLastError() != hipSuccess) rc = -5;
-  }
+  rc = launch_closest(L, d, s);
   (void)hipEventRecord(ar.ev[2], s);
   u64 *hBest = reinterpret_cast<u64 *>(ar.host + L.oBest);
   if (rc == 0 && hipMemcpyAsync(hBest, d.best, sizeof(u64) * nB, hipMemcpyDeviceToHost, s) != hipSuccess) rc = -7;

@@ -119,3 +119,20 @@ def test_uneven_lengths_and_padding_slots():
     gi, gd = gpu.ed_closest(opts, qs)
     ci, cd = native.module().closest_batch(opts, qs, 8)
     assert np.array_equal(gi, ci) and np.array_equal(gd, cd)
+
+
+def test_tile_classes_boundaries_and_wide_alphabet():
+    """Query lengths at every tile-class edge (8 x 16-bit, 4 x 32-bit, 2 x 64-bit
+    per workgroup) with partially filled tiles, on a > 63-symbol alphabet (the
+    unscaled-code kernels) and on a small one (scaled codes)."""
+    rng = random.Random(21)
+    for alphabet in ("".join(chr(c) for c in range(32, 127)), "acgt"):
+        opts = _rand_strings(rng, 1100, 0, 70, alphabet=alphabet)
+        qs = []
+        for n in (0, 1, 15, 16, 17, 31, 32, 33, 63, 64):
+            qs += _rand_strings(rng, 3, n, n, alphabet=alphabet)
+        rng.shuffle(qs)
+        assert np.array_equal(gpu.ed_matrix(opts, qs), _ref_matrix(opts, qs))
+        gi, gd = gpu.ed_closest(opts, qs)
+        ci, cd = native.module().closest_batch(opts, qs, 8)
+        assert np.array_equal(gi, ci) and np.array_equal(gd, cd)
