@@ -111,14 +111,17 @@ def plan_handler(a):
     if not os.path.isdir(srcpath):
         log.fatal("Input is a file, expected directory: %s", srcpath)
     if not os.path.exists(planfile):
-        if a.plan.endswith(os.sep) or "." not in os.path.basename(planfile):
+        # (the reference tests the trailing separator on the already-cleaned
+        # absolute path, so only an extension-less base name selects a directory)
+        if planfile.endswith(os.sep) or "." not in os.path.basename(planfile):
             planfile = os.path.join(planfile, DEFAULT_PLAN_FILE)
     elif os.path.isdir(planfile):
         planfile = os.path.join(planfile, DEFAULT_PLAN_FILE)
     p = move2kube.create_plan(srcpath, a.name)
     try:
         d = os.path.dirname(planfile)
-        if d:
+        if d and settings.fixed:
+            # the reference writes with ioutil.WriteFile: a missing directory is an error
             os.makedirs(d, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
         plantypes.write_plan(planfile, p)
     except OSError as e:

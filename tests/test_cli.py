@@ -1,0 +1,138 @@
+"""CLI verbs and flag semantics, in process (reference ``cmd/move2kube/*.go``):
+plan-path resolution (``plan.go:38-80``), translate with and without a plan,
+name/root overrides, the plan/source flag rules (``translate.go:93-177``),
+QA-cache slices, version output (``version.go``)."""
+
+import os
+import shutil
+
+import pytest
+
+from move2kube_amd.cli import main as cli
+from move2kube_amd.models import plan as plantypes
+from move2kube_amd.utils import yamlio
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture
+def work(tmp_path, monkeypatch):
+    monkeypatch.setenv("M2K_NO_NETWORK", "1")
+    monkeypatch.setenv("M2K_DISABLE_CNB", "1")
+    src = tmp_path / "src"
+    shutil.copytree(os.path.join(ROOT, "samples", "nodejs"), str(src / "nodejs"))
+    (src / ".m2kignore").write_text(".\n")
+    cwd = tmp_path / "cwd"
+    cwd.mkdir()
+    monkeypatch.chdir(cwd)
+    return tmp_path
+
+
+def _plan(path):
+    return plantypes.read_plan(str(path))
+
+
+def test_plan_default_file_in_cwd(work):
+    assert cli.main(["plan", "-s", str(work / "src")]) == 0
+    p = _plan(work / "cwd" / "m2k.plan")
+    assert p.name == "myproject" and "nodejs" in p.services
+    # the plan stores the root relative to the working directory
+    with open(work / "cwd" / "m2k.plan") as f:
+        assert "rootDir: ../src" in f.read()
+
+
+def test_plan_into_existing_directory_and_name(work):
+    (work / "plans").mkdir()
+    assert cli.main(["plan", "-s", str(work / "src"), "-p", str(work / "plans"), "-n", "shop"]) == 0
+    assert _plan(work / "plans" / "m2k.plan").name == "shop"
+
+
+def test_plan_extensionless_missing_path_is_a_directory(work):
+    target = work / "cwd" / "newdir"
+    # missing extension-less path -> <path>/m2k.plan; the reference does not
+    # create the directory, so the write fails (logged, exit 0)
+    assert cli.main(["plan", "-s", str(work / "src"), "-p", str(target)]) == 0
+    assert not (target / "m2k.plan").exists()
+    assert cli.main(["plan", "-s", str(work / "src"), "-p", str(work / "cwd" / "x.plan")]) == 0
+    assert (work / "cwd" / "x.plan").exists()
+
+
+@pytest.mark.parametrize("bad", ["missing", "file"])
+def test_plan_bad_source_is_fatal(work, bad):
+    (work / "file").write_text("x")
+    assert cli.main(["plan", "-s", str(work / bad)]) == 1
+
+
+def test_plan_requires_source(work):
+    with pytest.raises(SystemExit):
+        cli.main(["plan"])
+
+
+def test_translate_without_plan_plans_and_curates(work):
+    assert cli.main(["translate", "-s", str(work / "src"), "-o", str(work / "out"), "--qaskip"]) == 0
+    out = work / "out" / "myproject"
+    assert (out / "myproject" / "nodejs-deployment.yaml").exists()
+    assert (out / "m2kqacache.yaml").exists()
+
+
+def test_translate_needs_plan_or_source(work):
+    # no m2k.plan in cwd and no -s: fatal
+    assert cli.main(["translate", "--qaskip"]) == 1
+    # an explicit plan path that does not exist is fatal even with -s
+    assert cli.main(["translate", "-p", str(work / "nope.plan"), "-s", str(work / "src"), "--qaskip"]) == 1
+
+
+def test_translate_with_plan_name_and_root_overrides(work):
+    assert cli.main(["plan", "-s", str(work / "src")]) == 0
+    # plan from cwd, renamed
+    assert cli.main(["translate", "-n", "renamed", "-o", str(work / "out"), "--qaskip"]) == 0
+    assert (work / "out" / "renamed" / "renamed" / "nodejs-deployment.yaml").exists()
+    # same plan re-rooted onto a moved copy of the source
+    shutil.copytree(str(work / "src"), str(work / "moved"))
+    shutil.rmtree(str(work / "src"))
+    assert cli.main(["translate", "-s", str(work / "moved"), "-o", str(work / "out2"), "--qaskip"]) == 0
+    text = (work / "out2" / "myproject" / "copysources.sh").read_text()
+    assert "moved" in text
+
+
+def test_translate_plan_with_missing_root_is_fatal(work):
+    assert cli.main(["plan", "-s", str(work / "src")]) == 0
+    shutil.rmtree(str(work / "src"))
+    assert cli.main(["translate", "-o", str(work / "out"), "--qaskip"]) == 1
+
+
+def test_translate_qacache_slices_and_precedence(work):
+    def cache(path, answer):
+        path.write_text(yamlio.dump({
+            "apiVersion": "move2kube.konveyor.io/v1alpha1", "kind": "QACache",
+            "spec": {"solutions": [{"description": "Choose the artifact type:",
+                                    "solution": {"type": "Select", "answer": [answer]}, "resolved": True}]}}))
+        return str(path)
+    a = cache(work / "a.yaml", "Helm")
+    b = cache(work / "b.yaml", "Knative")
+    # comma-joined and repeated -q both work; the LAST cache listed has the
+    # highest priority (translate.go reverses the list, AddCaches prepends it)
+    assert cli.main(["translate", "-s", str(work / "src"), "-o", str(work / "o1"), "--qaskip", "-q", b + "," + a]) == 0
+    assert (work / "o1" / "myproject" / "myproject" / "Chart.yaml").exists()
+    assert cli.main(["translate", "-s", str(work / "src"), "-o", str(work / "o2"), "--qaskip", "-q", a, "-q", b]) == 0
+    assert "serving.knative.dev" in (work / "o2" / "myproject" / "myproject" / "nodejs-service.yaml").read_text()
+
+
+def test_translate_output_path_is_a_file(work):
+    (work / "out").mkdir()
+    (work / "out" / "myproject").write_text("not a dir")
+    assert cli.main(["translate", "-s", str(work / "src"), "-o", str(work / "out"), "--qaskip"]) == 1
+
+
+def test_version(capsys):
+    assert cli.main(["version"]) == 0
+    short = capsys.readouterr().out.strip()
+    assert short.startswith("v")
+    assert cli.main(["version", "-l"]) == 0
+    long = yamlio.load(capsys.readouterr().out)
+    assert long["version"] == short and long["goVersion"].startswith("python")
+
+
+def test_no_command_prints_help(capsys):
+    assert cli.main([]) == 0
+    assert "translate" in capsys.readouterr().out
