@@ -1,0 +1,98 @@
+"""Compose v3 feature coverage (reference ``internal/source/compose/v3.go:135-651``)
+on one file that uses every mapped key: container fields, security context,
+pid/hostname/domainname, long and short ports with expose, healthcheck ->
+liveness probe, deploy mode/resources/restart_policy/replicas, tmpfs,
+secrets and configs (top-level storages and per-service mounts), bind and
+named volumes, networks."""
+
+import os
+import shutil
+
+import pytest
+
+from move2kube_amd import api
+from move2kube_amd.source.compose import utils as cutils
+from move2kube_amd.utils import common, yamlio
+from move2kube_amd.utils.constants import settings
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIXTURE = os.path.join(ROOT, "tests", "fixtures", "compose_v3_full")
+
+
+def _translate(tmp_path, monkeypatch, compat):
+    monkeypatch.setenv("M2K_NO_NETWORK", "1")
+    monkeypatch.setenv("M2K_DISABLE_CNB", "1")
+    monkeypatch.setattr(settings, "compat", compat)
+    src = str(tmp_path / "app")
+    shutil.copytree(FIXTURE, src)
+    out = api.translate(src, str(tmp_path / "out"), name="full")
+    objs = {}
+    for f in sorted(os.listdir(os.path.join(out, "full"))):
+        with open(os.path.join(out, "full", f)) as fh:
+            objs[f] = yamlio.load(fh.read())
+    return src, out, objs
+
+
+def test_reference_mode_objects(tmp_path, monkeypatch):
+    src, out, objs = _translate(tmp_path, monkeypatch, "reference")
+    # the reference's Deployment handler does not list DaemonSet among its kinds,
+    # so a deploy.mode=global service gets no workload object (only its Service)
+    assert "web-daemonset.yaml" not in objs and "web-service.yaml" in objs
+    assert objs["worker-deployment.yaml"]["spec"]["replicas"] == 3
+    svc = objs["web-service.yaml"]
+    assert [(p["port"], p["targetPort"]) for p in svc["spec"]["ports"]] == [(8080, 80), (8443, 443), (5353, 53), (9000, 9000)]
+    assert svc["metadata"]["annotations"]["tier"] == "front"
+    # top-level secrets/configs -> Secret/ConfigMap objects
+    assert objs["db-pass-secret.yaml"]["data"] == {"db_pass": "czNjcmV0Cg=="}
+    assert "data" not in objs["api-key-secret.yaml"]          # external: no content
+    assert objs["app-cfg-configmap.yaml"]["data"] == {"app_cfg": "listen=80\n"}
+    assert objs["conf-dir-configmap.yaml"]["data"] == {"app.conf": "listen=80\n", "other.ini": "[x]\ny=1\n"}
+    assert objs["cache-persistentvolumeclaim.yaml"]["spec"]["storageClassName"] == "default"
+    np_ = objs["front-network-networkpolicy.yaml"]
+    assert np_["spec"]["podSelector"]["matchLabels"] == {"move2kube.konveyor.io/network/front-network": "true"}
+
+
+def test_fixed_mode_daemonset(tmp_path, monkeypatch):
+    src, out, objs = _translate(tmp_path, monkeypatch, "fixed")
+    ds = objs["web-daemonset.yaml"]
+    assert ds["kind"] == "DaemonSet"
+    pod = ds["spec"]["template"]["spec"]
+    assert pod["hostPID"] is True and pod["hostname"] == "webhost" and pod["subdomain"] == "example.org"
+    assert pod["restartPolicy"] == "Always"                    # unless-stopped -> Always
+    (c,) = pod["containers"]
+    assert c["name"] == "web-frontend"                         # container_name, lower-cased
+    assert c["command"] == ["/entry.sh"] and c["args"] == ["--port", "80"]
+    assert c["workingDir"] == "/srv" and c["stdin"] is True and c["tty"] is True
+    assert c["env"] == [{"name": "EMPTY", "value": "unknown"}, {"name": "MODE", "value": "prod"}]
+    assert c["securityContext"] == {"capabilities": {"add": ["NET_ADMIN"], "drop": ["ALL"]},
+                                    "privileged": True, "runAsUser": 1000}
+    assert c["livenessProbe"] == {"exec": {"command": ["curl -f http://localhost"]}, "failureThreshold": 3,
+                                  "initialDelaySeconds": 40, "periodSeconds": 30, "timeoutSeconds": 10}
+    # memory quantities built with an unknown format print in DecimalExponent form
+    assert c["resources"] == {"limits": {"cpu": "500m", "memory": "536870912"},
+                              "requests": {"cpu": "250m", "memory": "134217728"}}
+    assert [(p["containerPort"], p["protocol"]) for p in c["ports"]] == [(80, "TCP"), (443, "TCP"), (53, "UDP"),
+                                                                        (9000, "TCP")]
+    mounts = {m["name"]: m for m in c["volumeMounts"]}
+    assert mounts["web-tmpfs-0"]["mountPath"] == "/run"
+    assert mounts["db_pass"]["mountPath"] == "/var/secrets/db_pass"
+    assert mounts["api_key"]["mountPath"] == "/etc/keys/api"
+    assert mounts["app-cfg"] == {"mountPath": "/etc/app/app.conf", "name": "app-cfg", "subPath": "app.conf"}
+    assert mounts["conf-dir"] == {"mountPath": "/conf_dir", "name": "conf-dir", "subPath": "conf_dir"}
+    assert mounts["cache"]["mountPath"] == "/cache"
+    vols = {v["name"]: v for v in pod["volumes"]}
+    assert vols["web-tmpfs-0"]["emptyDir"] == {"medium": "Memory"}
+    assert vols["api_key"]["secret"] == {"defaultMode": 0o400, "items": [{"key": "api_key", "path": "api_key"}],
+                                         "secretName": "api_key"}
+    assert vols["app-cfg"]["configMap"] == {"defaultMode": 0o440, "items": [{"key": "app.conf", "path": "app.conf"}],
+                                            "name": "app-cfg"}
+    assert vols["cache"]["persistentVolumeClaim"] == {"claimName": "cache"}
+    data = os.path.join(src, "data")
+    host = [v for v in pod["volumes"] if "hostPath" in v]
+    assert host == [{"hostPath": {"path": data}, "name": "vol%d" % common.fnv64a(data.encode())}]
+
+
+@pytest.mark.parametrize("value,want", [(536870912, "536870912"), (512000000, "512e6"), (1000, "1e3"),
+                                        (1500, "1500"), (0, "0")])
+def test_decimal_exponent_quantities(value, want):
+    assert cutils.format_quantity_decimal_exponent(value) == want
