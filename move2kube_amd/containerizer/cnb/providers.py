@@ -25,6 +25,10 @@ from ...utils import common, log
 from ...utils.constants import settings
 
 ORDER_LABEL = "io.buildpacks.buildpack.order"
+# bounds for external tools (the reference waits forever; a hung pull or
+# detector must not hang `plan`)
+PULL_TIMEOUT_S = 1800
+RUN_TIMEOUT_S = 600
 DOCKER_SOCK = "/var/run/docker.sock"
 
 _warned_not_supported = False
@@ -332,11 +336,13 @@ class RuncProvider:
             if os.path.exists(os.path.join(images, image)):
                 continue
             p = subprocess.run(["skopeo", "copy", "docker://" + b, "oci:" + image + ":" + tag], cwd=images,
-                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                               timeout=PULL_TIMEOUT_S)
             if p.returncode != 0:
                 continue
             subprocess.run(["umoci", "unpack", "--image", image + ":" + tag, os.path.abspath(os.path.join(bundles, image))],
-                           cwd=images, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                           cwd=images, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                           timeout=RUN_TIMEOUT_S)
 
     def is_builder_supported(self, path, builder):
         if not self.is_available():
@@ -361,7 +367,8 @@ class RuncProvider:
         spec["process"]["terminal"] = False
         common.write_json(cfg_path, spec)
         p = subprocess.run(["runc", "run", "cnbbuilder"], cwd=os.path.dirname(cfg_path),
-                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                           timeout=RUN_TIMEOUT_S)
         if p.returncode != 0:
             raise ProviderError("Error while executing runc")
         return b"ERROR: No buildpack groups passed detection." not in p.stdout

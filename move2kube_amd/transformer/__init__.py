@@ -251,9 +251,13 @@ class K8sTransformer(Transformer):
             shutil.rmtree(opath, ignore_errors=True)
         _mkdir(opath)
         chart = os.path.abspath(os.path.join(basepath, project))
-        p = subprocess.run([sdk, "init", "--plugins=helm", "--helm-chart=" + chart, "--domain=io", "--group=" + project,
-                            "--version=v1alpha1"], cwd=opath, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                           stdin=subprocess.DEVNULL)
+        try:
+            p = subprocess.run([sdk, "init", "--plugins=helm", "--helm-chart=" + chart, "--domain=io",
+                                "--group=" + project, "--version=v1alpha1"], cwd=opath, stdout=subprocess.PIPE,
+                               stderr=subprocess.PIPE, stdin=subprocess.DEVNULL, timeout=600)
+        except (OSError, subprocess.SubprocessError) as e:
+            log.warning("Error during operator creation : %s", e)
+            return False
         if p.returncode != 0:
             log.warning("Error during operator creation : exit status %d, %s", p.returncode, p.stdout.decode("utf-8", "replace"))
             return False
