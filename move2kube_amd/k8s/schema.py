@@ -351,7 +351,8 @@ _empty = {}
 
 
 def _plan(typ):
-    """Per struct type: (json name, field type, omitempty, value when absent)."""
+    """Per struct type: (json name, field type, omitempty, value when absent,
+    compiled value marshaller, compiled omitempty test)."""
     pl = _plans.get(typ)
     if pl is None:
         pl = []
@@ -368,9 +369,74 @@ def _plan(typ):
                 absent = None
             else:
                 absent = _zero(ftype)
-            pl.append((jname, ftype, omit, absent))
+            empty = _empty_fn(ftype) if omit else None
+            pl.append((jname, ftype, omit, absent, _value_fn(ftype), empty))
         pl = _plans[typ] = tuple(pl)
     return pl
+
+
+# -- compiled per-type marshallers (same semantics as _marshal_value/_is_empty,
+#    without re-parsing the type string for every value) ----------------------
+
+_value_fns = {}
+_empty_fns = {}
+
+
+def _ident(v):
+    return v
+
+
+def _str_value(v):
+    return v if isinstance(v, str) else ("" if v is None else v)
+
+
+def _value_fn(typ):
+    fn = _value_fns.get(typ)
+    if fn is None:
+        fn = _value_fns[typ] = _compile_value(typ)
+    return fn
+
+
+def _compile_value(typ):
+    if typ.startswith("*"):
+        inner = _value_fn(typ[1:])
+        return lambda v: None if v is None else inner(v)
+    if typ.startswith("[]"):
+        inner = _value_fn(typ[2:])
+        return lambda v: None if v is None else [inner(x) for x in v]
+    if typ == "map":
+        return lambda v: None if v is None else dict(v)
+    if typ.startswith("map:"):
+        inner = _value_fn(typ[4:])
+        return lambda v: None if v is None else {k: inner(x) for k, x in v.items()}
+    if typ in ("bytes", "Time", "RawExtension"):
+        return lambda v: _marshal_value(v, typ)
+    if typ in ("string", "Quantity", "ArrayOrString"):
+        return _str_value
+    if typ == "bool":
+        return bool
+    if typ in _STRUCTS:
+        return lambda v: _marshal_struct(v or {}, typ)
+    return _ident  # int, IntOrString, any, unknown
+
+
+def _empty_fn(typ):
+    fn = _empty_fns.get(typ)
+    if fn is None:
+        if typ.startswith("*"):
+            fn = lambda v: False  # noqa: E731
+        elif typ == "string":
+            fn = lambda v: v == ""  # noqa: E731
+        elif typ == "int":
+            fn = lambda v: v == 0  # noqa: E731
+        elif typ == "bool":
+            fn = lambda v: v is False  # noqa: E731
+        elif typ.startswith("[]") or typ.startswith("map") or typ == "bytes":
+            fn = lambda v: len(v) == 0  # noqa: E731
+        else:
+            fn = lambda v, t=typ: _is_empty(v, t)  # noqa: E731
+        _empty_fns[typ] = fn
+    return fn
 
 
 def _empty_struct(typ):
@@ -390,7 +456,7 @@ def _marshal_struct(d, typ):
 def _marshal_fields(d, typ):
     out = {}
     get = d.get
-    for jname, ftype, omit, absent in _plan(typ):
+    for jname, ftype, omit, absent, value, empty in _plan(typ):
         if jname == "inline":
             out.update(_marshal_struct(d, ftype))
             continue
@@ -400,9 +466,9 @@ def _marshal_fields(d, typ):
                 continue
             out[jname] = _empty_struct(ftype) if absent is _EMPTY_STRUCT else absent
             continue
-        if omit and _is_empty(v, ftype):
+        if omit and empty(v):
             continue
-        out[jname] = _marshal_value(v, ftype)
+        out[jname] = value(v)
     return out
 
 

@@ -9,7 +9,6 @@ from hypothesis import given, settings, strategies as st
 from move2kube_amd.ops import editdistance, native
 from move2kube_amd.utils import yamlio
 
-import yaml
 
 _text = st.text(alphabet=st.characters(blacklist_categories=("Cs",), blacklist_characters="﻿\x85  "),
                 max_size=20)
@@ -27,7 +26,9 @@ def _norm(v):
 @given(st.dictionaries(_text, _values, max_size=5))
 def test_dump_roundtrips_through_yaml_loader(doc):
     text = yamlio.dump(doc)
-    back = yaml.load(text, Loader=yaml.SafeLoader)
+    # decoded with the go-yaml v3 resolution rules (PyYAML's YAML 1.1 SafeLoader
+    # also resolves e.g. "=" (the 1.1 "value" type), which go-yaml emits plain)
+    back = yamlio.load(text)
     assert back == (doc or {}), text
 
 
