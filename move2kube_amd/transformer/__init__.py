@@ -46,6 +46,7 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
     log.debug("Total number of containers : %d", len(containers))
     buildscripts, dockerimages, manualimages = [], [], []
     batch = []
+    made = set()
     for c in containers:
         if not c.new:
             continue
@@ -55,11 +56,14 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
         dockerimages.extend(c.image_names)
         for rel in sorted(c.new_files):
             wp = os.path.join(cpath, rel)
-            try:
-                _mkdir(os.path.dirname(wp))
-            except OSError as e:
-                log.error("Unable to create directory %s : %s", os.path.dirname(wp), e)
-                continue
+            d = os.path.dirname(wp)
+            if d not in made:
+                try:
+                    _mkdir(d)
+                except OSError as e:
+                    log.error("Unable to create directory %s : %s", d, e)
+                    continue
+                made.add(d)
             mode = DEFAULT_FILE_PERMISSION
             if common.go_ext(wp) == ".sh":
                 mode = DEFAULT_EXECUTABLE_PERMISSION
