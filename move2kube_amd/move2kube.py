@@ -2,9 +2,9 @@
 ``collect``, ``create_plan``, ``curate_plan``, ``translate``, ``get_version``."""
 
 import os
-import shutil
 
 from . import collector, customizer, metadata, optimizer, parameterizer, qaengine, transformer
+from .ops import native
 from .models import info, qa
 from .models import plan as plantypes
 from .source import translator as source_translator
@@ -189,10 +189,7 @@ def _emit(p, ir, outpath, qadisablecli):
     if os.path.lexists(outpath):
         qaengine.before_remove(outpath)
         try:
-            if os.path.isdir(outpath) and not os.path.islink(outpath):
-                shutil.rmtree(outpath)
-            else:
-                os.remove(outpath)
+            native.remove_tree(outpath)
         except OSError as e:
             log.error("Failed to remove the existing file/directory at the output path %r Error: %r", outpath, str(e))
             log.error("Anything in the output path will get overwritten.")

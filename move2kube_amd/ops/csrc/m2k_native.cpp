@@ -672,6 +672,83 @@ std::vector<int> write_files(const std::vector<std::string> &paths, const std::v
   return err;
 }
 
+// ---------------------------------------------------------------------------
+// remove_tree: RemoveAll(out) without Python per-entry overhead.  Depth-first
+// with openat/unlinkat relative to directory fds; symlinks are unlinked, never
+// followed.  Returns (errno, path) of the first failure, (0, "") on success.
+// ---------------------------------------------------------------------------
+static int remove_dir_contents(int dfd, const std::string &path, std::string &errpath) {
+  DIR *d = fdopendir(dfd);
+  if (!d) {
+    errpath = path;
+    int e = errno;
+    ::close(dfd);
+    return e;
+  }
+  int err = 0;
+  std::vector<std::pair<std::string, bool>> entries;
+  while (struct dirent *de = readdir(d)) {
+    const char *n = de->d_name;
+    if (n[0] == '.' && (n[1] == 0 || (n[1] == '.' && n[2] == 0))) continue;
+    bool isdir;
+    if (de->d_type == DT_DIR) {
+      isdir = true;
+    } else if (de->d_type == DT_UNKNOWN) {
+      struct stat st;
+      isdir = fstatat(dirfd(d), n, &st, AT_SYMLINK_NOFOLLOW) == 0 && S_ISDIR(st.st_mode);
+    } else {
+      isdir = false;
+    }
+    entries.emplace_back(n, isdir);
+  }
+  for (auto &e : entries) {
+    if (err) break;
+    if (e.second) {
+      int cfd = openat(dirfd(d), e.first.c_str(), O_RDONLY | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
+      if (cfd < 0) {
+        err = errno;
+        errpath = path + "/" + e.first;
+        break;
+      }
+      err = remove_dir_contents(cfd, path + "/" + e.first, errpath);
+      if (!err && unlinkat(dirfd(d), e.first.c_str(), AT_REMOVEDIR) != 0) {
+        err = errno;
+        errpath = path + "/" + e.first;
+      }
+    } else if (unlinkat(dirfd(d), e.first.c_str(), 0) != 0) {
+      err = errno;
+      errpath = path + "/" + e.first;
+    }
+  }
+  closedir(d);  // closes dfd
+  return err;
+}
+
+std::pair<int, std::string> remove_tree(const std::string &path) {
+  std::string errpath;
+  int err = 0;
+  {
+    py::gil_scoped_release nogil;
+    struct stat st;
+    if (lstat(path.c_str(), &st) != 0) {
+      err = errno;
+      errpath = path;
+    } else if (!S_ISDIR(st.st_mode)) {
+      if (unlink(path.c_str()) != 0) err = errno, errpath = path;
+    } else {
+      int fd = open(path.c_str(), O_RDONLY | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
+      if (fd < 0) {
+        err = errno;
+        errpath = path;
+      } else {
+        err = remove_dir_contents(fd, path, errpath);
+        if (!err && rmdir(path.c_str()) != 0) err = errno, errpath = path;
+      }
+    }
+  }
+  return {err, errpath};
+}
+
 // yaml_emit.cpp
 extern "C" PyObject* m2k_yaml_dump(PyObject* data, int sort_maps, PyObject* gomap, PyObject* scalar_fn,
                                    PyObject* style_fn, PyObject* sort_fn);
@@ -695,6 +772,7 @@ PYBIND11_MODULE(_m2k_native, m) {
         py::arg("dcost") = 1, py::arg("scost") = 2, py::arg("nthreads") = 8);
   m.def("pack_strings", &pack_strings, py::arg("items"));
   m.def("closest_batch", &closest_batch, py::arg("as"), py::arg("bs"), py::arg("nthreads") = 8);
+  m.def("remove_tree", &remove_tree, py::arg("path"));
   m.def("write_files", &write_files, py::arg("paths"), py::arg("datas"), py::arg("modes"), py::arg("nthreads") = 8);
   m.def("yaml_dump", &yaml_dump, py::arg("data"), py::arg("sort_maps"), py::arg("gomap"), py::arg("scalar_fn"),
         py::arg("style_fn"), py::arg("sort_fn"));

@@ -65,6 +65,22 @@ def sniff_dockerfiles(paths, nthreads=8):
     return [sniff_first_from(p) for p in paths]
 
 
+def remove_tree(path):
+    """``os.RemoveAll``-like delete of ``path`` (symlinks unlinked, not followed);
+    raises OSError on the first failure."""
+    m = _load()
+    if m is None:
+        import shutil
+        if os.path.isdir(path) and not os.path.islink(path):
+            shutil.rmtree(path)
+        else:
+            os.remove(path)
+        return
+    err, where = m.remove_tree(path)
+    if err:
+        raise OSError(err, os.strerror(err), where)
+
+
 def write_files(items, nthreads=8):
     """Write ``[(path, text_or_bytes, mode)]``; returns ``[OSError or None]`` per
     item.  Native: parallel, GIL released; a repeated path keeps its last content."""

@@ -93,3 +93,24 @@ def test_write_files_batch(tmp_path, monkeypatch):
     errs2 = nat.write_files(items)
     assert [type(e) for e in errs2] == [type(e) for e in errs]
     assert (d / "a.yaml").read_text() == "x: 2\n"
+
+
+def test_remove_tree(tmp_path):
+    from move2kube_amd.ops import native as nat
+    keep = tmp_path / "keep"
+    keep.mkdir()
+    (keep / "precious").write_text("x")
+    root = tmp_path / "out"
+    (root / "a" / "b").mkdir(parents=True)
+    (root / "a" / "b" / "f.yaml").write_text("1")
+    (root / "top.txt").write_text("2")
+    os.symlink(str(keep), str(root / "link-to-dir"))      # unlinked, never followed
+    os.symlink(str(tmp_path / "missing"), str(root / "dangling"))
+    nat.remove_tree(str(root))
+    assert not root.exists() and (keep / "precious").read_text() == "x"
+    f = tmp_path / "file"
+    f.write_text("z")
+    nat.remove_tree(str(f))
+    assert not f.exists()
+    with pytest.raises(OSError):
+        nat.remove_tree(str(tmp_path / "nope"))

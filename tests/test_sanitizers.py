@@ -52,6 +52,10 @@ DRIVER = textwrap.dedent(r'''
     items = [os.path.join(out, "f%03d.yaml" % (i % 150)) for i in range(300)]
     errs = m.write_files(items, [b"k: %d\n" % i for i in range(300)], [0o644] * 300, 8)
     assert not any(errs)
+    os.makedirs(os.path.join(out, "d1", "d2"))
+    os.symlink(work, os.path.join(out, "d1", "up"))
+    err, where = m.remove_tree(out)
+    assert err == 0 and not os.path.exists(out), (err, where)
     res = m.run_commands([["/bin/sh", "-c", "echo %d" % i] for i in range(24)], ["/"] * 24, 8, 30.0)
     assert len(res) == 24
     doc = {"a": [1, {"b": "x: y", "c": "multi\nline\n"}], "n": None, "f": 1.5, "u": "hé",
