@@ -53,7 +53,8 @@ def _use_gpu(pairs, device, queries):
 
 
 def _threads():
-    return max(1, min(16, os.cpu_count() or 1))
+    from ..utils.constants import host_threads
+    return host_threads(16)
 
 
 def matrix(options, queries, device="auto"):

@@ -34,6 +34,22 @@ DEFAULT_SERVICE_PORT = 8080
 DEFAULT_PVC_SIZE = "100Mi"
 
 
+
+def host_threads(cap):
+    """Threads this process should use: the CPUs it may run on (affinity, not
+    the whole machine), shared among the ranks torchrun placed on this node
+    (LOCAL_WORLD_SIZE), capped."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 4
+    try:
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
+    except ValueError:
+        local = 1
+    return max(1, min(cap, n // max(1, local)))
+
+
 class _Settings:
     """Process-wide mutable configuration (the reference's package globals)."""
 
@@ -47,7 +63,7 @@ class _Settings:
         # fixed regardless of this switch.
         self.compat = os.environ.get("M2K_COMPAT", "reference")
         # Number of parallel workers used for detector scripts and file sniffing.
-        self.workers = int(os.environ.get("M2K_WORKERS", "0") or 0) or min(32, (os.cpu_count() or 4))
+        self.workers = int(os.environ.get("M2K_WORKERS", "0") or 0) or host_threads(32)
 
     @property
     def fixed(self):
@@ -55,3 +71,4 @@ class _Settings:
 
 
 settings = _Settings()
+
