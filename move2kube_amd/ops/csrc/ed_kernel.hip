@@ -574,7 +574,8 @@ int grid_x(int nPanels, int tiles) {
   // groups, each walking enough panels to amortise staging its 4 KiB tile table
   // and the per-query reductions (16k tiny groups measured 3x slower for K16).
   // x is a multiple of 8 for the XCD remap.
-  int want = (4096 + tiles - 1) / tiles;
+  static const int target = getenv("M2K_ED_WGS") ? std::max(1, atoi(getenv("M2K_ED_WGS"))) : 4096;
+  int want = (target + tiles - 1) / tiles;
   want = std::max(8, std::min(want, 1024));
   int x = std::min(nPanels, want);
   if (x >= 8) x = (x / 8) * 8;
