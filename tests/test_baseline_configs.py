@@ -144,3 +144,21 @@ def test_config_helm_openshift(tmp_path, monkeypatch):
     assert any(f.endswith("-route.yaml") for f in files)
     assert not any(f.endswith("-ingress.yaml") for f in files)
     _check("helm-openshift", out)
+
+
+@pytest.mark.reference
+def test_reference_samples_tree(tmp_path):
+    """The reference's own ``samples/`` corpus (read-only fixture) end to end:
+    every sample becomes a service with a Deployment and a Service, the compose
+    file's api/redis/web and the two Dockerfiles are found as well."""
+    from conftest import ref_path
+    src = str(tmp_path / "samples")
+    shutil.copytree(ref_path("samples"), src, symlinks=True)
+    out = api.translate(src, str(tmp_path / "out"), name="refsamples")
+    files = set(os.listdir(os.path.join(out, "refsamples")))
+    services = {"api", "redis", "web", "docker-compose", "dockerfile", "golang", "java-gradle", "java-maven",
+                "nodejs", "php", "python", "ruby", "refsamples-docker-compose-api",
+                "refsamples-docker-compose-web", "refsamples-dockerfile"}
+    for s in services:
+        assert "%s-deployment.yaml" % s in files and "%s-service.yaml" % s in files, s
+    assert "refsamples-ingress.yaml" in files
