@@ -31,6 +31,7 @@
 #include <signal.h>
 #include <spawn.h>
 #include <string>
+#include <string_view>
 #include <sys/stat.h>
 #include <sys/time.h>
 #include <sys/types.h>
@@ -325,7 +326,7 @@ uint64_t fnv64a(const py::bytes &b) {
 // ----------------------------------------------------------------------------
 // Wagner-Fischer (smetrics.WagnerFischer semantics, byte-wise)
 // ----------------------------------------------------------------------------
-int wagner_fischer(const std::string &a, const std::string &b, int icost, int dcost, int scost) {
+int wf_distance(std::string_view a, std::string_view b, int icost, int dcost, int scost) {
   std::vector<int> row1(b.size() + 1), row2(b.size() + 1);
   for (size_t i = 1; i <= b.size(); i++) row1[i] = (int)i * icost;
   for (size_t i = 1; i <= a.size(); i++) {
@@ -345,6 +346,35 @@ int wagner_fischer(const std::string &a, const std::string &b, int icost, int dc
   return row1[b.size()];
 }
 
+int wagner_fischer(const std::string &a, const std::string &b, int icost, int dcost, int scost) {
+  return wf_distance(a, b, icost, dcost, scost);
+}
+
+// Borrowed UTF-8 (str) / raw (bytes) buffers of a Python list's items; valid
+// while the list is alive.  Avoids copying every item into a std::string
+// (200k-item lists cost ~20 ms of pybind11 conversion, more than the search).
+std::vector<std::string_view> views_of(const py::list &items) {
+  PyObject *lst = items.ptr();
+  const Py_ssize_t n = PyList_GET_SIZE(lst);
+  std::vector<std::string_view> v((size_t)n);
+  for (Py_ssize_t i = 0; i < n; i++) {
+    PyObject *o = PyList_GET_ITEM(lst, i);
+    Py_ssize_t len = 0;
+    const char *s;
+    if (PyUnicode_Check(o)) {
+      s = PyUnicode_AsUTF8AndSize(o, &len);
+      if (!s) throw py::error_already_set();
+    } else if (PyBytes_Check(o)) {
+      s = PyBytes_AS_STRING(o);
+      len = PyBytes_GET_SIZE(o);
+    } else {
+      throw py::type_error("items must be str or bytes");
+    }
+    v[(size_t)i] = std::string_view(s, (size_t)len);
+  }
+  return v;
+}
+
 // Bit-parallel LCS (Hyyro): with ins=del=1, sub=2 the weighted distance is
 // |a| + |b| - 2*LCS(a, b).  The query b is encoded once as per-byte match masks
 // over ceil(|b|/64) words; each byte of a then costs ~5 word ops per word.
@@ -353,7 +383,7 @@ struct QueryMasks {
   std::vector<uint64_t> m;  // [256][words]
 };
 
-QueryMasks make_masks(const std::string &b) {
+QueryMasks make_masks(std::string_view b) {
   QueryMasks q;
   q.len = (int)b.size();
   q.words = std::max(1, (q.len + 63) / 64);
@@ -362,7 +392,7 @@ QueryMasks make_masks(const std::string &b) {
   return q;
 }
 
-int lcs_distance(const std::string &a, const QueryMasks &q, std::vector<uint64_t> &V) {
+int lcs_distance(std::string_view a, const QueryMasks &q, std::vector<uint64_t> &V) {
   const int W = q.words;
   if (W == 1) {
     uint64_t v = ~0ULL;
@@ -412,9 +442,18 @@ void parallel_for(size_t n, int nthreads, size_t grain, F f) {
   for (auto &th : pool) th.join();
 }
 
+// Threads worth starting for `pairs` LCS evaluations: each thread gets at
+// least ~16k pairs (~0.3 ms), so small batches never pay thread start-up
+// (16 threads for 1.6k pairs cost 0.49 ms vs ~0.04 ms on one thread, MI355X host).
+static int threads_for(size_t pairs, int nthreads) {
+  const size_t t = pairs / 16384;
+  return (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, nthreads), t));
+}
+
 // distance matrix [len(as) x len(bs)] as an int32 numpy array
-py::array_t<int32_t> edit_distance_batch(const std::vector<std::string> &as, const std::vector<std::string> &bs,
-                                         int icost, int dcost, int scost, int nthreads) {
+py::array_t<int32_t> edit_distance_batch(const py::list &as_list, const py::list &bs_list, int icost, int dcost,
+                                         int scost, int nthreads) {
+  const std::vector<std::string_view> as = views_of(as_list), bs = views_of(bs_list);
   const size_t na = as.size(), nb = bs.size();
   py::array_t<int32_t> arr({na, nb});
   int32_t *out = arr.mutable_data();
@@ -424,14 +463,14 @@ py::array_t<int32_t> edit_distance_batch(const std::vector<std::string> &as, con
     if (lcs) {
       std::vector<QueryMasks> qm(nb);
       for (size_t j = 0; j < nb; j++) qm[j] = make_masks(bs[j]);
-      parallel_for(na, nthreads, 64, [&](size_t lo, size_t hi) {
+      parallel_for(na, threads_for(na * nb, nthreads), 1, [&](size_t lo, size_t hi) {
         std::vector<uint64_t> V;
         for (size_t i = lo; i < hi; i++)
           for (size_t j = 0; j < nb; j++) out[i * nb + j] = lcs_distance(as[i], qm[j], V);
       });
     } else {
       parallel_for(na * nb, nthreads, 4096, [&](size_t lo, size_t hi) {
-        for (size_t k = lo; k < hi; k++) out[k] = wagner_fischer(as[k / nb], bs[k % nb], icost, dcost, scost);
+        for (size_t k = lo; k < hi; k++) out[k] = wf_distance(as[k / nb], bs[k % nb], icost, dcost, scost);
       });
     }
   }
@@ -475,26 +514,61 @@ std::tuple<py::bytes, py::array_t<int64_t>, int64_t> pack_strings(const py::list
 }
 
 // For every query: (first index of the minimum distance, that distance); (-1, -1) without options.
-std::pair<py::array_t<int32_t>, py::array_t<int32_t>> closest_batch(const std::vector<std::string> &as,
-                                                                    const std::vector<std::string> &bs, int nthreads) {
+std::pair<py::array_t<int32_t>, py::array_t<int32_t>> closest_batch(const py::list &as_list, const py::list &bs_list,
+                                                                    int nthreads) {
+  const std::vector<std::string_view> as = views_of(as_list), bs = views_of(bs_list);
   const size_t na = as.size(), nb = bs.size();
   py::array_t<int32_t> idx(nb), dist(nb);
   int32_t *pi = idx.mutable_data(), *pd = dist.mutable_data();
   {
     py::gil_scoped_release nogil;
-    parallel_for(nb, nthreads, 2, [&](size_t lo, size_t hi) {
-      std::vector<uint64_t> V;
-      for (size_t j = lo; j < hi; j++) {
-        const QueryMasks q = make_masks(bs[j]);
+    const int nt = threads_for(na * nb, nthreads);
+    std::vector<QueryMasks> qm(nb);
+    for (size_t j = 0; j < nb; j++) qm[j] = make_masks(bs[j]);
+    if (nb >= (size_t)nt * 2 || nt == 1) {
+      // enough queries: split them
+      parallel_for(nb, nt, 1, [&](size_t lo, size_t hi) {
+        std::vector<uint64_t> V;
+        for (size_t j = lo; j < hi; j++) {
+          int bi = -1, bd = -1;
+          for (size_t i = 0; i < na; i++) {
+            const int d = lcs_distance(as[i], qm[j], V);
+            if (bi < 0 || d < bd) bi = (int)i, bd = d;
+          }
+          pi[j] = bi;
+          pd[j] = bd;
+        }
+      });
+    } else {
+      // few queries, many options: split the options, merge per query in range
+      // order so ties still resolve to the first index
+      const size_t chunk = (na + nt - 1) / nt;
+      std::vector<int> pbi((size_t)nt * nb, -1), pbd((size_t)nt * nb, -1);
+      parallel_for((size_t)nt, nt, 1, [&](size_t tlo, size_t thi) {
+        std::vector<uint64_t> V;
+        for (size_t t = tlo; t < thi; t++) {
+          const size_t lo = t * chunk, hi = std::min(na, lo + chunk);
+          for (size_t j = 0; j < nb; j++) {
+            int bi = -1, bd = -1;
+            for (size_t i = lo; i < hi; i++) {
+              const int d = lcs_distance(as[i], qm[j], V);
+              if (bi < 0 || d < bd) bi = (int)i, bd = d;
+            }
+            pbi[t * nb + j] = bi;
+            pbd[t * nb + j] = bd;
+          }
+        }
+      });
+      for (size_t j = 0; j < nb; j++) {
         int bi = -1, bd = -1;
-        for (size_t i = 0; i < na; i++) {
-          const int d = lcs_distance(as[i], q, V);
-          if (bi < 0 || d < bd) bi = (int)i, bd = d;
+        for (int t = 0; t < nt; t++) {
+          const int i = pbi[(size_t)t * nb + j], d = pbd[(size_t)t * nb + j];
+          if (i >= 0 && (bi < 0 || d < bd)) bi = i, bd = d;
         }
         pi[j] = bi;
         pd[j] = bd;
       }
-    });
+    }
   }
   return {idx, dist};
 }

@@ -7,12 +7,30 @@ builder buildpack lists) are offloaded to the MI355X kernel in
 """
 
 import os
+import sys
 
 import numpy as np
 
 from . import gpu, native
 
-GPU_MIN_PAIRS = int(os.environ.get("M2K_GPU_MIN_PAIRS", "65536"))
+# Crossover measured on MI355X (profiles/r01_ed_crossover.log): once the HIP
+# runtime is up, the GPU wins from ~8k pairs (0.09 ms vs 0.09-0.22 ms on 16
+# threads); the first HIP call of a process costs ~280 ms, which the CPU path
+# only exceeds around 10^8 pairs.
+GPU_MIN_PAIRS = int(os.environ.get("M2K_GPU_MIN_PAIRS", "8192"))
+GPU_MIN_PAIRS_COLD = int(os.environ.get("M2K_GPU_MIN_PAIRS_COLD", "100000000"))
+
+
+def _gpu_warm():
+    """True when this process already paid the HIP start-up (our library ran,
+    or torch initialised the device)."""
+    if gpu.warm():
+        return True
+    torch = sys.modules.get("torch")
+    try:
+        return bool(torch is not None and torch.cuda.is_initialized())
+    except Exception:  # noqa: BLE001
+        return False
 
 
 def wagner_fischer_py(a, b, icost=1, dcost=1, scost=2):
@@ -49,7 +67,9 @@ def _use_gpu(pairs, device, queries):
         if not fits:
             raise gpu.GpuUnavailable("queries longer than 64 bytes are not supported on the GPU path")
         return True
-    return fits and pairs >= GPU_MIN_PAIRS and gpu.gpu_host()
+    if not fits or pairs < GPU_MIN_PAIRS or not gpu.gpu_host():
+        return False
+    return pairs >= GPU_MIN_PAIRS_COLD or _gpu_warm()
 
 
 def _threads():

@@ -70,6 +70,14 @@ def available():
     return lib is not None and lib.m2k_gpu_device_count() > 0
 
 
+_warm = False
+
+
+def warm():
+    """A kernel call has completed in this process (HIP runtime initialised)."""
+    return _warm
+
+
 def last_timings():
     """{prep, h2d, kernel, d2h} milliseconds of the last ed_matrix/ed_closest call."""
     lib = _lib_or_raise()
@@ -126,6 +134,8 @@ def ed_matrix(options, queries):
         raise GpuUnsupportedInput("m2k_ed_matrix cannot take this input (code %d)" % rc)
     if rc != 0:
         raise GpuUnavailable("m2k_ed_matrix failed with code %d" % rc)
+    global _warm
+    _warm = True
     return outT.T
 
 
@@ -148,4 +158,6 @@ def ed_closest(options, queries):
         raise GpuUnsupportedInput("m2k_ed_closest cannot take this input (code %d)" % rc)
     if rc != 0:
         raise GpuUnavailable("m2k_ed_closest failed with code %d" % rc)
+    global _warm
+    _warm = True
     return idx, dist

@@ -1,12 +1,15 @@
 """Numerics of the gfx950 batched edit-distance kernels vs the plain CPU
 Wagner-Fischer reference (ins=1, del=1, sub=2)."""
 
+import os
 import random
 
 import numpy as np
 import pytest
 
 from move2kube_amd.ops import editdistance, gpu, native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -69,6 +72,8 @@ def test_ed_closest_many_query_slabs():
 
 
 def test_dispatch_uses_gpu_for_large_batches(monkeypatch):
+    gpu.ed_closest(["warm"], ["up"])  # a warm runtime uses the small-batch threshold
+    assert editdistance._gpu_warm()
     calls = []
     real = gpu.ed_closest
 
@@ -136,3 +141,21 @@ def test_tile_classes_boundaries_and_wide_alphabet():
         gi, gd = gpu.ed_closest(opts, qs)
         ci, cd = native.module().closest_batch(opts, qs, 8)
         assert np.array_equal(gi, ci) and np.array_equal(gd, cd)
+
+
+def test_cold_process_keeps_small_batches_on_cpu():
+    """In a fresh process the first HIP call costs ~280 ms: a batch above the
+    warm threshold but far below the cold one stays on the CPU."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from move2kube_amd.ops import editdistance, gpu\n"
+            "calls = []\n"
+            "real = gpu.ed_closest\n"
+            "gpu.ed_closest = lambda o, q: calls.append(1) or real(o, q)\n"
+            "opts = ['buildpack-%%d' %% i for i in range(4000)]\n"
+            "editdistance.closest_indices(opts, ['node', 'java', 'go'] * 10)\n"
+            "print(len(calls), gpu.warm())\n") % (ROOT,)
+    p = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, timeout=300)
+    assert p.stdout.split() == ["0", "False"]
+
