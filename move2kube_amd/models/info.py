@@ -1,6 +1,5 @@
 """Version information (reference ``types/info/versioninfo.go``)."""
 
-import platform
 import re
 
 from ..utils import log
@@ -58,6 +57,7 @@ class VersionInfo:
 
 
 def get_version_info():
+    import platform  # only `version -l` needs it (CLI start-up time)
     return VersionInfo(get_version(), GIT_COMMIT, GIT_TREE_STATE, "python" + platform.python_version())
 
 

@@ -59,14 +59,16 @@ def engines():
 
 
 def start_engine(qaskip=False, qaport=0, qadisablecli=False):
-    from .cli_engine import CliEngine
-    from .default_engine import DefaultEngine
-    from .rest_engine import HTTPRESTEngine
+    # imported on demand: the REST engine pulls in http.server, which a
+    # --qaskip or terminal run never needs (CLI start-up time)
     if qaskip:
+        from .default_engine import DefaultEngine
         e = DefaultEngine()
     elif not qadisablecli:
+        from .cli_engine import CliEngine
         e = CliEngine()
     else:
+        from .rest_engine import HTTPRESTEngine
         e = HTTPRESTEngine(qaport)
     add_engine(e)
     return e

@@ -50,3 +50,17 @@ def test_two_ranks_gloo():
     assert d["n_gpus"] == 2
     assert d["config"]["parallelism"] == "dp2"
     assert d["scaling"] == "weak"
+
+
+def test_baseline_configs_bench_golang():
+    """benchmarks/baseline_configs.py (BASELINE.md per-configuration wall clock):
+    one warm, one reference-model and one cold CLI run of the golang config, all
+    identical to the expected tree."""
+    p = subprocess.run([sys.executable, os.path.join("benchmarks", "baseline_configs.py"), "--runs", "1",
+                        "--refmodel-runs", "1", "--configs", "golang"], cwd=ROOT, env=_env(),
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    rows = [json.loads(l) for l in p.stdout.decode().splitlines() if l.startswith("{")]
+    cfg = [r for r in rows if r.get("config") == "golang"]
+    assert len(cfg) == 1 and cfg[0]["manifest_diff"] == 0
+    assert cfg[0]["warm_p50_ms"] > 0 and cfg[0]["cold_p50_ms"] > 0 and cfg[0]["refmodel_p50_ms"] > 0
