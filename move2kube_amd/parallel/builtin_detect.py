@@ -29,8 +29,18 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _ASSETS_SRC = os.path.join(os.path.dirname(_HERE), "assets", "m2kassets")
 
 
-def _exists_file(p):
-    return os.path.isfile(p)
+def _exists_file(src, name):
+    """``test -f "$src/name"``, answered from the scope's directory index when
+    it covers ``src`` (the plan/translate scopes always do) - no stat per
+    (detector x directory) pair; symlinks and unknowns still go to the FS."""
+    idx = fsindex.peek_index(src)
+    if idx is not None:
+        k = idx.child_kind(name)
+        if k == fsindex.FILE:
+            return True
+        if k in (fsindex.MISSING, fsindex.DIR, fsindex.OTHER):
+            return False
+    return os.path.isfile(os.path.join(src, name))
 
 
 def _find_any(src, pattern):
@@ -77,7 +87,7 @@ _FAIL = (1, b"")
 
 def _simple(marker, out):
     def fn(src):
-        return _ok(out) if _exists_file(os.path.join(src, marker)) else _FAIL
+        return _ok(out) if _exists_file(src, marker) else _FAIL
     return fn
 
 
@@ -89,10 +99,14 @@ def _recursive(pattern, out):
 
 def _war(port):
     def fn(src):
-        try:
-            wars = sorted(n for n in os.listdir(src) if n.endswith(".war") and not n.startswith("."))
-        except OSError:
-            wars = []
+        idx = fsindex.peek_index(src)
+        if idx is not None and idx.kinds and idx.kinds[0] == fsindex.DIR:
+            wars = idx.children_matching("*.war")
+        else:
+            try:
+                wars = sorted(n for n in os.listdir(src) if n.endswith(".war") and not n.startswith("."))
+            except OSError:
+                wars = []
         # the script's loop exits 1 unless the first (sorted) match exists
         if not wars or not os.path.exists(os.path.join(src, wars[0])):
             return _FAIL
@@ -105,29 +119,29 @@ _PY_MARKERS = ("requirements.txt", "setup.py", "environment.yml", "Pipfile")
 
 def _python_df(src):
     for m in _PY_MARKERS:
-        if _exists_file(os.path.join(src, m)):
+        if _exists_file(src, m):
             return _ok('{"main_script_rel_path": "%s", "app_name": "app", "port": 8080}' % _find_main(src))
     return _FAIL
 
 
 def _python_s2i(src):
     for m in _PY_MARKERS:
-        if _exists_file(os.path.join(src, m)):
+        if _exists_file(src, m):
             return _ok('{"builder": "%s", "app_file": "%s", "app_name": "app", "port": 8080}'
                        % ("registry.access.redhat.com/rhscl/python-36-rhel7:latest", _find_main(src)))
     return _FAIL
 
 
 def _golang_s2i(src):
-    if not _exists_file(os.path.join(src, "go.mod")) and not _find_any(src, "*.go"):
+    if not _exists_file(src, "go.mod") and not _find_any(src, "*.go"):
         return _FAIL
     return _ok('{"builder": "%s", "port": 8080}\n' % "registry.access.redhat.com/ubi8/go-toolset:latest")
 
 
 def _java_s2i(src):
-    if _exists_file(os.path.join(src, "build.gradle")) or _exists_file(os.path.join(src, "build.xml")):
+    if _exists_file(src, "build.gradle") or _exists_file(src, "build.xml"):
         return _FAIL
-    if _exists_file(os.path.join(src, "pom.xml")):
+    if _exists_file(src, "pom.xml"):
         return _ok('{"builder": "%s", "port": 8080}\n' % "registry.access.redhat.com/jboss-eap-6/eap64-openshift:latest")
     if not _find_any(src, "*.java"):
         return _FAIL

@@ -73,19 +73,23 @@ def _run_detect_jobs(jobs):
     if todo:
         spawn, spawn_idx = [], []
         fns = {}
-        for k, (d, script, target) in enumerate(todo):
-            if (d, script) not in fns:
-                fns[(d, script)] = builtin_detect.lookup(d, script)
-            fn = fns[(d, script)]
+        shared = {}  # (code, stdout bytes) -> one read-only DetectResult
+        for k, job in enumerate(todo):
+            d, script, target = job
+            fn = fns.get((d, script), False)
+            if fn is False:
+                fn = fns[(d, script)] = builtin_detect.lookup(d, script)
             if fn is None:
-                spawn.append(todo[k])
+                spawn.append(job)
                 spawn_idx.append(k)
                 continue
-            code, out = fn(target)
-            r = DetectResult(code, out.decode("utf-8", "replace"))
+            key = fn(target)
+            r = shared.get(key)
+            if r is None:
+                r = shared[key] = DetectResult(key[0], key[1].decode("utf-8", "replace"))
             results[todo_idx[k]] = r
             if cache is not None:
-                cache[todo[k]] = r
+                cache[job] = r
         todo = spawn
         todo_idx = [todo_idx[k] for k in spawn_idx]
     if todo:

@@ -17,11 +17,14 @@ afresh so callers never observe stale listings.
 
 import contextlib
 import os
+import re
 import threading
 
 from . import log
 
 FILE, DIR, SYMLINK, OTHER = 0, 1, 2, 3
+MISSING = -1
+_SUFFIX_PATTERN = re.compile(r"^\*\.[A-Za-z0-9_+-]+$")
 
 _local = threading.local()
 
@@ -102,13 +105,27 @@ class FileIndex:
             self._by_ext, self._by_name = by_ext, by_name
         return self._by_ext, self._by_name
 
-    def _select(self, table, keys):
+    def _select(self, which, keys):
+        """Entries listed under ``keys`` in the base index's ext/name map,
+        restricted to this index's range (sub-indexes share the base maps)."""
+        import bisect
+        base = self.base or self
+        table = base._file_maps()[which]
+        lo, hi = self.lo, self.lo + len(self.paths)
+        whole = base is self
         pos = []
         for key in keys:
-            pos.extend(table.get(key, ()))
+            ps = table.get(key)
+            if not ps:
+                continue
+            if whole:
+                pos.extend(ps)
+            else:
+                pos.extend(ps[bisect.bisect_left(ps, lo):bisect.bisect_left(ps, hi)])
         if len(keys) > 1:
             pos.sort()
-        return [self.paths[i] for i in pos]
+        bp = base.paths
+        return [bp[i] for i in pos]
 
     def files(self):
         return [p for p, k in zip(self.paths, self.kinds) if k != DIR]
@@ -118,11 +135,11 @@ class FileIndex:
 
     def files_by_ext(self, exts):
         """Non-directories whose extension (Go ``filepath.Ext``) is in ``exts``, in walk order."""
-        return self._select(self._file_maps()[0], list(dict.fromkeys(exts)))
+        return self._select(0, list(dict.fromkeys(exts)))
 
     def files_by_name(self, names):
         """Non-directories whose base name is in ``names``, in walk order."""
-        return self._select(self._file_maps()[1], list(dict.fromkeys(names)))
+        return self._select(1, list(dict.fromkeys(names)))
 
     # -- subtree ranges -------------------------------------------------------
     def _positions(self):
@@ -147,28 +164,74 @@ class FileIndex:
         return self._end
 
     def sub_index(self, sub_root):
-        """Listing of a sub-directory derived from this index (no new walk)."""
-        i = self._positions().get(sub_root)
-        if i is None:
-            return FileIndex(sub_root, [], [], [], self.base or self, self.lo)
-        j = self._ends()[i]
+        """Listing of a sub-directory derived from this index (no new walk).
+        Positions and subtree ends come from the base index (computed once),
+        so deriving many nested sub-indexes costs one slice each."""
+        base = self.base or self
+        i = base._positions().get(sub_root)
+        if i is None or not self.lo <= i < self.lo + len(self.paths):
+            return FileIndex(sub_root, [], [], [], base, self.lo)
+        j = base._ends()[i]
         prefix = sub_root.rstrip("/") + "/"
         errors = [e for e in self.errors if e[0] == sub_root or e[0].startswith(prefix)]
-        return FileIndex(sub_root, self.paths[i:j], self.kinds[i:j], errors, self.base or self, self.lo + i)
+        return FileIndex(sub_root, base.paths[i:j], base.kinds[i:j], errors, base, i)
+
+    def child_kind(self, name):
+        """Kind of the entry ``<root>/<name>`` as of the walk (``MISSING`` when
+        the root listing had no such name), or None when the index cannot
+        answer: the root is not a directory (a symlinked root is not followed
+        by the walk, but ``test -f root/name`` follows it) or the entry could
+        not be stat'ed.  Lets detectors answer ``test -f`` without a syscall."""
+        if not self.kinds or self.kinds[0] != DIR:
+            return None
+        base = self.base or self
+        p = self.root + "/" + name if self.root != "/" else "/" + name
+        i = base._positions().get(p)
+        if i is not None:
+            return base.kinds[i]
+        if self.errors and any(e[0] == p for e in self.errors):
+            return None
+        return MISSING
+
+    def children_matching(self, pattern):
+        """Sorted names of the root's direct children (any kind) whose name
+        matches the shell ``pattern`` and does not start with a dot - what
+        ``for f in <pattern>`` expands to in that directory."""
+        base = self.base or self
+        prefix = self.root.rstrip("/") + "/"
+        pos = base._pattern_positions(pattern)
+        import bisect
+        lo, hi = self.lo + 1, self.lo + len(self.paths)
+        out = []
+        for k in range(bisect.bisect_left(pos, lo), bisect.bisect_left(pos, hi)):
+            rest = base.paths[pos[k]][len(prefix):]
+            if "/" not in rest and not rest.startswith("."):
+                out.append(rest)
+        return sorted(out)
+
+    def _pattern_positions(self, pattern):
+        """Positions (in this base index) of entries whose basename matches ``pattern``."""
+        if self._match is None:
+            self._match = {}
+        pos = self._match.get(pattern)
+        if pos is None:
+            if _SUFFIX_PATTERN.match(pattern):
+                # "*.go"-style: the basename ends with the suffix iff the path does
+                suffix = pattern[1:]
+                pos = [i for i, p in enumerate(self.paths) if p.endswith(suffix)]
+            else:
+                import fnmatch
+                rx = re.compile(fnmatch.translate(pattern))
+                pos = [i for i, p in enumerate(self.paths) if rx.match(p.rsplit("/", 1)[-1])]
+            self._match[pattern] = pos
+        return pos
 
     def has_match(self, pattern, include_root=False):
         """True if some entry of this index (other than its root unless asked)
         has a basename matching the shell ``pattern`` (``find -name``)."""
         import bisect
-        import fnmatch
         base = self.base or self
-        if base._match is None:
-            base._match = {}
-        pos = base._match.get(pattern)
-        if pos is None:
-            rx = __import__("re").compile(fnmatch.translate(pattern))
-            pos = [i for i, p in enumerate(base.paths) if rx.match(p.rsplit("/", 1)[-1])]
-            base._match[pattern] = pos
+        pos = base._pattern_positions(pattern)
         lo = self.lo if include_root else self.lo + 1
         hi = self.lo + len(self.paths)
         k = bisect.bisect_left(pos, lo)
@@ -206,7 +269,7 @@ def _walk_py(root):
                     rec(p)
                 else:
                     paths.append(p)
-                    kinds.append(FILE)
+                    kinds.append(FILE if e.is_file(follow_symlinks=False) else OTHER)
             except OSError as ex:
                 errors.append((p, str(ex)))
     rec(root)
@@ -228,7 +291,41 @@ def walk(root):
     return FileIndex(root, paths, kinds, errors)
 
 
+def peek_index(root):
+    """The index of ``root`` if the enclosing scope already has it or one of
+    its ancestors (derived without a walk); None otherwise.  Never walks."""
+    cache = _cache()
+    if cache is None:
+        return None
+    idx = cache.get(root)
+    if idx is not None:
+        return idx
+    root = root.rstrip("/") or "/"
+    idx = cache.get(root)
+    if idx is not None:
+        return idx
+    anc = root
+    while True:
+        parent_dir = os.path.dirname(anc)
+        if parent_dir == anc:
+            return None
+        anc = parent_dir
+        parent = cache.get(anc)
+        if parent is not None:
+            if (parent.base or parent)._positions().get(root) is None:
+                return None
+            idx = parent.sub_index(root)
+            cache[root] = idx
+            return idx
+
+
 def get_index(root):
+    cache = _cache()
+    if cache is not None:
+        # a cached root existed when it was walked: skip the stat checks
+        idx = cache.get(root.rstrip("/") or "/")
+        if idx is not None:
+            return idx
     if not os.path.exists(root):
         log.warning("Error in walking through files due to : %r", "lstat %s: no such file or directory" % root)
         raise FileNotFoundError(root)

@@ -56,6 +56,38 @@ def test_builtin_matches_scripts(tmp_path, assets_dir, monkeypatch):
     assert mism == []
 
 
+def test_builtin_matches_scripts_index_backed(tmp_path, assets_dir, monkeypatch):
+    """Inside an fsindex scope the detectors answer ``test -f`` and the
+    ``*.war`` glob from the directory index; edge cases must still agree with
+    the scripts: markers that are directories, symlinks (to files, to
+    directories, dangling), FIFOs, a symlinked source root, ``.war`` dirs."""
+    from move2kube_amd.utils import fsindex
+    base = str(tmp_path / "src")
+    targets = _make_tree(base)
+    extra = os.path.join(base, "edge")
+    os.makedirs(os.path.join(extra, "package.json"))           # marker is a directory
+    os.makedirs(os.path.join(extra, "z.war"))                  # .war directory
+    with open(os.path.join(base, "real_gemfile"), "w") as f:
+        f.write("")
+    os.symlink(os.path.join(base, "real_gemfile"), os.path.join(extra, "Gemfile"))  # symlink to a file
+    os.symlink(os.path.join(extra, "nowhere"), os.path.join(extra, "pom.xml"))     # dangling symlink
+    os.symlink(os.path.join(base, "empty"), os.path.join(extra, "build.xml"))      # symlink to a dir
+    os.mkfifo(os.path.join(extra, "Pipfile"))                                       # not a regular file
+    os.symlink(os.path.join(base, "node"), os.path.join(base, "linkroot"))         # symlinked root
+    targets += [extra, os.path.join(base, "linkroot")]
+    jobs = [(os.path.join(assets_dir, rel), script, t)
+            for rel, script in sorted(builtin_detect.DETECTORS) for t in targets]
+    with fsindex.scope():
+        fsindex.get_index(base)
+        assert fsindex.peek_index(extra) is not None
+        native_res = detect_pool.run_detect_jobs(jobs)
+    monkeypatch.setenv("M2K_NATIVE_DETECT", "0")
+    script_res = detect_pool.run_detect_jobs(jobs)
+    mism = [(j, a.code, a.stdout, b.code, b.stdout) for j, a, b in zip(jobs, native_res, script_res)
+            if (a.code == 0) != (b.code == 0) or (a.code == 0 and a.stdout != b.stdout)]
+    assert mism == []
+
+
 def test_modified_detector_is_not_shortcut(tmp_path, assets_dir):
     d = os.path.join(assets_dir, "dockerfiles", "nodejs")
     script = os.path.join(d, "m2kdfdetect.sh")
