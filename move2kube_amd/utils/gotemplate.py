@@ -99,6 +99,30 @@ def _truth(v):
     return True
 
 
+def go_type_name(v):
+    """Go's %T of a value decoded from YAML/JSON or produced by a template."""
+    if v is None:
+        return "<nil>"
+    if isinstance(v, bool):
+        return "bool"
+    if isinstance(v, int):
+        return "int"
+    if isinstance(v, float):
+        return "float64"
+    if isinstance(v, str):
+        return "string"
+    if isinstance(v, dict):
+        return "map[string]interface {}"
+    if isinstance(v, (list, tuple)):
+        return "[]interface {}"
+    return type(v).__name__
+
+
+def _bad_verb(verb, a):
+    """fmt's rendering of an operand the verb does not apply to: %!d(string=x)."""
+    return "%!" + verb + "(" + go_type_name(a) + "=" + go_sprint(a) + ")"
+
+
 def go_sprintf(fmt, args):
     out = []
     i = 0
@@ -141,33 +165,51 @@ def go_sprintf(fmt, args):
             continue
         a = args[ai]
         ai += 1
-        if verb in "vs":
+        if a is None and verb not in "vT":
+            # fmt prints a nil operand as %!verb(<nil>) for every verb but %v/%T
+            s = "%!" + verb + "(<nil>)"
+        elif verb == "v":
             s = go_sprint(a)
-            if prec:
-                s = s[:int(prec)]
+        elif verb == "s":
+            if isinstance(a, (bool, int, float)):
+                s = _bad_verb(verb, a)
+            else:
+                s = go_sprint(a)
+                if prec:
+                    s = s[:int(prec)]
         elif verb == "q":
-            s = json.dumps(go_sprint(a)) if not isinstance(a, int) else "'%s'" % chr(a)
+            if isinstance(a, bool) or isinstance(a, float):
+                s = _bad_verb(verb, a)
+            elif isinstance(a, int):
+                s = "'%s'" % chr(a)
+            else:
+                s = json.dumps(go_sprint(a))
         elif verb == "d":
-            s = str(int(a)) if isinstance(a, (int, float)) else "%!d(" + go_sprint(a) + ")"
+            s = str(a) if isinstance(a, int) and not isinstance(a, bool) else _bad_verb(verb, a)
         elif verb in "xX":
-            if isinstance(a, int):
+            if isinstance(a, bool):
+                s = _bad_verb(verb, a)
+            elif isinstance(a, int):
                 s = format(a, verb)
             else:
                 s = go_sprint(a).encode().hex()
                 if verb == "X":
                     s = s.upper()
         elif verb in "feEgG":
-            p = int(prec) if prec else 6
-            if verb == "g":
-                s = go_format_float(float(a)) if prec is None else ("%." + str(p) + "g") % a
+            if not isinstance(a, (int, float)) or isinstance(a, bool):
+                s = _bad_verb(verb, a)
             else:
-                s = ("%." + str(p) + verb) % a
+                p = int(prec) if prec else 6
+                if verb == "g":
+                    s = go_format_float(float(a)) if prec is None else ("%." + str(p) + "g") % a
+                else:
+                    s = ("%." + str(p) + verb) % a
         elif verb == "t":
-            s = go_sprint(bool(a))
+            s = go_sprint(a) if isinstance(a, bool) else _bad_verb(verb, a)
         elif verb == "T":
-            s = type(a).__name__
+            s = go_type_name(a)
         else:
-            s = go_sprint(a)
+            s = _bad_verb(verb, a)
         if width:
             w = int(width)
             if "-" in flags:

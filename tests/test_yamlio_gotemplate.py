@@ -91,3 +91,40 @@ def test_parse_cache_returns_private_copies_and_reraises():
             else:
                 raise AssertionError("expected a YAML error")
     assert y._memo is None
+
+
+GO_TEMPLATE_CASES = [
+    # (template, data, output of Go's text/template + fmt)
+    ("{{- /* c */ -}} a", {}, "a"),
+    ("{{range $i, $e := .L}}{{$i}}={{$e}};{{end}}", {"L": ["x", "y"]}, "0=x;1=y;"),
+    ("{{range .L}}{{.}}{{else}}empty{{end}}", {"L": []}, "empty"),
+    ("{{with .A}}{{.}}{{else}}none{{end}}", {"A": ""}, "none"),
+    ("{{or .A .B}}|{{and .A .B}}", {"A": 0, "B": "z"}, "z|0"),
+    ('{{printf "%q" .S}}', {"S": 'a"b'}, '"a\\"b"'),
+    ('{{printf "%5d|%-4s|%x" 42 "ab" 255}}', {}, "   42|ab  |ff"),
+    ("{{eq .A 1 2 3}}", {"A": 3}, "true"),
+    ('{{.A | printf "%s-%s" "x"}}', {"A": "y"}, "x-y"),
+    ('{{define "t"}}[{{.}}]{{end}}{{template "t" .A}}', {"A": "q"}, "[q]"),
+    ("a  {{- 1 -}}  b", {}, "a1b"),
+    # fmt.Sprint: a space only between operands when neither is a string
+    ('{{print 1 2 "a" 3 "b" "c"}}', {}, "1 2a3bc"),
+    ('{{println 1 "a"}}', {}, "1 a\n"),
+    ('{{html "<a&b>"}}|{{urlquery "a b&c"}}|{{js "a\'b"}}', {}, "&lt;a&amp;b&gt;|a+b%26c|a\\'b"),
+    ("{{.M}}|{{.L}}", {"M": {"b": 1, "a": 2}, "L": [1, "x", True]}, "map[a:2 b:1]|[1 x true]"),
+    ("{{$x := 1}}{{if true}}{{$x = 2}}{{end}}{{$x}}", {}, "2"),
+    ('{{slice "abcdef" 1 3}}|{{.Missing}}', {}, "bc|<no value>"),
+    ("{{ 3.5 }} {{ 1e3 }} {{ 0x10 }} {{ 'a' }}", {}, "3.5 1000 16 97"),
+    # fmt's bad-verb and nil renderings
+    ('{{printf "%d|%d|%d" true 1.5 "x"}}', {}, "%!d(bool=true)|%!d(float64=1.5)|%!d(string=x)"),
+    ('{{printf "%s|%s|%t|%t" 5 true 1 false}}', {}, "%!s(int=5)|%!s(bool=true)|%!t(int=1)|false"),
+    ('{{printf "%T %T %T %T" 1 "a" .M .L}}', {"M": {}, "L": []}, "int string map[string]interface {} []interface {}"),
+    ('{{printf "%v|%d|%s" nil nil nil}}', {}, "<nil>|%!d(<nil>)|%!s(<nil>)"),
+    ('{{printf "%05d|%-3d|%3s" 42 7 "ab"}}', {}, "00042|7  | ab"),
+    ('{{printf "%.2f|%e|%g" 3.14159 1234.5 0.000001}}', {}, "3.14|1.234500e+03|1e-06"),
+]
+
+
+@pytest.mark.parametrize("src,data,want", GO_TEMPLATE_CASES)
+def test_go_template_semantics(src, data, want):
+    from move2kube_amd.utils.gotemplate import Template
+    assert Template(src).execute(data) == want
