@@ -43,7 +43,7 @@ def parse_v2(path):
     """Parse a v1/v2 compose file -> {"version", "project", "services": [...], "networks": {...}}."""
     try:
         text = common.read_text(path)
-        parsed = yamlio.load(text)
+        parsed = yamlio.load_v2(text)
     except (OSError, yamlio.YAMLError) as e:
         raise ComposeError("Failed to load docker compose file at path %s Error: %s" % (path, e))
     if parsed is None:

@@ -154,7 +154,7 @@ def parse_v3(path):
     """Parse and load a v3 compose file -> normalized config dict."""
     try:
         text = common.read_text(path)
-        parsed = yamlio.load(text)
+        parsed = yamlio.load_v2(text)
     except (OSError, yamlio.YAMLError) as e:
         raise ComposeError("Unable to load Compose file at path %s Error: %s" % (path, e))
     if not isinstance(parsed, dict):

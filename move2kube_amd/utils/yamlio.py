@@ -592,13 +592,88 @@ def _make_loader(name, keep_resolvers):
     return cls
 
 
-# YAML 1.2-ish core schema as go-yaml v3 resolves it: no yes/no/on/off bools,
-# no timestamps (kept as strings for interface{} targets).
-_TypedLoader = _make_loader("_TypedLoader", {
-    "tag:yaml.org,2002:null", "tag:yaml.org,2002:int", "tag:yaml.org,2002:float",
-    "tag:yaml.org,2002:merge"})
-_TypedLoader.add_implicit_resolver(
-    "tag:yaml.org,2002:bool", re.compile(r"^(?:true|True|TRUE|false|False|FALSE)$"), list("tTfF"))
+_INT64_MIN, _INT64_MAX, _UINT64_MAX = -(1 << 63), (1 << 63) - 1, (1 << 64) - 1
+_DOT_FLOAT = re.compile(r"^\.[0-9][0-9_]*(?:[eE][-+]?[0-9]+)?$")
+
+
+def _go_int_value(t):
+    """Value of a string accepted by :func:`_go_parse_int` (base-0 Go syntax)."""
+    neg = t[:1] == "-"
+    if t[:1] in "+-":
+        t = t[1:]
+    low = t[:2].lower()
+    if low == "0x":
+        v = int(t[2:], 16)
+    elif low == "0o":
+        v = int(t[2:], 8)
+    elif low == "0b":
+        v = int(t[2:], 2)
+    elif len(t) > 1 and t[0] == "0":
+        v = int(t[1:], 8)
+    else:
+        v = int(t)
+    return -v if neg else v
+
+
+def go_resolve_number(s):
+    """go-yaml (v2 and v3) ``resolve()`` of a plain scalar whose first byte is
+    a sign, a digit or a dot: an int (``strconv.ParseInt(plain, 0, 64)``, then
+    ``ParseUint``, with every ``_`` removed), a float (``yamlStyleFloat``) or
+    the scalar itself as a string.  Unlike PyYAML's YAML 1.1 resolvers there
+    are no base-60 numbers (``22:22`` stays a string) and ``1e3``/``0o17``
+    are numbers."""
+    if s in _SPECIAL_FLOATS:
+        low = s.lower()
+        return float("nan") if "nan" in low else float("-inf" if low[0] == "-" else "inf")
+    if s[0] == ".":
+        if _DOT_FLOAT.match(s):
+            return float(s)
+        return s
+    plain = s.replace("_", "")
+    if _go_parse_int(plain):
+        v = _go_int_value(plain)
+        if _INT64_MIN <= v <= _INT64_MAX or (0 <= v <= _UINT64_MAX and plain[:1] not in "+-"):
+            return v
+    if _YAML_FLOAT.match(plain):
+        v = float(plain)
+        if not math.isinf(v):
+            return v
+    return s
+
+
+def _construct_go_number(loader, node):
+    return go_resolve_number(node.value)
+
+
+_GONUM_TAG = "tag:move2kube:go-number"
+_GONUM_FIRST = re.compile(r"^[-+0-9.]")
+
+
+def _add_go_scalars(cls, bools):
+    cls.add_implicit_resolver("tag:yaml.org,2002:bool", re.compile("^(?:" + "|".join(bools) + ")$"),
+                              sorted({b[0] for b in bools}))
+    cls.add_implicit_resolver(_GONUM_TAG, _GONUM_FIRST, list("-+0123456789."))
+    cls.add_constructor(_GONUM_TAG, _construct_go_number)
+
+
+# go-yaml v3 into interface{}: bools are only true/false, no timestamps (kept
+# as strings for interface{} targets), go-yaml's int/float rules.
+_TypedLoader = _make_loader("_TypedLoader", {"tag:yaml.org,2002:null", "tag:yaml.org,2002:merge"})
+_add_go_scalars(_TypedLoader, ["true", "True", "TRUE", "false", "False", "FALSE"])
+
+# go-yaml v2 (what docker/cli's compose v3 loader and libcompose parse compose
+# files with): v3's rules plus the YAML 1.1 y/yes/on and n/no/off bools.
+_V2Loader = _make_loader("_V2Loader", {"tag:yaml.org,2002:null", "tag:yaml.org,2002:merge"})
+_add_go_scalars(_V2Loader, ["y", "Y", "yes", "Yes", "YES", "true", "True", "TRUE", "on", "On", "ON",
+                            "n", "N", "no", "No", "NO", "false", "False", "FALSE", "off", "Off", "OFF"])
+_TRUE_WORDS = {"y", "Y", "yes", "Yes", "YES", "true", "True", "TRUE", "on", "On", "ON"}
+
+
+def _construct_v2_bool(loader, node):
+    return node.value in _TRUE_WORDS
+
+
+_V2Loader.add_constructor("tag:yaml.org,2002:bool", _construct_v2_bool)
 
 # Every scalar is kept as its source text (what go-yaml does when decoding a
 # scalar into a Go string field); only nulls resolve.
@@ -687,6 +762,11 @@ def load(text):
 
 def load_all(text):
     return _memoized("typed*", text, lambda t: list(yaml.load_all(t, Loader=_TypedLoader)))
+
+
+def load_v2(text):
+    """Decode like go-yaml v2 into ``interface{}`` (compose files)."""
+    return _memoized("typed-v2", text, lambda t: yaml.load(t, Loader=_V2Loader))
 
 
 def load_raw(text):

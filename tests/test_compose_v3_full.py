@@ -96,3 +96,18 @@ def test_fixed_mode_daemonset(tmp_path, monkeypatch):
                                         (1500, "1500"), (0, "0")])
 def test_decimal_exponent_quantities(value, want):
     assert cutils.format_quantity_decimal_exponent(value) == want
+
+
+def test_compose_files_decode_with_go_yaml_v2_rules(tmp_path, monkeypatch):
+    """docker/cli and libcompose parse compose files with go-yaml v2: ``yes``/``no``
+    are bools, ``1e3`` is a float, ``22:22`` a string; environment mapping values
+    are then rendered with fmt.Sprint."""
+    from move2kube_amd.source.compose import v3
+    p = tmp_path / "docker-compose.yaml"
+    p.write_text("version: '3'\nservices:\n  s:\n    image: busybox\n    tty: yes\n    stdin_open: no\n"
+                 "    environment:\n      A: yes\n      B: 1e3\n      C: 0777\n      D: 22:22\n      E: 1.5\n")
+    parsed = yamlio.load_v2(p.read_text())
+    svc = parsed["services"]["s"]
+    assert svc["tty"] is True and svc["stdin_open"] is False
+    env = v3._mapping_with_equals(svc["environment"])
+    assert env == {"A": "true", "B": "1000", "C": "511", "D": "22:22", "E": "1.5"}

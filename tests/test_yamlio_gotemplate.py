@@ -128,3 +128,45 @@ GO_TEMPLATE_CASES = [
 def test_go_template_semantics(src, data, want):
     from move2kube_amd.utils.gotemplate import Template
     assert Template(src).execute(data) == want
+
+
+# plain scalar -> (go-yaml v3 value, go-yaml v2 value) decoding into interface{}
+GO_YAML_SCALARS = [
+    ("22:22", "22:22", "22:22"),        # no YAML 1.1 base-60 ints in go-yaml
+    ("190:20:30", "190:20:30", "190:20:30"),
+    ("1:30.5", "1:30.5", "1:30.5"),
+    ("1e3", 1000.0, 1000.0),            # yamlStyleFloat: exponent without a dot
+    ("0o17", 15, 15),
+    ("0777", 511, 511),                 # ParseInt base 0: leading 0 is octal
+    ("09", 9.0, 9.0),                   # not octal -> yamlStyleFloat
+    ("1__0", 10, 10),                   # every '_' removed first
+    ("0x_1F", 31, 31),
+    ("_1", "_1", "_1"),
+    ("+12", 12, 12),
+    (".5", 0.5, 0.5),
+    ("1.", 1.0, 1.0),
+    ("1e400", "1e400", "1e400"),        # ParseFloat range error -> string
+    ("18446744073709551615", 18446744073709551615, 18446744073709551615),   # uint64
+    ("2001-12-14", "2001-12-14", "2001-12-14"),   # timestamps stay strings
+    ("yes", "yes", True),
+    ("Off", "Off", False),
+    ("y", "y", True),
+    ("TRUE", True, True),
+    ("1.2.3", "1.2.3", "1.2.3"),
+]
+
+
+@pytest.mark.parametrize("text,v3,v2", GO_YAML_SCALARS)
+def test_go_yaml_scalar_resolution(text, v3, v2):
+    assert yamlio.load("a: " + text)["a"] == v3
+    assert yamlio.load_v2("a: " + text)["a"] == v2
+    # the emitter agrees with the v3 decoder about which strings need quotes
+    if isinstance(v3, str):
+        assert yamlio.load(yamlio.dump({"a": text}))["a"] == text
+
+
+def test_go_yaml_special_floats():
+    import math
+    assert math.isnan(yamlio.load("a: .NaN")["a"])
+    assert yamlio.load("a: -.inf")["a"] == float("-inf")
+    assert yamlio.load("a: +.Inf")["a"] == float("inf")
