@@ -453,22 +453,46 @@ def _marshal_struct(d, typ):
     return _marshal_fields(d, typ)
 
 
-def _marshal_fields(d, typ):
-    out = {}
-    get = d.get
-    for jname, ftype, omit, absent, value, empty in _plan(typ):
-        if jname == "inline":
-            out.update(_marshal_struct(d, ftype))
-            continue
-        v = get(jname)
-        if v is None:
-            if absent is _SKIP:
+_keyed = {}
+
+
+def _keyed_plan(typ):
+    """(json name -> (omitempty, value fn, empty fn), inline struct types,
+    {json name: value} of the fields an absent key still produces)."""
+    kp = _keyed.get(typ)
+    if kp is None:
+        fields, inlines, base = {}, [], {}
+        for jname, ftype, omit, absent, value, empty in _plan(typ):
+            if jname == "inline":
+                inlines.append(ftype)
                 continue
-            out[jname] = _empty_struct(ftype) if absent is _EMPTY_STRUCT else absent
+            fields[jname] = (omit, value, empty)
+            if absent is not _SKIP:
+                base[jname] = _empty_struct(ftype) if absent is _EMPTY_STRUCT else absent
+        kp = _keyed[typ] = (fields, tuple(inlines), base)
+    return kp
+
+
+def _marshal_fields(d, typ):
+    # Driven by the keys present in ``d`` rather than by every field of the
+    # struct (a PodSpec has ~40, a typical one sets 3): fields an absent key
+    # still produces start from a per-type template.  Key order differs from
+    # Go's struct order, which is fine: the only consumer (dumps_k8s) emits
+    # every mapping sorted, as go-yaml does for the reference's Go maps.
+    fields, inlines, base = _keyed_plan(typ)
+    out = dict(base)
+    for ftype in inlines:
+        out.update(_marshal_struct(d, ftype))
+    get = fields.get
+    for k, v in d.items():
+        f = get(k)
+        if f is None or v is None:
             continue
+        omit, value, empty = f
         if omit and empty(v):
+            out.pop(k, None)
             continue
-        out[jname] = value(v)
+        out[k] = value(v)
     return out
 
 

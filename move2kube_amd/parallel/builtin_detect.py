@@ -199,6 +199,19 @@ def lookup(script_dir, script):
     """The in-process implementation for this detector, or None."""
     if not enabled():
         return None
+    # within one plan/translate scope the assets directory does not change:
+    # resolve and hash-check each detector once per scope
+    memo = fsindex.scoped_cache("builtin-detect")
+    if memo is not None:
+        key = (script_dir, script, settings.assets_path)
+        fn = memo.get(key, False)
+        if fn is False:
+            fn = memo[key] = _lookup(script_dir, script)
+        return fn
+    return _lookup(script_dir, script)
+
+
+def _lookup(script_dir, script):
     assets = os.path.abspath(settings.assets_path)
     d = os.path.abspath(script_dir)
     if not d.startswith(assets + os.sep):
