@@ -764,8 +764,15 @@ def load_all(text):
     return _memoized("typed*", text, lambda t: list(yaml.load_all(t, Loader=_TypedLoader)))
 
 
+_V2_ONLY_WORDS = re.compile(r"\b(?:[yYnN]|yes|Yes|YES|no|No|NO|on|On|ON|off|Off|OFF)\b")
+
+
 def load_v2(text):
-    """Decode like go-yaml v2 into ``interface{}`` (compose files)."""
+    """Decode like go-yaml v2 into ``interface{}`` (compose files).  The two
+    decoders differ only in the YAML 1.1 bool words, so a document that does
+    not contain one anywhere shares the v3 parse (and its memo entry)."""
+    if isinstance(text, str) and not _V2_ONLY_WORDS.search(text):
+        return load(text)
     return _memoized("typed-v2", text, lambda t: yaml.load(t, Loader=_V2Loader))
 
 
