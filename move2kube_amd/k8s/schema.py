@@ -270,6 +270,107 @@ def type_for(obj):
     return KIND_TYPES.get(kind)
 
 
+# -- typed-decode checks -------------------------------------------------------
+# The reference decodes manifests with client-go's UniversalDeserializer:
+# sigs.k8s.io/yaml turns the YAML into JSON (go-yaml v2 scalars) and
+# encoding/json fills the typed struct, failing the whole object on a type
+# mismatch (a quoted ``containerPort: "80"``, ``replicas: 1.5``, a label
+# ``version: 1``).  :func:`check` reports the first such mismatch the same way,
+# so these objects are skipped with a message instead of flowing on with
+# values no Go field could hold.  Unknown fields are ignored (non-strict
+# decoding); ``any``/``RawExtension``/untyped maps are not looked into.
+
+_STRING_MAPS = {("ObjectMeta", "labels"), ("ObjectMeta", "annotations"), ("PodSpec", "nodeSelector"),
+                ("LabelSelector", "matchLabels")}
+
+
+def _json_kind(v):
+    if isinstance(v, bool):
+        return "bool"
+    if isinstance(v, (int, float)):
+        return "number"
+    if isinstance(v, str):
+        return "string"
+    if isinstance(v, list):
+        return "array"
+    if isinstance(v, dict):
+        return "object"
+    return "value"
+
+
+def _mismatch(v, typ, path):
+    raise ValueError("json: cannot unmarshal %s into Go struct field %s of type %s" % (_json_kind(v), path, typ))
+
+
+def _check_value(v, typ, path):
+    if v is None:
+        return
+    if typ.startswith("*"):
+        return _check_value(v, typ[1:], path)
+    if typ.startswith("[]"):
+        if not isinstance(v, list):
+            _mismatch(v, typ, path)
+        for x in v:
+            _check_value(x, typ[2:], path)
+        return
+    if typ == "map" or typ.startswith("map:"):
+        if not isinstance(v, dict):
+            _mismatch(v, typ, path)
+        if typ.startswith("map:"):
+            for x in v.values():
+                _check_value(x, typ[4:], path)
+        return
+    if typ in ("string", "Time", "bytes"):
+        if not isinstance(v, str):
+            _mismatch(v, typ, path)
+    elif typ == "int":
+        if isinstance(v, bool) or not isinstance(v, (int, float)) or (isinstance(v, float) and not v.is_integer()):
+            _mismatch(v, typ, path)
+    elif typ == "bool":
+        if not isinstance(v, bool):
+            _mismatch(v, typ, path)
+    elif typ == "IntOrString":
+        if isinstance(v, bool) or not isinstance(v, (int, float, str)) or (isinstance(v, float) and not v.is_integer()):
+            _mismatch(v, typ, path)
+    elif typ == "Quantity":
+        if isinstance(v, bool) or not isinstance(v, (int, float, str)):
+            _mismatch(v, typ, path)
+    elif typ in _STRUCTS:
+        _check_struct(v, typ, path)
+
+
+def _check_struct(d, typ, path):
+    if not isinstance(d, dict):
+        _mismatch(d, typ, path)
+    for jname, ftype, _omit in _STRUCTS[typ]:
+        if jname == "inline":
+            _check_struct(d, ftype, path)
+            continue
+        v = d.get(jname)
+        if v is None:
+            continue
+        fpath = "%s.%s" % (path, jname) if path else jname
+        if (typ, jname) in _STRING_MAPS:
+            if not isinstance(v, dict):
+                _mismatch(v, "map[string]string", typ + "." + fpath)
+            for x in v.values():
+                if x is not None and not isinstance(x, str):
+                    _mismatch(x, "string", typ + "." + fpath)
+            continue
+        _check_value(v, ftype, fpath)
+
+
+def check(obj):
+    """Raise ValueError if ``obj`` could not be decoded into its Go type."""
+    typ = type_for(obj)
+    if typ is None:
+        md = obj.get("metadata")
+        if md is not None:
+            _check_struct(md, "ObjectMeta", "metadata")
+        return
+    _check_struct(obj, typ, "")
+
+
 def _is_empty(v, typ):
     if v is None:
         return True

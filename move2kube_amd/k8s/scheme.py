@@ -8,6 +8,7 @@ below list the group/versions and kinds of those API packages (k8s 1.19,
 OpenShift 4.6, Tekton pipelines 0.18 / triggers 0.10, Knative serving 0.19).
 """
 
+from . import schema
 from ..utils import yamlio
 
 _CORE_V1 = ("Binding ComponentStatus ConfigMap Endpoints Event LimitRange Namespace Node PersistentVolume "
@@ -128,7 +129,8 @@ def decode(data, scheme="k8s"):
     Raises DecodeError when the document has no registered apiVersion/kind."""
     try:
         text = data.decode("utf-8", "surrogateescape") if isinstance(data, bytes) else data
-        docs = yamlio.load_all(text)
+        # sigs.k8s.io/yaml converts YAML to JSON with go-yaml v2 scalars
+        docs = yamlio.load_all_v2(text)
     except (yamlio.YAMLError, ValueError) as e:
         raise DecodeError("yaml: %s" % e)
     obj = docs[0] if docs else None
@@ -145,6 +147,10 @@ def decode(data, scheme="k8s"):
     md = obj.get("metadata")
     if md is not None and not isinstance(md, dict):
         raise DecodeError("metadata must be an object")
+    try:
+        schema.check(obj)
+    except ValueError as e:
+        raise DecodeError(str(e))
     return obj
 
 

@@ -150,6 +150,32 @@ def _validate(d):
     return services
 
 
+def _go_repr(k):
+    """Go ``%#v`` of a YAML key go-yaml v2 decoded into interface{}."""
+    if k is None:
+        return "<nil>"
+    if isinstance(k, bool):
+        return "true" if k else "false"
+    if isinstance(k, float):
+        return yamlio.go_format_float(k)
+    return str(k)
+
+
+def _check_string_keys(v, prefix):
+    """docker/cli ``ParseYAML``: every mapping key in the document must be a
+    string (go-yaml v2 turns ``y:``, ``on:``, ``1:`` keys into bools/ints),
+    otherwise the whole file fails to load (``convertToStringKeysRecursive``)."""
+    if isinstance(v, dict):
+        for k, x in v.items():
+            if not isinstance(k, str):
+                where = "at top level" if not prefix else "in " + prefix
+                raise ComposeError("Non-string key %s: %s" % (where, _go_repr(k)))
+            _check_string_keys(x, k if not prefix else prefix + "." + k)
+    elif isinstance(v, list):
+        for i, x in enumerate(v):
+            _check_string_keys(x, "%s[%d]" % (prefix, i))
+
+
 def parse_v3(path):
     """Parse and load a v3 compose file -> normalized config dict."""
     try:
@@ -159,6 +185,7 @@ def parse_v3(path):
         raise ComposeError("Unable to load Compose file at path %s Error: %s" % (path, e))
     if not isinstance(parsed, dict):
         raise ComposeError("Top-level object must be a mapping")
+    _check_string_keys(parsed, "")
     parsed = remove_non_existent_env_files(path, parsed)
     version = _version(parsed)
     if version not in SUPPORTED_V3:

@@ -776,6 +776,12 @@ def load_v2(text):
     return _memoized("typed-v2", text, lambda t: yaml.load(t, Loader=_V2Loader))
 
 
+def load_all_v2(text):
+    if isinstance(text, str) and not _V2_ONLY_WORDS.search(text):
+        return load_all(text)
+    return _memoized("typed-v2*", text, lambda t: list(yaml.load_all(t, Loader=_V2Loader)))
+
+
 def load_raw(text):
     """Decode keeping scalars as raw strings (for typed struct decoding)."""
     return _memoized("raw", text, lambda t: yaml.load(t, Loader=_RawLoader))

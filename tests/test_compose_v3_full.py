@@ -111,3 +111,15 @@ def test_compose_files_decode_with_go_yaml_v2_rules(tmp_path, monkeypatch):
     assert svc["tty"] is True and svc["stdin_open"] is False
     env = v3._mapping_with_equals(svc["environment"])
     assert env == {"A": "true", "B": "1000", "C": "511", "D": "22:22", "E": "1.5"}
+
+
+@pytest.mark.parametrize("env,where", [("Y: 1", "services.s.environment: true"),
+                                       ("1: x", "services.s.environment: 1")])
+def test_compose_v3_non_string_keys_fail_the_file(tmp_path, env, where):
+    """docker/cli's ParseYAML rejects a document with any non-string mapping key
+    (go-yaml v2 reads ``Y`` as a bool), so the v3 loader does not load it."""
+    from move2kube_amd.source.compose import v3
+    p = tmp_path / "docker-compose.yaml"
+    p.write_text("version: '3'\nservices:\n  s:\n    image: busybox\n    environment:\n      %s\n" % env)
+    with pytest.raises(v3.ComposeError, match="Non-string key in " + where.replace(".", "\\.")):
+        v3.parse_v3(str(p))

@@ -61,3 +61,72 @@ def test_ingress_and_openshift_extras(tmp_path, monkeypatch):
     assert route["spec"]["host"] == "web.example.com" and route["spec"]["to"]["name"] == "plain-dep"
     for name in WORKLOADS:
         assert "%s-imagestream.yaml" % name in ocp and "%s-route.yaml" % name in ocp
+
+
+# -- typed decode (client-go UniversalDeserializer: sigs.k8s.io/yaml + encoding/json)
+
+_DEPLOY = """apiVersion: apps/v1
+kind: Deployment
+metadata:
+  name: d
+  labels: {app: d}
+spec:
+  replicas: %s
+  template:
+    spec:
+      containers:
+      - name: c
+        image: i
+        ports:
+        - containerPort: %s
+"""
+
+
+@pytest.mark.parametrize("replicas,port,ok", [
+    ("2", "80", True),
+    ("2.0", "80", True),          # JSON 2 after the YAML->JSON step
+    ("2.5", "80", False),         # not an int32
+    ('"2"', "80", False),         # string into *int32
+    ("2", '"80"', False),         # string into int32 containerPort
+    ("yes", "80", False),         # go-yaml v2: yes is a bool
+])
+def test_typed_decode_rejects_type_mismatches(replicas, port, ok):
+    from move2kube_amd.k8s import scheme
+    text = _DEPLOY % (replicas, port)
+    if ok:
+        assert scheme.decode(text)["spec"]["template"]["spec"]["containers"][0]["ports"][0]["containerPort"] == 80
+    else:
+        with pytest.raises(scheme.DecodeError, match="cannot unmarshal"):
+            scheme.decode(text)
+
+
+def test_typed_decode_string_maps_and_int_or_string():
+    from move2kube_amd.k8s import scheme
+    svc = "apiVersion: v1\nkind: Service\nmetadata: {name: s, labels: {version: %s}}\n" \
+          "spec: {ports: [{port: 80, targetPort: %s}]}\n"
+    assert scheme.decode(svc % ('"1"', "http"))["spec"]["ports"][0]["targetPort"] == "http"
+    assert scheme.decode(svc % ('"1"', "8080"))["spec"]["ports"][0]["targetPort"] == 8080
+    with pytest.raises(scheme.DecodeError, match="map\\[string\\]string|type string"):
+        scheme.decode(svc % ("1", "http"))        # label value must be a string
+    with pytest.raises(scheme.DecodeError):
+        scheme.decode(svc % ('"1"', "1.5"))       # IntOrString takes no fractions
+
+
+def test_emitted_objects_decode_back():
+    """Every registered object in the expected output trees passes the typed decode."""
+    from move2kube_amd.k8s import scheme, schema
+    from move2kube_amd.utils import yamlio
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    n = 0
+    for dp, _dn, fns in os.walk(golden):
+        for fn in fns:
+            if not fn.endswith((".yaml", ".yml")):
+                continue
+            with open(os.path.join(dp, fn)) as f:
+                docs = yamlio.load_all_v2(f.read())
+            for d in docs:
+                if (isinstance(d, dict) and isinstance(d.get("kind"), str) and isinstance(d.get("apiVersion"), str)
+                        and scheme.is_registered(d["apiVersion"], d["kind"], "all")):
+                    schema.check(d)
+                    n += 1
+    assert n > 200
