@@ -14,6 +14,7 @@ from ...containerizer.reusedockerfile import ReuseDockerfileContainerizer
 from ...models import ir as irtypes
 from ...utils import common, log, yamlio
 from ...utils.constants import VOLUME_PREFIX, settings
+from . import schema as cschema
 from . import utils as cu
 from .interpolate import InterpolationError, interpolate, parse_env_file
 from .v3 import ComposeError, _as_list_of_str, _labels, _scalar_str
@@ -96,6 +97,10 @@ def parse_v2(path):
         for k in svc:
             if k not in allowed:
                 raise ComposeError("Unsupported config option for %s service: '%s'" % (name, k))
+        try:
+            cschema.validate_v2_service(name, svc)
+        except cschema.SchemaError as e:
+            raise ComposeError("Service %s configuration is invalid: %s" % (name, e))
         if version == "":
             has_build = "build" in svc or "dockerfile" in svc
             if ("image" in svc) == ("build" in svc) or ("image" in svc and has_build):
@@ -117,12 +122,18 @@ def parse_v2(path):
                     else:
                         log.warning("Unable to find env config file %s referred in service %s in file %s. Ignoring it.", p, name, path)
                 svc[cu.ENV_FILE] = kept
-        services.append(_load_service(name, svc, base, version))
+        try:
+            services.append(_load_service(name, svc, base, version))
+        except (ValueError, TypeError) as e:  # bad port spec, memory size, ...
+            raise ComposeError("Failed to load service %s in %s: %s" % (name, path, e))
     services.sort(key=lambda s: s["name"])
     networks = {}
     if version:
-        for nname, spec in (parsed.get("networks") or {}).items():
-            spec = spec or {}
+        nets = parsed.get("networks") or {}
+        if not isinstance(nets, dict):
+            raise ComposeError("networks must be a mapping")
+        for nname, spec in nets.items():
+            spec = spec if isinstance(spec, dict) else {}
             ext = spec.get("external")
             external = bool(ext) if not isinstance(ext, dict) else True
             real = nname

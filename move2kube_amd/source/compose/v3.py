@@ -14,6 +14,7 @@ from ...containerizer.reusedockerfile import ReuseDockerfileContainerizer
 from ...models import ir as irtypes
 from ...utils import common, log, yamlio
 from ...utils.constants import VOLUME_PREFIX
+from . import schema as cschema
 from . import utils as cu
 from .interpolate import InterpolationError, interpolate, parse_env_file
 
@@ -196,6 +197,10 @@ def parse_v3(path):
     except InterpolationError as e:
         raise ComposeError(str(e))
     services = _validate(parsed)
+    try:
+        cschema.validate_v3(parsed)
+    except cschema.SchemaError as e:
+        raise ComposeError(str(e))
     wd = os.path.dirname(path)
     cfg = {"version": version, "services": [], "networks": {}, "volumes": parsed.get("volumes") or {},
            "secrets": {}, "configs": {}}
@@ -219,7 +224,10 @@ def parse_v3(path):
                 f = cu.resolve_bind_source(f, wd)
             cfg[kind][name] = {"file": f, "external": external, "name": spec.get("name") or ""}
     for sname in services:
-        cfg["services"].append(_load_service(sname, services[sname] or {}, wd, env))
+        try:
+            cfg["services"].append(_load_service(sname, services[sname] or {}, wd, env))
+        except (ValueError, TypeError) as e:  # bad port spec, duration, size, ...
+            raise ComposeError("Failed to load service %s in %s: %s" % (sname, path, e))
     cfg["services"].sort(key=lambda s: s["name"])
     return cfg
 

@@ -66,3 +66,55 @@ def test_native_emitter_matches_python_specification(doc, sort_maps):
     if not yamlio._native():
         return
     assert yamlio.dump(doc, sort_maps) == yamlio.dump_py(doc, sort_maps)
+
+
+# -- robustness: arbitrary compose documents never crash the loaders ---------
+
+_FUZZ_KEYS = ["image", "build", "ports", "expose", "environment", "env_file", "volumes", "deploy", "healthcheck",
+              "command", "entrypoint", "labels", "networks", "secrets", "configs", "tmpfs", "restart", "user",
+              "working_dir", "hostname", "domainname", "privileged", "tty", "stdin_open", "cap_add", "cap_drop",
+              "dns", "extra_hosts", "logging", "mem_limit", "cpu_shares", "pid", "stop_grace_period", "devices",
+              "links", "depends_on", "container_name", "ulimits", "sysctls", "security_opt", "read_only",
+              "shm_size", "init"]
+_FUZZ_INNER = ["target", "published", "source", "type", "mode", "resources", "limits", "memory", "cpus",
+               "replicas", "test", "interval", "disable", "external", "name", "driver", "file", "read_only",
+               "size", "protocol", "x-a"]
+_FUZZ_SCALARS = [None, True, False, 0, 1, -5, 80, 1.5, "", "x", "80:80", "1g", "a=b", "/tmp:/x:ro",
+                 "8080-8081:80-81", "udp", "10s", "${X}", "$$", "CMD-SHELL", "127.0.0.1:5000:5000/udp"]
+
+
+def _fuzz_value(rng, depth=0):
+    r = rng.random()
+    if depth > 2 or r < 0.5:
+        return rng.choice(_FUZZ_SCALARS)
+    if r < 0.75:
+        return [_fuzz_value(rng, depth + 1) for _ in range(rng.randint(0, 3))]
+    return {rng.choice(_FUZZ_KEYS + _FUZZ_INNER): _fuzz_value(rng, depth + 1) for _ in range(rng.randint(0, 4))}
+
+
+def test_compose_loaders_never_crash(tmp_path):
+    """Randomly typed compose documents either load or fail with ComposeError
+    (the reference's loaders reject them through the compose JSON schema)."""
+    import random
+    from move2kube_amd.models import plan as plantypes
+    from move2kube_amd.source.compose import v1v2, v3
+    rng = random.Random(1234)
+    p = str(tmp_path / "docker-compose.yaml")
+    plan = plantypes.new_plan()
+    plan.root_dir = str(tmp_path)
+    loaded = 0
+    for _ in range(250):
+        svc = {rng.choice(_FUZZ_KEYS): _fuzz_value(rng) for _ in range(rng.randint(1, 6))}
+        doc = {"version": rng.choice(["3", "3.7", "2", "2.1"]), "services": {"s": svc}}
+        for key in ("volumes", "networks", "secrets"):
+            if rng.random() < 0.3:
+                doc[key] = {"k": _fuzz_value(rng)}
+        with open(p, "w") as f:
+            f.write(yamlio.dump(doc))
+        for loader in (v3.V3Loader, v1v2.V1V2Loader):
+            try:
+                loader().convert_to_ir(p, plan, plantypes.Service("s", plantypes.COMPOSE2KUBE))
+                loaded += 1
+            except v3.ComposeError:
+                pass
+    assert loaded > 0
