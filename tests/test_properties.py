@@ -118,3 +118,52 @@ def test_compose_loaders_never_crash(tmp_path):
             except v3.ComposeError:
                 pass
     assert loaded > 0
+
+
+_K8S_KINDS = [("apps/v1", "Deployment"), ("v1", "Service"), ("networking.k8s.io/v1", "Ingress"),
+              ("extensions/v1beta1", "Ingress"), ("v1", "Pod"), ("apps/v1", "StatefulSet"), ("apps/v1", "DaemonSet"),
+              ("batch/v1", "Job"), ("v1", "ConfigMap"), ("v1", "Secret"), ("v1", "PersistentVolumeClaim"),
+              ("serving.knative.dev/v1", "Service"), ("route.openshift.io/v1", "Route"),
+              ("apps.openshift.io/v1", "DeploymentConfig"), ("networking.k8s.io/v1", "NetworkPolicy")]
+_K8S_KEYS = ["spec", "template", "containers", "ports", "containerPort", "port", "targetPort", "name", "image",
+             "replicas", "selector", "matchLabels", "rules", "http", "paths", "path", "backend", "serviceName",
+             "servicePort", "service", "number", "volumes", "volumeMounts", "env", "value", "resources", "data",
+             "type", "host", "to", "kind", "tls", "hosts", "labels", "clusterIP", "protocol", "accessModes"]
+_K8S_SCALARS = [None, True, False, 0, 80, "80", "x", "http", "/", 1.5, "", "TCP", "ClusterIP", "1Gi"]
+
+
+def test_translate_never_crashes_on_arbitrary_manifests(tmp_path, monkeypatch):
+    """Randomly shaped Kubernetes/Knative/OpenShift manifests: translate either
+    completes or stops with the reference's fatal "nothing to containerize";
+    objects that do not fit their Go types are skipped at decode time."""
+    import random
+    from move2kube_amd import api
+    from move2kube_amd.utils import log
+    monkeypatch.setenv("M2K_NO_NETWORK", "1")
+    monkeypatch.setenv("M2K_DISABLE_CNB", "1")
+    rng = random.Random(99)
+
+    def val(d=0):
+        r = rng.random()
+        if d > 5 or r < 0.3:
+            return rng.choice(_K8S_SCALARS)
+        if r < 0.55:
+            return [val(d + 1) for _ in range(rng.randint(0, 2))]
+        return {rng.choice(_K8S_KEYS): val(d + 1) for _ in range(rng.randint(1, 4))}
+
+    done = 0
+    for it in range(40):
+        src = tmp_path / ("src%d" % it)
+        src.mkdir()
+        for i in range(rng.randint(1, 3)):
+            gv, kind = rng.choice(_K8S_KINDS)
+            obj = {"apiVersion": gv, "kind": kind, "metadata": {"name": rng.choice("abc")}}
+            for _ in range(rng.randint(1, 3)):
+                obj[rng.choice(["spec", "data", "status"])] = val()
+            (src / ("o%d.yaml" % i)).write_text(yamlio.dump(obj))
+        try:
+            api.translate(str(src), str(tmp_path / ("out%d" % it)))
+            done += 1
+        except log.FatalError as e:
+            assert "No containerization technique was selected" in str(e), str(e)
+    assert done > 0
