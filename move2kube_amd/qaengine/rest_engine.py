@@ -6,9 +6,11 @@ Reference: ``internal/qaengine/httprestengine.go:33-143``.
   the translator produces one.
 * ``POST /problems/current/solution``  -> body is a JSON ``[]string`` answer.
 
-The translator thread and the HTTP handlers hand problems/answers over through
-queues; access to the current problem is guarded by a lock (the reference
-shares it across handler goroutines unsynchronised - SURVEY 2.13 #12).
+The translator thread publishes the open problem under a condition variable
+that GET handlers wait on (every concurrent GET sees the same problem) and
+takes the answer off a queue; the reference shares ``currentProblem`` across
+handler goroutines unsynchronised and hands each waiting GET its own problem
+off a channel.
 """
 
 import json
@@ -41,8 +43,10 @@ class HTTPRESTEngine(Engine):
         self.port = port
         self.host = host
         self.current = qa.Problem(id=0, resolved=True)
-        self._cur_lock = threading.Lock()
-        self.problems = queue.Queue()
+        # guards ``current``; GET handlers wait on it for an open problem, so
+        # any number of concurrent GETs see the same problem (the reference
+        # hands each waiting handler its own problem off a channel)
+        self._cond = threading.Condition()
         self.answers = queue.Queue()
         self.server = None
         self.thread = None
@@ -74,10 +78,10 @@ class HTTPRESTEngine(Engine):
                 if self.path.split("?")[0] != CURRENT_SOLUTION_URL:
                     self._send(404, "404 page not found\n", "text/plain")
                     return
-                n = int(self.headers.get("Content-Length") or 0)
-                body = self.rfile.read(n)
                 try:
-                    sol = json.loads(body.decode() or "null")
+                    n = int(self.headers.get("Content-Length") or 0)
+                    body = self.rfile.read(max(0, n))
+                    sol = json.loads(body.decode("utf-8") or "null")
                     if sol is not None and not (isinstance(sol, list) and all(isinstance(x, str) for x in sol)):
                         raise ValueError("solution must be a JSON array of strings")
                 except ValueError as e:
@@ -104,21 +108,14 @@ class HTTPRESTEngine(Engine):
             self.server.server_close()
 
     # called from HTTP handler threads
-    def next_problem(self):
-        with self._cur_lock:
-            cur = self.current
-            if cur.resolved or cur.id == 0:
-                need_new = True
-            else:
-                return cur.copy()
-        if need_new:
-            p = self.problems.get()
-            with self._cur_lock:
-                self.current = p
-                return p.copy()
+    def next_problem(self, timeout=None):
+        """The open problem; blocks until the translator asks one."""
+        with self._cond:
+            self._cond.wait_for(lambda: self.current.id != 0 and not self.current.resolved, timeout)
+            return self.current.copy()
 
     def submit_solution(self, sol):
-        with self._cur_lock:
+        with self._cond:
             if self.current.id == 0 or self.current.resolved:
                 return "no open problem"
             p = self.current.copy()
@@ -136,7 +133,9 @@ class HTTPRESTEngine(Engine):
             prob.resolved = True
         if not prob.resolved:
             log.debug("Passing problem to HTTP REST QA Engine ID: %d, desc: %s", prob.id, prob.desc)
-            self.problems.put(prob)
+            with self._cond:
+                self.current = prob.copy()
+                self._cond.notify_all()
             prob = self.answers.get()
             if not prob.resolved:
                 raise qa.ProblemError("Unable to resolve question %s" % prob.desc)

@@ -60,6 +60,45 @@ def test_rest_engine_round_trip():
         e.stop()
 
 
+def test_rest_engine_concurrent_gets_and_bad_requests():
+    """GETs that wait at the same time all receive the same open problem, and
+    two problems asked in a row are served in order; malformed solution
+    bodies get a 500 without disturbing the open problem."""
+    e = HTTPRESTEngine(0, "127.0.0.1")
+    qaengine.reset()
+    qaengine.add_engine(e)
+    answers = []
+
+    def ask():
+        for desc in ("first", "second"):
+            p = qa.new_input_problem(desc, [], "d")
+            answers.append(qaengine.fetch_answer(p).get_string_answer())
+
+    seen = []
+
+    def get():
+        seen.append(json.loads(_get(e.port, "/problems/current")[1])["description"])
+
+    getters = [threading.Thread(target=get) for _ in range(4)]
+    for g in getters:
+        g.start()
+    t = threading.Thread(target=ask)
+    t.start()
+    try:
+        for g in getters:
+            g.join(20)
+        assert seen == ["first"] * 4
+        assert _post(e.port, "/problems/current/solution", "{not json")[0] == 500
+        assert _post(e.port, "/problems/current/solution", '[1, 2]')[0] == 500
+        assert _post(e.port, "/problems/current/solution", '["one"]')[0] == 200
+        assert json.loads(_get(e.port, "/problems/current")[1])["description"] == "second"
+        assert _post(e.port, "/problems/current/solution", '["two"]')[0] == 200
+        t.join(20)
+        assert answers == ["one", "two"]
+    finally:
+        e.stop()
+
+
 def test_cli_engine_select_confirm_input_multiselect():
     out = io.StringIO()
     inp = io.StringIO("2\ny\nhello\n1,3\n\n")
