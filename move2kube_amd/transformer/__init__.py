@@ -79,7 +79,7 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
                                           DEFAULT_FILE_PERMISSION)
         else:
             # the reference hands the template a struct without the field it ranges over,
-            # so template execution fails and no file is written (SURVEY 2.13 #1)
+            # so template execution fails and no file is written (SURVEY 2.13 #2)
             log.error("Unable to create manual image : template: manualimages:5:17: executing \"manualimages\" at "
                       "<.Images>: can't evaluate field Images in type struct { Scripts []string }")
     if buildscripts:

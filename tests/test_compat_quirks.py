@@ -1,0 +1,132 @@
+"""Behaviour switch for the reference's output-affecting quirks.
+
+``M2K_COMPAT=reference`` (the default) keeps the reference's observable behaviour
+so that manifests and QA caches match it; ``M2K_COMPAT=fixed`` applies the bug
+fix.  Each test pins both sides of one numbered quirk.  Crash/hang quirks are
+fixed in both modes and are pinned by their own tests (``test_qa_engines_io.py``
+for #12, ``test_collectors.py`` for #8)."""
+
+import os
+
+import pytest
+
+from move2kube_amd.apiresourceset import KnativeAPIResourceSet
+from move2kube_amd.collector import images
+from move2kube_amd.containerizer.base import ContainerizerError, Containerizers
+from move2kube_amd.models import plan as plantypes
+from move2kube_amd.models import qa
+from move2kube_amd.source.compose import v3
+from move2kube_amd.utils.constants import settings
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STUBS = os.path.join(ROOT, "tests", "fixtures", "stubbin")
+
+MODES = ["reference", "fixed"]
+
+KSVC = """apiVersion: serving.knative.dev/v1
+kind: Service
+metadata:
+  name: hello
+spec:
+  template:
+    spec:
+      containers:
+        - image: gcr.io/knative-samples/helloworld-go
+"""
+
+
+@pytest.fixture(params=MODES)
+def mode(request, monkeypatch):
+    monkeypatch.setattr(settings, "compat", request.param)
+    return request.param
+
+
+def test_default_mode_is_reference(monkeypatch):
+    monkeypatch.delenv("M2K_COMPAT", raising=False)
+    from move2kube_amd.utils.constants import _Settings
+    assert _Settings().compat == "reference" and not _Settings().fixed
+
+
+def test_q1_knative_services_discovered_only_when_fixed(tmp_path, mode):
+    (tmp_path / "ksvc.yaml").write_text(KSVC)
+    (tmp_path / "other.yaml").write_text("apiVersion: v1\nkind: ConfigMap\nmetadata:\n  name: c\n")
+    p = plantypes.new_plan()
+    p.root_dir = str(tmp_path)
+    services = KnativeAPIResourceSet().get_service_options(str(tmp_path), p)
+    if mode == "reference":
+        assert services == []  # inverted type check: real Knative services are skipped
+    else:
+        assert [s.service_name for s in services] == ["hello"]
+        assert services[0].source_artifacts[plantypes.KNATIVE_FILE_ARTIFACT] == [str(tmp_path / "ksvc.yaml")]
+
+
+def test_q6_compose_v3_zero_value_storages(tmp_path, mode):
+    (tmp_path / "s.txt").write_text("s3cret\n")
+    (tmp_path / "docker-compose.yaml").write_text(
+        'version: "3.7"\nservices:\n  web:\n    image: nginx\n    secrets: [db]\n'
+        'secrets:\n  db:\n    file: ./s.txt\n')
+    p = plantypes.new_plan()
+    p.root_dir = str(tmp_path)
+    ir = v3.V3Loader().convert_to_ir(str(tmp_path / "docker-compose.yaml"), p,
+                                     plantypes.Service("web", plantypes.COMPOSE2KUBE))
+    names = [s.name for s in ir.storages]
+    if mode == "reference":
+        assert names == ["", "db"]  # make([]Storage, n) then append
+    else:
+        assert names == ["db"]
+
+
+def test_q9_image_names_collected_only_when_fixed(monkeypatch, mode):
+    monkeypatch.setenv("PATH", STUBS + os.pathsep + "/usr/bin:/bin")
+    got = images.get_all_image_names()
+    assert got == ([] if mode == "reference" else ["app/web:1.0"])  # "<none>" entries always dropped
+
+
+def test_q10_cache_merge_duplicates(mode):
+    def cache(answer):
+        c = qa.Cache("c.yaml")
+        p = qa.new_input_problem("Enter the name", [], "")
+        p.set_answer([answer])
+        c.problems.append(p)
+        return c
+
+    a = cache("first")
+    a._merge(cache("second"))
+    answers = [p.answer[0] for p in a.problems]
+    assert answers == (["first", "second"] if mode == "reference" else ["first"])
+    # either way the first answer is the one replayed
+    q = qa.new_input_problem("Enter the name", [], "")
+    assert a.get_solution(q).answer == ["first"]
+
+
+def test_q15_manual_containerization_dispatch(tmp_path, mode):
+    cz = Containerizers()  # registry without Manual, as in the reference
+    s = plantypes.Service("app", plantypes.CFMANIFEST2KUBE)
+    s.container_build_type = plantypes.MANUAL
+    s.image = "app:latest"
+    if mode == "reference":
+        with pytest.raises(ContainerizerError):
+            cz.get_container(plantypes.new_plan(), s)
+    else:
+        c = cz.get_container(plantypes.new_plan(), s)
+        assert c.image_names == ["app:latest"] and c.new
+
+
+def test_q5_cf_app_path_joined_onto_manifest_file(tmp_path, mode, monkeypatch):
+    from move2kube_amd import assets
+    from move2kube_amd.source.cfmanifest2kube import CfManifestTranslator
+    monkeypatch.setenv("M2K_DISABLE_CNB", "1")
+    assets.setup()
+    app = tmp_path / "src" / "app"
+    app.mkdir(parents=True)
+    (app / "package.json").write_text('{"name": "web", "scripts": {"start": "node index.js"}}\n')
+    (tmp_path / "src" / "manifest.yml").write_text("applications:\n- name: web\n  path: app\n")
+    p = plantypes.new_plan()
+    p.root_dir = str(tmp_path / "src")
+    services = CfManifestTranslator().get_service_options(str(tmp_path / "src"), p)
+    dockerfile = [s for s in services if s.container_build_type == plantypes.NEW_DOCKERFILE]
+    if mode == "reference":
+        # <manifest.yml>/app does not exist, so the nodejs detector never sees the app
+        assert dockerfile == []
+    else:
+        assert [s.service_name for s in dockerfile] == ["web"]
