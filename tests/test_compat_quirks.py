@@ -130,3 +130,72 @@ def test_q5_cf_app_path_joined_onto_manifest_file(tmp_path, mode, monkeypatch):
         assert dockerfile == []
     else:
         assert [s.service_name for s in dockerfile] == ["web"]
+
+
+def _translate(tmp_path, monkeypatch, files, name="q", curate=True):
+    import shutil
+    from move2kube_amd import api
+    from move2kube_amd.utils import yamlio
+    monkeypatch.setenv("M2K_NO_NETWORK", "1")
+    monkeypatch.setenv("M2K_DISABLE_CNB", "1")
+    src = tmp_path / "src"
+    src.mkdir()
+    for rel, text in files.items():
+        if text is None:
+            shutil.copytree(os.path.join(ROOT, "samples", rel), str(src / rel))
+        else:
+            (src / rel).parent.mkdir(parents=True, exist_ok=True)
+            (src / rel).write_text(text)
+    with api.Session(qaskip=True) as session:
+        # curate=False keeps the planner's choices (the curator's default cluster is Kubernetes)
+        out = session.translate(str(src), str(tmp_path / "out"), name=name, curate=curate)
+    objdir = os.path.join(out, name)
+    return {f: yamlio.load(open(os.path.join(objdir, f)).read()) for f in sorted(os.listdir(objdir))}
+
+
+CLUSTER_WITHOUT_HPA = """apiVersion: move2kube.konveyor.io/v1alpha1
+kind: ClusterMetadata
+metadata:
+  name: nohpa
+spec:
+  storageClasses: [default]
+  apiKindVersionMap:
+    Deployment: [apps/v1]
+    Service: [v1]
+    Secret: [v1]
+    PersistentVolumeClaim: [v1]
+"""
+
+HPA = ("apiVersion: autoscaling/v1\nkind: HorizontalPodAutoscaler\nmetadata:\n  name: web\nspec:\n"
+       "  maxReplicas: 3\n  scaleTargetRef:\n    apiVersion: apps/v1\n    kind: Deployment\n    name: nodejs\n")
+
+
+def test_q3_unsupported_kinds_written_unless_fixed(tmp_path, mode, monkeypatch):
+    objs = _translate(tmp_path, monkeypatch, {"nodejs": None, "k8s/hpa.yaml": HPA,
+                                             "cluster/nohpa.yaml": CLUSTER_WITHOUT_HPA},
+                      curate=False)
+    assert "nodejs-deployment.yaml" in objs and "nodejs-service.yaml" in objs
+    # the K8s transformer never copies IgnoreUnsupportedKinds from the IR in the reference
+    assert ("web-horizontalpodautoscaler.yaml" in objs) == (mode == "reference")
+
+
+COMPOSE_TWO_VOLUMES = """version: "3.7"
+services:
+  db:
+    image: postgres:13
+    volumes:
+      - data1:/var/lib/a
+      - data2:/var/lib/b
+volumes:
+  data1: {}
+  data2: {}
+"""
+
+
+def test_q4_storage_class_for_all_claims(tmp_path, mode, monkeypatch):
+    objs = _translate(tmp_path, monkeypatch, {"docker-compose.yaml": COMPOSE_TWO_VOLUMES})
+    pvcs = {f: o for f, o in objs.items() if o.get("kind") == "PersistentVolumeClaim"}
+    assert sorted(pvcs) == ["data1-persistentvolumeclaim.yaml", "data2-persistentvolumeclaim.yaml"]
+    classes = [o["spec"].get("storageClassName") for o in pvcs.values()]
+    # one class chosen for all claims is assigned to a loop copy in the reference
+    assert classes == ([None, None] if mode == "reference" else ["default", "default"])
