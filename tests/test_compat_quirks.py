@@ -199,3 +199,31 @@ def test_q4_storage_class_for_all_claims(tmp_path, mode, monkeypatch):
     classes = [o["spec"].get("storageClassName") for o in pvcs.values()]
     # one class chosen for all claims is assigned to a loop copy in the reference
     assert classes == ([None, None] if mode == "reference" else ["default", "default"])
+
+
+def test_q13_pull_secret_looked_up_by_registry(tmp_path, mode, monkeypatch):
+    import base64
+    import json
+    from move2kube_amd import api
+    cfg = tmp_path / "dockercfg"
+    cfg.mkdir()
+    (cfg / "config.json").write_text(json.dumps(
+        {"auths": {"quay.io": {"auth": base64.b64encode(b"u:p").decode()}}}))
+    monkeypatch.setenv("DOCKER_CONFIG", str(cfg))
+    monkeypatch.setenv("HOME", str(tmp_path))
+    monkeypatch.setattr(api.Session, "__init__", _session_with_env(api.Session.__init__))
+    objs = _translate(tmp_path, monkeypatch, {"docker-compose.yaml":
+                                              'version: "3.7"\nservices:\n  web:\n    image: quay.io/org/web:1\n'})
+    pod = objs["web-deployment.yaml"]["spec"]["template"]["spec"]
+    # the reference looks the auth up by the target RegistryURL instead of the image's registry,
+    # so a login for quay.io never yields a pull secret for quay.io images
+    secrets = [e["name"] for e in pod.get("imagePullSecrets", [])]
+    assert (secrets == []) == (mode == "reference")
+    if mode == "fixed":
+        assert len(secrets) == 1 and "quay" in secrets[0]
+
+
+def _session_with_env(init):
+    def patched(self, qaskip=True, qacaches=(), ignore_env=True):
+        init(self, qaskip=qaskip, qacaches=qacaches, ignore_env=False)
+    return patched
