@@ -227,3 +227,21 @@ def _session_with_env(init):
     def patched(self, qaskip=True, qacaches=(), ignore_env=True):
         init(self, qaskip=qaskip, qacaches=qacaches, ignore_env=False)
     return patched
+
+
+def test_q2_q15_manual_cf_app_and_manual_images_readme(tmp_path, mode, monkeypatch):
+    from move2kube_amd import api
+    monkeypatch.setenv("M2K_NO_NETWORK", "1")
+    monkeypatch.setenv("M2K_DISABLE_CNB", "1")
+    src = tmp_path / "src"
+    (src / "app").mkdir(parents=True)
+    (src / "app" / "data.bin").write_text("no detector matches this\n")
+    (src / "manifest.yml").write_text("applications:\n- name: legacy\n  path: app\n")
+    out = api.translate(str(src), str(tmp_path / "out"), name="q")
+    readme = os.path.join(out, "Manualimages.md")
+    if mode == "reference":
+        # Manual is not in the containerizer registry and the readme template gets the wrong struct
+        assert not os.path.exists(readme)
+    else:
+        assert os.path.exists(os.path.join(out, "q", "legacy-deployment.yaml"))
+        assert "legacy" in open(readme).read()
