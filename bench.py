@@ -1,30 +1,32 @@
 #!/usr/bin/env python3
-"""Headline benchmark: end-to-end ``translate --qaskip`` of the samples corpus.
+"""Headline benchmark: BASELINE.json configuration 5 on the reference's own
+``samples/`` corpus.
 
 The reference (a Go CLI) publishes no performance numbers; BASELINE.json names
-the fallback metric "translate wall-clock + manifest diff vs ref on samples/".
-One *step* is a complete in-process ``plan`` + ``curate`` (default answers) +
-``translate`` of the whole ``samples/`` tree (13 services: 7 source-directory
-apps, a Dockerfile app, a 3-service compose app, a CF manifest app and a
-Kubernetes YAML app), writing every artifact (k8s YAMLs, compose, Tekton, build
-scripts, QA cache) to a private output directory.  Nothing is cached between
-steps (fresh file index, fresh detector runs, fresh QA engines).
+the fallback metric "translate wall-clock + manifest diff vs ref on samples/"
+and five configurations.  The headline step is configuration 5, "full samples/
+tree -> Helm chart + Operator output with target-cluster GroupVersion
+customize": ``move2kube translate -s samples --qaskip -q
+helm-openshift-qacache.yaml`` (Helm artifacts, Openshift cluster profile, so
+every object goes through the profile's group/version selection:
+DeploymentConfig, Route, ImageStream), including the operator-sdk call
+(stand-in on ``PATH``).  One step = plan + curate (answers replayed from the QA
+cache, defaults otherwise) + translate + write of every artifact, in process;
+nothing is cached between steps (fresh file index, detector runs, QA engines,
+output directory).  ``benchmarks/refconfigs.py`` defines the commands.
 
 Multi-GPU: one rank per GPU (torch.distributed), each rank translating its own
 copy of the corpus (weak scaling); the timed region is bracketed by a barrier
 and ``torch.cuda.synchronize()`` and the slowest rank's time is reported.
-``value`` = total translated services per second over all ranks.
+``value`` = translated services per second summed over all ranks.
 
-Before timing, rank 0 checks the output of one step against the checked-in
-expected tree (``tests/golden/samples``) and reports ``manifest_diff`` (number
-of differing/missing/extra files; 0 = identical).
-
-After timing, a couple of untimed steps rerun in the reference's execution
-model (every detector forked as ``/bin/sh`` one at a time, as
-``internal/containerizer/dockerfilecontainerizer.go:76-83`` does) and report
-``reference_model_ms_per_step`` - a same-machine proxy for the Go tool, whose
-cost is dominated by those forks; the reference publishes no numbers, so
-``vs_baseline`` stays null.
+Correctness (untimed, rank 0): ``manifest_diff_vs_ref`` is the number of
+files that differ from the reference-derived expected trees
+(``tests/golden/reference/<config>``) over all five configurations, and
+``per_config`` gives each configuration's diff plus its warm in-process and
+cold CLI-process p50.  The reference's execution model
+is only emulated in Python (``benchmarks/baseline_configs.py``), so nothing
+here is a measured comparison with the Go tool and ``vs_baseline`` is null.
 """
 
 import argparse
@@ -36,12 +38,13 @@ import tempfile
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SAMPLES = os.path.join(HERE, "samples")
-GOLDEN = os.path.join(HERE, "tests", "golden", "samples")
+for _p in (HERE, os.path.join(HERE, "benchmarks")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
 
-# deterministic, offline runs: no ssh-keyscan, no docker/podman/pack probing
-os.environ.setdefault("M2K_NO_NETWORK", "1")
-os.environ.setdefault("M2K_DISABLE_CNB", "1")
+import refconfigs  # noqa: E402
+
+BASELINE_CONFIG = "full samples/ tree → Helm chart + Operator output with target-cluster GroupVersion customize"
 
 
 def _dist_env():
@@ -49,39 +52,31 @@ def _dist_env():
 
 
 def tree_files(root):
+    return refconfigs.tree_files(root)
+
+
+def per_config_checks(runs):
+    """Untimed: every configuration's diff vs the reference-derived tree and its
+    warm / cold p50 (``benchmarks/baseline_configs.py``)."""
+    import baseline_configs
     out = {}
-    for dp, _dn, fns in os.walk(root):
-        for fn in fns:
-            p = os.path.join(dp, fn)
-            out[os.path.relpath(p, root)] = p
+    for name in refconfigs.CONFIGS:
+        r = baseline_configs.warm_runs(name, runs)
+        cold, cold_diff = baseline_configs.cold_runs(name, runs)
+        out[name] = {"manifest_diff_vs_ref": r["manifest_diff_vs_ref"] + cold_diff,
+                     "warm_p50_ms": r["warm_p50_ms"], "cold_p50_ms": cold}
     return out
-
-
-def manifest_diff(actual_root, golden_root):
-    """Count of files that differ, are missing or are extra vs the golden tree."""
-    if not os.path.isdir(golden_root):
-        return None
-    a, g = tree_files(actual_root), tree_files(golden_root)
-    diff = 0
-    for rel in set(a) | set(g):
-        if rel not in a or rel not in g:
-            diff += 1
-            continue
-        with open(a[rel], "rb") as fa, open(g[rel], "rb") as fg:
-            if fa.read() != fg.read():
-                diff += 1
-    return diff
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--src", default=SAMPLES)
-    ap.add_argument("--keep", action="store_true", help="keep the output directory")
-    ap.add_argument("--reference-model-steps", type=int, default=2,
-                    help="untimed steps in the reference's serial fork-per-detector mode (0 = skip)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default=refconfigs.HEADLINE, choices=sorted(refconfigs.CONFIGS))
+    ap.add_argument("--check-runs", type=int, default=3,
+                    help="warm/cold runs per configuration in the untimed per-config check (0 = skip)")
+    ap.add_argument("--keep", action="store_true", help="keep the work directory")
     args = ap.parse_args()
 
     world, rank, local_rank = _dist_env()
@@ -103,71 +98,46 @@ def main():
         if have_cuda:
             torch.cuda.synchronize()
 
-    sys.path.insert(0, HERE)
-    from move2kube_amd import api
     from move2kube_amd.utils import log
     log.set_quiet()
 
     work = tempfile.mkdtemp(prefix="m2k-bench-r%d-" % rank)
+    run = refconfigs.Run(args.config, work).prepare()
+    undo = run.apply_env()
     n_services = 0
+    diff_headline = None
     phase_ms = None
     try:
-        # private copy outside any git checkout, so output is location independent
-        src = os.path.join(work, "samples")
-        shutil.copytree(args.src, src, symlinks=True)
-        with api.Session(qaskip=True) as s:
-            def step():
-                out = s.translate(src, os.path.join(work, "out"), name="samples")
-                return out
-
-            # correctness gate (rank 0) + service count
-            out = step()
-            plan = s.plan(src, "samples")
-            n_services = len(plan.services)
-            diff = manifest_diff(out, GOLDEN) if rank == 0 else None
+        with run.session() as s:
+            out = run.step(s)  # first (warm-up) step doubles as the correctness gate
+            n_services = len(s.plan(run.src, refconfigs.PROJECT).services)
+            if rank == 0:
+                diff_headline = refconfigs.manifest_diff_vs_ref(args.config, out)
             for _ in range(max(0, args.warmup - 1)):
-                step()
+                run.step(s)
             barrier()
             t0 = time.perf_counter()
             for _ in range(args.steps):
-                step()
+                run.step(s)
             barrier()
             elapsed = time.perf_counter() - t0
-            # Untimed: one traced step for the per-phase breakdown (utils/trace.py)
-            phase_ms = None
             if rank == 0:
+                # untimed: one traced step for the per-phase breakdown (utils/trace.py)
                 from move2kube_amd.utils import trace
                 trace.enable("")
                 try:
-                    step()
+                    run.step(s)
                     phase_ms = {k: round(v, 3) for k, v in list(trace.summary().items())[:12]}
                 finally:
                     trace._events = None
-            # Untimed ablation: the reference's execution model (every detector
-            # forked as a shell process, one at a time), same output required.
-            ref_ms = None
-            if args.reference_model_steps > 0 and rank == 0:
-                from move2kube_amd.utils.constants import settings
-                saved = (os.environ.get("M2K_NATIVE_DETECT"), settings.workers)
-                os.environ["M2K_NATIVE_DETECT"] = "0"
-                settings.workers = 1
-                try:
-                    out_ref = step()
-                    t1 = time.perf_counter()
-                    for _ in range(args.reference_model_steps):
-                        step()
-                    ref_ms = (time.perf_counter() - t1) * 1000.0 / args.reference_model_steps
-                    if rank == 0 and diff is not None:
-                        diff += manifest_diff(out_ref, GOLDEN)
-                finally:
-                    if saved[0] is None:
-                        os.environ.pop("M2K_NATIVE_DETECT", None)
-                    else:
-                        os.environ["M2K_NATIVE_DETECT"] = saved[0]
-                    settings.workers = saved[1]
     finally:
+        undo()
         if not args.keep:
             shutil.rmtree(work, ignore_errors=True)
+
+    per_config = None
+    if rank == 0 and args.check_runs > 0:
+        per_config = per_config_checks(args.check_runs)
 
     if dist is not None:
         dev = torch.device("cuda", torch.cuda.current_device()) if have_cuda else torch.device("cpu")
@@ -177,8 +147,11 @@ def main():
     ms = elapsed * 1000.0 / max(1, args.steps)
     value = world * n_services * args.steps / elapsed if elapsed > 0 else 0.0
     if rank == 0:
+        total_diff = diff_headline
+        if per_config is not None and total_diff is not None:
+            total_diff = sum(v["manifest_diff_vs_ref"] for v in per_config.values())
         print(json.dumps({
-            "metric": "translate_throughput_samples",
+            "metric": "translate_throughput (BASELINE fallback: translate wall-clock + manifest diff vs ref on samples/)",
             "value": round(value, 3),
             "unit": "services/s",
             "n_gpus": world,
@@ -189,13 +162,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "n/a",
-            "data": "samples/ corpus (%d services), in-process translate --qaskip, CNB disabled" % n_services,
-            "manifest_diff": diff,
-            "reference_model_ms_per_step": None if ref_ms is None else round(ref_ms, 3),
-            "speedup_vs_reference_model": None if not ref_ms else round(ref_ms / ms, 2),
+            "data": "reference samples/ corpus (%d services), in-process plan+curate+translate per step; "
+                    "stand-ins for operator-sdk; no container engine" % n_services,
+            "manifest_diff_vs_ref": total_diff,
+            "manifest_diff_vs_ref_headline": diff_headline,
+            "per_config": per_config,
             "phase_ms_one_step": phase_ms,
-            "config": {"model": "move2kube translate samples/ (full tree)", "global_batch": world,
-                       "seq_len": n_services, "parallelism": "dp%d" % world},
+            "config": {"model": BASELINE_CONFIG, "command": "move2kube translate -s samples --qaskip -q "
+                       "helm-openshift-qacache.yaml" if args.config == refconfigs.HEADLINE else args.config,
+                       "global_batch": world, "seq_len": n_services, "parallelism": "dp%d" % world},
         }), flush=True)
     if dist is not None:
         dist.destroy_process_group()

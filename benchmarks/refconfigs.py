@@ -1,0 +1,198 @@
+"""The five BASELINE.json configurations over the reference's own ``samples/``
+corpus, shared by ``bench.py``, ``benchmarks/baseline_configs.py`` and
+``tests/test_reference_configs.py``.
+
+Each configuration is a command a user of the reference would type, run
+against a private copy of its inputs laid out the same way every time
+(``<work>/samples``, ``<work>/out``), so that paths embedded in the output
+(``copysources.sh``) are reproducible:
+
+====================  ==========================================================
+``golang``            ``move2kube translate -s samples/golang --qaskip``
+``docker-compose``    ``move2kube translate -s samples/docker-compose --qaskip``
+``java-cnb``          ``move2kube translate -s java --qaskip -q java-cnb-qacache.yaml``
+                      where ``java/`` holds ``samples/java-maven`` and
+                      ``samples/java-gradle``; the cache picks the CNB mode, and
+                      a ``podman`` stand-in on ``PATH`` answers the reference's
+                      container-runtime CNB provider
+                      (``internal/containerizer/cnb/containerruntimeprovider.go``)
+``cf``                ``move2kube collect -a cf -s cf -o collect`` (``cf`` CLI
+                      stand-in), the collected ``m2k_collect/`` copied into the
+                      source tree, then ``move2kube translate -s cf --qaskip``
+``helm-openshift``    ``move2kube translate -s samples --qaskip -q
+                      helm-openshift-qacache.yaml``: the whole corpus to a Helm
+                      chart for the Openshift profile (DeploymentConfig, Route,
+                      ImageStream group/versions), plus the operator
+                      (``operator-sdk`` stand-in)
+====================  ==========================================================
+
+The expected output trees live in ``tests/golden/reference/<config>/``.  They
+are derived from the reference's code and fixtures (``PROVENANCE.md`` there)
+and are never rewritten by a test run; allowed byte differences from what the
+Go binary would write are listed with their reason in ``DEVIATIONS.md``.
+
+External tools are stand-ins on ``PATH`` (``tests/fixtures/configs/bin``);
+``HOME`` points at an empty directory so ``~/.docker/config.json`` of the host
+does not leak into the registry questions (``registrycustomizer.go:71``).
+"""
+
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SAMPLES = os.path.join(ROOT, "samples")
+FIXTURES = os.path.join(ROOT, "tests", "fixtures")
+CONFIG_FIXTURES = os.path.join(FIXTURES, "configs")
+STUB_BIN = os.path.join(CONFIG_FIXTURES, "bin")
+CF_APP = os.path.join(FIXTURES, "extra_samples", "cfapp")
+GOLDEN_REF = os.path.join(ROOT, "tests", "golden", "reference")
+PROJECT = "myproject"  # the CLI default (-n)
+
+# name -> (layout, source dir relative to <work>, QA caches, CNB probing on, collect annotations)
+CONFIGS = {
+    "golang": ("samples", "samples/golang", [], False, None),
+    "docker-compose": ("samples", "samples/docker-compose", [], False, None),
+    "java-cnb": ("java", "java", ["java-cnb-qacache.yaml"], True, None),
+    "cf": ("cf", "cf", [], True, ["cf"]),
+    "helm-openshift": ("samples", "samples", ["helm-openshift-qacache.yaml"], False, None),
+}
+HEADLINE = "helm-openshift"
+
+
+class Run:
+    """One prepared configuration: inputs copied under ``work``."""
+
+    def __init__(self, name, work):
+        self.name = name
+        self.work = os.path.abspath(work)
+        layout, src, caches, cnb, collect = CONFIGS[name]
+        self.layout = layout
+        self.src = os.path.join(self.work, src)
+        self.caches = [os.path.join(CONFIG_FIXTURES, c) for c in caches]
+        self.cnb = cnb
+        self.collect_annotations = collect
+        self.outdir = os.path.join(self.work, "out")
+        self.home = os.path.join(self.work, "home")
+
+    @property
+    def out(self):
+        return os.path.join(self.outdir, PROJECT)
+
+    def prepare(self):
+        os.makedirs(self.home, exist_ok=True)
+        if self.layout == "samples":
+            shutil.copytree(SAMPLES, os.path.join(self.work, "samples"), symlinks=True)
+        elif self.layout == "java":
+            root = os.path.join(self.work, "java")
+            os.makedirs(root)
+            with open(os.path.join(root, ".m2kignore"), "w") as f:
+                f.write(".\n")
+            for d in ("java-maven", "java-gradle"):
+                shutil.copytree(os.path.join(SAMPLES, d), os.path.join(root, d), symlinks=True)
+        elif self.layout == "cf":
+            shutil.copytree(CF_APP, os.path.join(self.work, "cf"), symlinks=True)
+        return self
+
+    def env(self, base=None):
+        """Environment of a configuration run (stand-in tools, private HOME)."""
+        env = dict(os.environ if base is None else base)
+        env["PATH"] = STUB_BIN + os.pathsep + env.get("PATH", "")
+        env["HOME"] = self.home
+        env["M2K_NO_NETWORK"] = "1"
+        env["M2K_DISABLE_CNB"] = "0" if self.cnb else "1"
+        return env
+
+    # -- in-process -------------------------------------------------------
+    def apply_env(self):
+        """Switch this process to the configuration's environment; returns an undo."""
+        saved = {k: os.environ.get(k) for k in ("PATH", "HOME", "M2K_NO_NETWORK", "M2K_DISABLE_CNB")}
+        os.environ.update(self.env())
+
+        def restore():
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        return restore
+
+    def collect_inprocess(self):
+        from move2kube_amd import move2kube
+        # what `collect -o <work>/collect` does (cmd/move2kube/collect.go:41-73)
+        cdir = os.path.join(self.work, "collect", "m2k_collect")
+        shutil.rmtree(cdir, ignore_errors=True)
+        move2kube.collect(self.src, cdir, self.collect_annotations)
+        dst = os.path.join(self.src, "m2k_collect")
+        shutil.rmtree(dst, ignore_errors=True)
+        shutil.copytree(cdir, dst)
+
+    def step(self, session):
+        """One in-process run of the configuration's commands (``session`` is an
+        ``api.Session(qaskip=True, qacaches=run.caches, ignore_env=False)``)."""
+        if self.collect_annotations:
+            self.collect_inprocess()
+        return session.translate(self.src, self.outdir, name=PROJECT)
+
+    def session(self):
+        from move2kube_amd import api
+        return api.Session(qaskip=True, qacaches=self.caches, ignore_env=False)
+
+    # -- CLI processes ------------------------------------------------------
+    def cli_commands(self):
+        """argv lists (after ``python -m move2kube_amd``) of the user's commands."""
+        cmds = []
+        if self.collect_annotations:
+            cmds.append(["collect", "-a", ",".join(self.collect_annotations), "-s", self.src,
+                         "-o", os.path.join(self.work, "collect")])
+        t = ["translate", "-s", self.src, "-o", self.outdir, "--qaskip"]
+        for c in self.caches:
+            t += ["-q", c]
+        cmds.append(t)
+        return cmds
+
+    def run_cli(self, extra_env=None, cwd=None):
+        """Run the commands as separate ``python -m move2kube_amd`` processes."""
+        env = self.env()
+        env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+        if extra_env:
+            env.update(extra_env)
+        for argv in self.cli_commands():
+            p = subprocess.run([sys.executable, "-m", "move2kube_amd"] + argv, env=env, cwd=cwd or self.work,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+            if p.returncode != 0:
+                raise RuntimeError("%s failed: %s" % (argv[0], p.stderr.decode(errors="replace")[-2000:]))
+            if argv[0] == "collect":
+                dst = os.path.join(self.src, "m2k_collect")
+                shutil.rmtree(dst, ignore_errors=True)
+                shutil.copytree(os.path.join(self.work, "collect", "m2k_collect"), dst)
+        return self.out
+
+
+def tree_files(root):
+    out = {}
+    for dp, _dn, fns in os.walk(root):
+        for fn in fns:
+            p = os.path.join(dp, fn)
+            out[os.path.relpath(p, root)] = p
+    return out
+
+
+def diff_files(actual_root, expected_root):
+    """Relative paths that differ, are missing or are extra (sorted)."""
+    a, g = tree_files(actual_root), tree_files(expected_root)
+    bad = sorted(set(a) ^ set(g))
+    for rel in sorted(set(a) & set(g)):
+        with open(a[rel], "rb") as fa, open(g[rel], "rb") as fg:
+            if fa.read() != fg.read():
+                bad.append(rel)
+    return sorted(bad)
+
+
+def manifest_diff_vs_ref(name, actual_root):
+    """Number of files differing from the reference-derived expected tree."""
+    golden = os.path.join(GOLDEN_REF, name)
+    if not os.path.isdir(golden):
+        return None
+    return len(diff_files(actual_root, golden))

@@ -1,6 +1,6 @@
 Move2Kube
 ---------
-The generated artifacts in this directory move all your application components to Knative. Use them to deploy your application in a Knative instance.
+Congratulations! Move2Kube has generated the necessary build artfiacts for moving all your application components to Knative. Using the artifacts in this directory you can deploy your application in a Knative instance
 
 Prerequisites
 -------------
@@ -10,7 +10,7 @@ Prerequisites
 Next Steps
 ----------
 {{if .NewImages -}}
-* Copy this directory into your base source directory, so that the scripts gets merged at the right contexts.
+* Copy this directory into your base source directory, so that the scripts gets merged at the right contexts. 
 * Build your images using buildimages.sh
 * Push images to registry pushimages.sh
 {{end -}}

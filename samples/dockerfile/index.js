@@ -1,1 +1,7 @@
-require("http").createServer((q, r) => r.end("hi\n")).listen(3000);
+import express from 'express'
+
+const port = 8080;
+
+const server = express();
+server.use(express.static("public"))
+server.listen(port, () => console.log("Listening on port", port));

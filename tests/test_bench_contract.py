@@ -30,20 +30,26 @@ def _last_json(stdout):
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only contract test")
 def test_single_rank():
-    p = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1"], cwd=ROOT, env=_env(),
+    p = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--check-runs", "1"], cwd=ROOT,
+                       env=_env(),
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
     assert p.returncode == 0, p.stderr.decode()
     d = _last_json(p.stdout.decode())
     assert KEYS <= set(d)
     assert d["n_gpus"] == 1 and d["steps"] == 1 and d["value"] > 0
-    assert d["manifest_diff"] == 0
+    assert d["manifest_diff_vs_ref"] == 0 and d["manifest_diff_vs_ref_headline"] == 0
+    assert sorted(d["per_config"]) == ["cf", "docker-compose", "golang", "helm-openshift", "java-cnb"]
+    assert all(v["manifest_diff_vs_ref"] == 0 for v in d["per_config"].values())
+    # the headline names BASELINE.json configuration 5 verbatim
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        assert d["config"]["model"] in json.load(f)["configs"]
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only contract test")
 def test_two_ranks_gloo():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29533", "bench.py", "--gpus", "2", "--steps", "1",
-           "--warmup", "1"]
+           "--warmup", "1", "--check-runs", "0"]
     p = subprocess.run(cmd, cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
     assert p.returncode == 0, p.stderr.decode()[-3000:]
     d = _last_json(p.stdout.decode())
@@ -54,13 +60,14 @@ def test_two_ranks_gloo():
 
 def test_baseline_configs_bench_golang():
     """benchmarks/baseline_configs.py (BASELINE.md per-configuration wall clock):
-    one warm, one reference-model and one cold CLI run of the golang config, all
-    identical to the expected tree."""
+    one warm, one fork-model emulation and one cold CLI run of the golang
+    config, all identical to the reference-derived expected tree."""
     p = subprocess.run([sys.executable, os.path.join("benchmarks", "baseline_configs.py"), "--runs", "1",
-                        "--refmodel-runs", "1", "--configs", "golang"], cwd=ROOT, env=_env(),
+                        "--emulation-runs", "1", "--configs", "golang"], cwd=ROOT, env=_env(),
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
     assert p.returncode == 0, p.stderr.decode()[-3000:]
     rows = [json.loads(l) for l in p.stdout.decode().splitlines() if l.startswith("{")]
     cfg = [r for r in rows if r.get("config") == "golang"]
-    assert len(cfg) == 1 and cfg[0]["manifest_diff"] == 0
-    assert cfg[0]["warm_p50_ms"] > 0 and cfg[0]["cold_p50_ms"] > 0 and cfg[0]["refmodel_p50_ms"] > 0
+    assert len(cfg) == 1 and cfg[0]["manifest_diff_vs_ref"] == 0
+    assert cfg[0]["warm_p50_ms"] > 0 and cfg[0]["cold_p50_ms"] > 0
+    assert cfg[0]["python_emulation_of_reference_fork_model_p50_ms"] > 0

@@ -100,3 +100,39 @@ def test_user_detector_outside_assets_not_shortcut(tmp_path, assets_dir):
     d = tmp_path / "custom"
     shutil.copytree(os.path.join(assets_dir, "dockerfiles", "nodejs"), str(d))
     assert builtin_detect.lookup(str(d), "m2kdfdetect.sh") is None
+
+
+@pytest.mark.reference
+def test_detectors_match_reference_scripts(tmp_path, assets_dir):
+    """Oracle: the reference's own detector scripts
+    (``internal/assets/{dockerfiles,s2i}/*/m2k*detect.sh``), run as shell
+    scripts, against our detectors (in-process built-ins) on every directory of
+    the reference ``samples/`` corpus plus the synthetic edge trees above.
+    Exit status (match / no match) and the JSON printed on a match must agree.
+
+    The reference runs them with ``/bin/sh`` (``dockerfilecontainerizer.go:77``).
+    Its python detectors use bash arrays, so they only work where ``/bin/sh``
+    is bash (the reference's UBI8 image, macOS); the oracle runs them with
+    ``bash`` to pin that behaviour (DEVIATIONS.md, "platform shell")."""
+    import subprocess
+    from conftest import ref_path
+    if shutil.which("bash") is None:
+        pytest.skip("bash not available")
+    targets = _make_tree(str(tmp_path / "src"))
+    samples = ref_path("samples")
+    for dp, dns, _fns in os.walk(samples):
+        dns.sort()
+        targets.append(dp)
+    jobs, ref = [], []
+    for rel, script in sorted(builtin_detect.DETECTORS):
+        ref_dir = ref_path("internal", "assets", rel)
+        assert os.path.isfile(os.path.join(ref_dir, script)), rel
+        for t in targets:
+            jobs.append((os.path.join(assets_dir, rel), script, t))
+            p = subprocess.run(["bash", script, t], cwd=ref_dir, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
+            ref.append((p.returncode, p.stdout.decode()))
+    ours = detect_pool.run_detect_jobs(jobs)
+    mism = [(j, rc, out, a.code, a.stdout) for j, (rc, out), a in zip(jobs, ref, ours)
+            if (rc == 0) != (a.code == 0) or (rc == 0 and out != a.stdout)]
+    assert mism == []
+    assert sum(1 for rc, _ in ref if rc == 0) > 20  # the corpus really exercises the detectors

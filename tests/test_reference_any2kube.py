@@ -149,9 +149,7 @@ def test_translate_nodejs_services_to_ir():
     assert c.image_names == wc["imagenames"]
     assert c.new is True and c.exposed_ports == wc["exposedports"] and c.user_id == wc["userid"]
     assert sorted(c.new_files) == sorted(wc["newfiles"])
-    # the script body (after each tool's own comment header) is the same command
-    body = [l for l in c.new_files["nodejs-cnb-build.sh"].splitlines() if l and not l.startswith("#")]
-    wbody = [l for l in wc["newfiles"]["nodejs-cnb-build.sh"].splitlines() if l and not l.startswith("#")]
-    assert body == wbody
+    # byte for byte, license header included
+    assert c.new_files["nodejs-cnb-build.sh"] == wc["newfiles"]["nodejs-cnb-build.sh"]
     assert ir.kubernetes.artifact_type == want["kubernetes"]["artifactType"]
     assert ir.kubernetes.target_cluster_type == want["kubernetes"]["targetCluster"]["type"]
