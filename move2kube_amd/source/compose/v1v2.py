@@ -1,10 +1,15 @@
 """Compose file format v1/v2 loader (reference ``internal/source/compose/v1v2.go``).
 
-Parsing mirrors libcompose as the reference configures it: interpolation with
-``.env`` (current directory) then OS environment lookups, schema validation
-(v1: every top-level key is a service; v2: ``services``/``networks``/
-``volumes``), pruning of missing env_files, and resolution of build contexts
-and bind-volume sources relative to the compose file.
+Parsing mirrors libcompose's ``project.Parse()`` as the reference configures
+it (``v1v2.go:93-129``): interpolation with ``.env`` (current directory) then
+OS environment lookups, pruning of missing env_files (the Preprocess hook,
+``v1v2.go:49-90``), schema validation (v1: every top-level key is a service;
+v2: ``services``/``networks``/``volumes``), then per service libcompose's
+``readEnvFile`` (env_file lines folded into ``environment``) and ``extends``
+(same file or ``file:``, chained; lists appended, maps merged, scalars
+replaced; ``links``/``volumes_from`` cannot be extended), and resolution of
+build contexts and bind-volume sources relative to the file that declared
+them.
 """
 
 import os
@@ -40,8 +45,8 @@ def _normalize_project_name(s):
     return re.sub(r"[^a-z0-9]", "", s.lower())
 
 
-def parse_v2(path):
-    """Parse a v1/v2 compose file -> {"version", "project", "services": [...], "networks": {...}}."""
+def _read_raw(path):
+    """``CreateConfig``: the raw document -> (version, raw services, parsed)."""
     try:
         text = common.read_text(path)
         parsed = yamlio.load_v2(text)
@@ -64,12 +69,15 @@ def parse_v2(path):
         raw_services = parsed.get("services") or {}
         if not isinstance(raw_services, dict):
             raise ComposeError("services must be a mapping")
-        allowed = V2_SERVICE_KEYS
     else:
         version = ""
         raw_services = parsed
-        allowed = V1_SERVICE_KEYS
-    # env lookup: .env of the working directory first, then the OS environment (libcompose)
+    return version, raw_services, parsed
+
+
+def _env_lookup():
+    """libcompose ``ComposableEnvLookup``: ``.env`` of the working directory,
+    then the OS environment (``v1v2.go:98-112``)."""
     env_path = ".env" if settings.ignore_environment else os.path.abspath(".env")
     dotenv = {}
     if os.path.isfile(env_path):
@@ -82,12 +90,40 @@ def parse_v2(path):
         if k in dotenv:
             return dotenv[k]
         return os.environ.get(k)
-    try:
-        raw_services = interpolate(raw_services, lookup, warn_missing=True)
-    except InterpolationError as e:
-        raise ComposeError(str(e))
-    base = os.path.dirname(os.path.abspath(path))
-    services = []
+    return lookup
+
+
+def _prune_env_files(raw_services, compose_path):
+    """``removeNonExistentEnvFilesV2`` (``v1v2.go:49-90``), the Preprocess hook.
+    Paths are checked against the directory of the compose file the reference
+    passed in - also for services of a file pulled in through ``extends``."""
+    base = os.path.dirname(os.path.abspath(compose_path))
+    for name, svc in raw_services.items():
+        if not isinstance(svc, dict) or cu.ENV_FILE not in svc:
+            continue
+        ef = svc[cu.ENV_FILE]
+        if isinstance(ef, str):
+            p = ef if os.path.isabs(ef) else os.path.join(base, ef)
+            if not os.path.isfile(p):
+                log.warning("Unable to find env config file %s referred in service %s in file %s. Ignoring it.",
+                            p, name, compose_path)
+                del svc[cu.ENV_FILE]
+        elif isinstance(ef, list):
+            kept = []
+            for e in ef:
+                if not isinstance(e, str):
+                    continue
+                p = e if os.path.isabs(e) else os.path.join(base, e)
+                if os.path.isfile(p):
+                    kept.append(e)
+                else:
+                    log.warning("Unable to find env config file %s referred in service %s in file %s. Ignoring it.",
+                                p, name, compose_path)
+            svc[cu.ENV_FILE] = kept
+
+
+def _validate(raw_services, version):
+    allowed = V2_SERVICE_KEYS if version else V1_SERVICE_KEYS
     for name, svc in raw_services.items():
         if not isinstance(name, str):
             raise ComposeError("Non-string service name %r" % (name,))
@@ -101,29 +137,148 @@ def parse_v2(path):
             cschema.validate_v2_service(name, svc)
         except cschema.SchemaError as e:
             raise ComposeError("Service %s configuration is invalid: %s" % (name, e))
-        if version == "":
+        if version == "" and "extends" not in svc:
             has_build = "build" in svc or "dockerfile" in svc
             if ("image" in svc) == ("build" in svc) or ("image" in svc and has_build):
-                raise ComposeError("Service %s has neither an image nor a build context specified. At least one must be provided." % name)
-        # prune env files that do not exist
-        if cu.ENV_FILE in svc:
-            ef = svc[cu.ENV_FILE]
-            if isinstance(ef, str):
-                p = ef if os.path.isabs(ef) else os.path.join(base, ef)
-                if not os.path.isfile(p):
-                    log.warning("Unable to find env config file %s referred in service %s in file %s. Ignoring it.", p, name, path)
-                    del svc[cu.ENV_FILE]
-            elif isinstance(ef, list):
-                kept = []
-                for e in ef:
-                    p = e if os.path.isabs(e) else os.path.join(base, e)
-                    if os.path.isfile(p):
-                        kept.append(e)
-                    else:
-                        log.warning("Unable to find env config file %s referred in service %s in file %s. Ignoring it.", p, name, path)
-                svc[cu.ENV_FILE] = kept
+                raise ComposeError("Service %s has neither an image nor a build context specified. "
+                                   "At least one must be provided." % name)
+
+
+def _load_file(path, lookup, compose_path):
+    """Interpolate -> Preprocess -> Validate, as libcompose's ``Merge`` /
+    ``parseV2`` does for the main file and for every ``extends: {file: ...}``."""
+    version, raw_services, parsed = _read_raw(path)
+    try:
+        raw_services = interpolate(raw_services, lookup, warn_missing=True)
+    except InterpolationError as e:
+        raise ComposeError(str(e))
+    _prune_env_files(raw_services, compose_path)
+    _validate(raw_services, version)
+    return version, raw_services, parsed
+
+
+class _EnvSlice(tuple):
+    """libcompose ``MaporEqualSlice``: ``environment`` after ``readEnvFile``.
+    A typed slice, so ``merge`` (which only appends ``[]interface{}``) replaces it."""
+
+
+def _environment_slice(env):
+    if isinstance(env, dict):
+        return ["%s=%s" % (k, _scalar_str(v)) if v is not None else str(k) for k, v in env.items()]
+    return _as_list_of_str(env)
+
+
+def _read_env_file(svc, in_file):
+    """libcompose ``readEnvFile``: fold ``env_file`` into ``environment``.
+    Files are read last to first; a line is added unless an existing entry
+    starts with its key (the text up to and including the first ``=``), so
+    explicit ``environment`` entries win, then later files over earlier ones.
+    Lines are taken verbatim (trimmed; blank and ``#`` lines skipped)."""
+    if cu.ENV_FILE not in svc:
+        return svc
+    ef = svc[cu.ENV_FILE]
+    files = [ef] if isinstance(ef, str) else [e for e in (ef or []) if isinstance(e, str)]
+    if not files:
+        return svc
+    env = _environment_slice(svc.get("environment")) if "environment" in svc else []
+    for f in reversed(files):
+        p = f
+        if p.startswith("~/"):
+            p = os.environ.get("HOME", "") + p[1:]
+        if not os.path.isabs(p):
+            p = os.path.join(os.path.dirname(in_file), p)
         try:
-            services.append(_load_service(name, svc, base, version))
+            with open(p, encoding="utf-8", errors="replace") as fh:
+                lines = fh.read().splitlines()
+        except OSError as e:
+            raise ComposeError("Failed to read env file %s: %s" % (p, e))
+        for raw in lines:
+            line = raw.strip()
+            if not line or line.startswith("#"):
+                continue
+            key = line[:line.index("=") + 1] if "=" in line else line
+            if not any(v.startswith(key) for v in env):
+                env.append(line)
+    svc["environment"] = _EnvSlice(env)
+    del svc[cu.ENV_FILE]
+    return svc
+
+
+def _merge_value(existing, value):
+    """libcompose ``merge``: raw lists append, raw maps merge, anything else is replaced."""
+    if type(existing) is list and type(value) is list:
+        return existing + value
+    if isinstance(existing, dict) and isinstance(value, dict):
+        out = dict(existing)
+        out.update(value)
+        return out
+    return value
+
+
+_NO_MERGE = ("links", "volumes_from")
+
+
+def _parse_service(svc, in_file, datas, lookup, compose_path, depth=0):
+    """libcompose ``parseV1``/``parseV2``: env files, then ``extends``.
+    Returns the raw service with ``_file`` naming the file each path-like value
+    is relative to (the extended service's own file for inherited keys)."""
+    if depth > 32:
+        raise ComposeError("extends: circular or too deep reference in %s" % in_file)
+    svc = _read_env_file(dict(svc), in_file)
+    svc.setdefault("_file", {})
+    svc["_file"] = dict(svc["_file"])
+    for k in svc:
+        if k != "_file" and k not in svc["_file"]:
+            svc["_file"][k] = in_file
+    ext = svc.get("extends")
+    if not isinstance(ext, dict):
+        return svc
+    file = _scalar_str(ext.get("file") or "")
+    service = _scalar_str(ext.get("service") or "")
+    if not service:
+        return svc
+    if not file:
+        if service not in datas:
+            raise ComposeError("Failed to find service %s to extend" % service)
+        base = _parse_service(datas[service], in_file, datas, lookup, compose_path, depth + 1)
+    else:
+        if file.startswith("~/"):
+            file = os.environ.get("HOME", "") + file[1:]
+        resolved = file if os.path.isabs(file) else os.path.join(os.path.dirname(in_file), file)
+        _v, base_services, _p = _load_file(resolved, lookup, compose_path)
+        if service not in base_services:
+            raise ComposeError("Failed to find service %s in file %s" % (service, file))
+        base = _parse_service(base_services[service], resolved, base_services, lookup, compose_path, depth + 1)
+    for k in _NO_MERGE:
+        if k in base:
+            raise ComposeError("Cannot extend service '%s' in %s: services with '%s' cannot be extended"
+                               % (service, file or in_file, k))
+    merged = dict(base)
+    files = dict(base["_file"])
+    for k, v in svc.items():
+        if k == "_file":
+            continue
+        merged[k] = _merge_value(merged[k], v) if k in merged else v
+        if not (k in base and type(base[k]) is list and type(v) is list):
+            files[k] = svc["_file"].get(k, in_file)
+    merged["_file"] = files
+    return merged
+
+
+def parse_v2(path):
+    """Parse a v1/v2 compose file the way the reference's libcompose
+    ``project.Parse()`` does (``v1v2.go:93-129``): interpolation (``.env`` then
+    OS env), env-file pruning, validation, then per service ``env_file``
+    folding and ``extends`` resolution (same file or ``file:``, chained).
+    Returns {"version", "project", "services": [...], "networks": {...}}."""
+    lookup = _env_lookup()
+    version, raw_services, parsed = _load_file(path, lookup, path)
+    base = os.path.dirname(os.path.abspath(path))
+    services = []
+    for name, svc in raw_services.items():
+        merged = _parse_service(svc, os.path.abspath(path), raw_services, lookup, path)
+        try:
+            services.append(_load_service(name, merged, base, version))
         except (ValueError, TypeError) as e:  # bad port spec, memory size, ...
             raise ComposeError("Failed to load service %s in %s: %s" % (name, path, e))
     services.sort(key=lambda s: s["name"])
@@ -157,6 +312,11 @@ def _is_url(s):
 
 
 def _load_service(name, d, base, version):
+    files = d.get("_file") or {}
+
+    def base_of(key):
+        f = files.get(key)
+        return os.path.dirname(f) if f else base
     s = {"name": name}
     b = d.get("build")
     ctx, dockerfile = "", ""
@@ -168,7 +328,7 @@ def _load_service(name, d, base, version):
     if version == "" and d.get("dockerfile"):
         dockerfile = _scalar_str(d.get("dockerfile"))
     if ctx and not _is_url(ctx):
-        ctx = _resolve(ctx, base)
+        ctx = _resolve(ctx, base_of("build"))
     s["build_context"], s["build_dockerfile"] = ctx, dockerfile
     s["image"] = _scalar_str(d.get("image") or "")
     s["container_name"] = _scalar_str(d.get("container_name") or "")
@@ -214,7 +374,7 @@ def _load_service(name, d, base, version):
                 vol["access_mode"] = parts[2]
         src = vol["source"]
         if src and src[0] in "./~":
-            vol["source"] = _resolve(src, base)
+            vol["source"] = _resolve(src, base_of("volumes"))
         vols.append(vol)
     s["volumes"] = vols
     return s
