@@ -30,11 +30,13 @@ class Session:
         self._temp = None
 
     def __enter__(self):
+        self._saved_ignore_env = settings.ignore_environment
         self._temp = assets.setup()
         return self
 
     def __exit__(self, *exc):
         assets.cleanup(self._temp)
+        settings.ignore_environment = self._saved_ignore_env
         return False
 
     def _start(self):

@@ -95,10 +95,13 @@ class RegistryCustomizer:
             user_login = "UserName/Password"
             existing = "Use existing pull secret"
             options = [existing, no_auth, user_login]
-            lookup = ir.kubernetes.registry_url if not settings.fixed else registry  # SURVEY 2.13 #13
+            # the reference looks the auth up by the target registry
+            # and names the secret from an empty map value; "fixed" uses the loop's registry
+            lookup = ir.kubernetes.registry_url if not settings.fixed else registry
             if lookup in auths:
-                pull_secrets[registry] = IMAGE_PULL_SECRET_PREFIX + common.make_file_name_compliant(
-                    pull_secrets.get(registry, "") if not settings.fixed else registry)
+                if not settings.fixed:
+                    pull_secrets[registry] = IMAGE_PULL_SECRET_PREFIX + common.make_file_name_compliant(
+                        pull_secrets.get(registry, ""))
                 dauth["auth"] = auths[lookup]
                 options.append(docker_login)
             prob = qa.new_select_problem("[%s] What type of container registry login do you want to use?" % registry,
@@ -110,7 +113,9 @@ class RegistryCustomizer:
             elif auth == existing:
                 prob = qa.new_input_problem("[%s] Enter the name of the pull secret : " % registry,
                                             ["The pull secret should exist in the namespace where you will be deploying the application."], "")
-                pull_secrets[registry] = qaengine.fetch_answer(prob).get_string_answer()
+                name = qaengine.fetch_answer(prob).get_string_answer()
+                if name or not settings.fixed:
+                    pull_secrets[registry] = name
             elif auth != docker_login:
                 prob = qa.new_input_problem("[%s] Enter the container registry username : " % registry,
                                             ["Enter username for container registry login"], "iamapikey")
@@ -126,8 +131,16 @@ class RegistryCustomizer:
                     entry["auth"] = base64.b64encode(("%s:%s" % (dauth["username"], dauth["password"])).encode()).decode()
                 elif settings.fixed and dauth["auth"]:
                     entry["auth"] = dauth["auth"]
-                content = json.dumps({"auths": {ir.kubernetes.registry_url: entry}}, indent="\t").encode()
-                ir.add_storage(irtypes.Storage(name=pull_secrets.get(registry, ""), storage_type=irtypes.PULL_SECRET_KIND,
+                if settings.fixed:
+                    # the Secret is keyed by, and named after, the registry it authenticates
+                    # to; only now is it referenced from imagePullSecrets
+                    secret_name = IMAGE_PULL_SECRET_PREFIX + common.make_file_name_compliant(registry)
+                    pull_secrets[registry] = secret_name
+                    content = json.dumps({"auths": {registry: entry}}, indent="\t").encode()
+                else:
+                    secret_name = pull_secrets.get(registry, "")
+                    content = json.dumps({"auths": {ir.kubernetes.registry_url: entry}}, indent="\t").encode()
+                ir.add_storage(irtypes.Storage(name=secret_name, storage_type=irtypes.PULL_SECRET_KIND,
                                                content={".dockerconfigjson": content}))
         ir.values.registry_namespace = ir.kubernetes.registry_namespace
         ir.values.registry_url = ir.kubernetes.registry_url

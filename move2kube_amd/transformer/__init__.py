@@ -53,7 +53,10 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
         if not c.new_files:
             manualimages.extend(c.image_names)
         log.debug("New Container : %s", c.image_names[0] if c.image_names else "")
-        dockerimages.extend(c.image_names)
+        if c.new_files or not settings.fixed:
+            # the reference also lists manual images in pushimages.sh although
+            # buildimages.sh never builds them; "fixed" leaves them to Manualimages.md
+            dockerimages.extend(c.image_names)
         for rel in sorted(c.new_files):
             wp = os.path.join(cpath, rel)
             d = os.path.dirname(wp)

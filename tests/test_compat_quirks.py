@@ -132,7 +132,7 @@ def test_q5_cf_app_path_joined_onto_manifest_file(tmp_path, mode, monkeypatch):
         assert [s.service_name for s in dockerfile] == ["web"]
 
 
-def _translate(tmp_path, monkeypatch, files, name="q", curate=True):
+def _translate(tmp_path, monkeypatch, files, name="q", curate=True, qacaches=(), ignore_env=True):
     import shutil
     from move2kube_amd import api
     from move2kube_amd.utils import yamlio
@@ -146,7 +146,7 @@ def _translate(tmp_path, monkeypatch, files, name="q", curate=True):
         else:
             (src / rel).parent.mkdir(parents=True, exist_ok=True)
             (src / rel).write_text(text)
-    with api.Session(qaskip=True) as session:
+    with api.Session(qaskip=True, qacaches=qacaches, ignore_env=ignore_env) as session:
         # curate=False keeps the planner's choices (the curator's default cluster is Kubernetes)
         out = session.translate(str(src), str(tmp_path / "out"), name=name, curate=curate)
     objdir = os.path.join(out, name)
@@ -201,32 +201,81 @@ def test_q4_storage_class_for_all_claims(tmp_path, mode, monkeypatch):
     assert classes == ([None, None] if mode == "reference" else ["default", "default"])
 
 
-def test_q13_pull_secret_looked_up_by_registry(tmp_path, mode, monkeypatch):
+Q13_LOGIN_FROM_CONFIG = """apiVersion: move2kube.konveyor.io/v1alpha1
+kind: QACache
+spec:
+  solutions:
+    - description: '[quay.io] What type of container registry login do you want to use?'
+      solution:
+        type: Select
+        answer:
+          - Docker login from config
+      resolved: true
+"""
+
+
+def _q13(tmp_path, monkeypatch, caches=()):
     import base64
     import json
-    from move2kube_amd import api
     cfg = tmp_path / "dockercfg"
     cfg.mkdir()
     (cfg / "config.json").write_text(json.dumps(
         {"auths": {"quay.io": {"auth": base64.b64encode(b"u:p").decode()}}}))
     monkeypatch.setenv("DOCKER_CONFIG", str(cfg))
     monkeypatch.setenv("HOME", str(tmp_path))
-    monkeypatch.setattr(api.Session, "__init__", _session_with_env(api.Session.__init__))
-    objs = _translate(tmp_path, monkeypatch, {"docker-compose.yaml":
-                                              'version: "3.7"\nservices:\n  web:\n    image: quay.io/org/web:1\n'})
-    pod = objs["web-deployment.yaml"]["spec"]["template"]["spec"]
-    # the reference looks the auth up by the target RegistryURL instead of the image's registry,
-    # so a login for quay.io never yields a pull secret for quay.io images
-    secrets = [e["name"] for e in pod.get("imagePullSecrets", [])]
-    assert (secrets == []) == (mode == "reference")
-    if mode == "fixed":
-        assert len(secrets) == 1 and "quay" in secrets[0]
+    return _translate(tmp_path, monkeypatch, {"docker-compose.yaml":
+                                              'version: "3.7"\nservices:\n  web:\n    image: quay.io/org/web:1\n'},
+                      qacaches=caches, ignore_env=False)
 
 
-def _session_with_env(init):
-    def patched(self, qaskip=True, qacaches=(), ignore_env=True):
-        init(self, qaskip=qaskip, qacaches=qacaches, ignore_env=False)
-    return patched
+def _pull_secret_refs_resolve(objs):
+    """Every imagePullSecrets entry names a Secret that is written."""
+    secrets = {o["metadata"]["name"]: o for o in objs.values() if o.get("kind") == "Secret"}
+    refs = []
+    for o in objs.values():
+        pod = ((o.get("spec") or {}).get("template") or {}).get("spec") or {}
+        refs += [e["name"] for e in pod.get("imagePullSecrets", [])]
+    return refs, secrets
+
+
+def test_q13_no_authentication_leaves_no_dangling_pull_secret(tmp_path, mode, monkeypatch):
+    """Default answer "No authentication": no Secret, and (fixed) no reference to one."""
+    objs = _q13(tmp_path, monkeypatch)
+    refs, secrets = _pull_secret_refs_resolve(objs)
+    assert refs == [] and secrets == {}
+
+
+def test_q13_login_from_config_keyed_by_image_registry(tmp_path, mode, monkeypatch):
+    """A docker-config login for quay.io, chosen through a QA cache.  The
+    reference looks the auth up by the target RegistryURL (docker.io), so the
+    option is not offered for quay.io and nothing is emitted; "fixed" emits a
+    Secret whose .dockerconfigjson is keyed by quay.io and references it."""
+    import base64
+    import json
+    cache = tmp_path / "q13cache.yaml"
+    cache.write_text(Q13_LOGIN_FROM_CONFIG)
+    objs = _q13(tmp_path, monkeypatch, caches=[str(cache)])
+    refs, secrets = _pull_secret_refs_resolve(objs)
+    if mode == "reference":
+        assert refs == [] and secrets == {}
+        return
+    assert len(refs) == 1 and "quay" in refs[0]
+    assert set(refs) <= set(secrets)
+    sec = secrets[refs[0]]
+    assert sec["type"] == "kubernetes.io/dockerconfigjson"
+    cfg = json.loads(base64.b64decode(sec["data"][".dockerconfigjson"]))
+    assert list(cfg["auths"]) == ["quay.io"]
+    assert base64.b64decode(cfg["auths"]["quay.io"]["auth"]) == b"u:p"
+
+
+def test_session_restores_ignore_environment():
+    from move2kube_amd import api
+    from move2kube_amd.utils.constants import settings
+    before = settings.ignore_environment
+    with api.Session(ignore_env=not before) as s:
+        s._start()
+        assert settings.ignore_environment == (not before)
+    assert settings.ignore_environment == before
 
 
 def test_q2_q15_manual_cf_app_and_manual_images_readme(tmp_path, mode, monkeypatch):
@@ -245,3 +294,35 @@ def test_q2_q15_manual_cf_app_and_manual_images_readme(tmp_path, mode, monkeypat
     else:
         assert os.path.exists(os.path.join(out, "q", "legacy-deployment.yaml"))
         assert "legacy" in open(readme).read()
+
+
+def test_q2_write_containers_manual_image(tmp_path, mode, caplog):
+    """Quirk #2 directly: a new container without files (a manual image).  The
+    reference hands Manualimages.md the wrong struct, so the template fails,
+    the error is logged and no file is written; "fixed" writes it and keeps the
+    manual image out of pushimages.sh (buildimages.sh never builds it)."""
+    from move2kube_amd import transformer
+    from move2kube_amd.models import ir as irtypes
+    from move2kube_amd.models import plan as plantypes
+    manual = irtypes.new_container(plantypes.MANUAL, "legacy:latest", True)
+    built = irtypes.new_container(plantypes.NEW_DOCKERFILE, "web:latest", True)
+    built.new_files = {"web/Dockerfile.web": "FROM scratch\n", "web/web-docker-build.sh": "docker build .\n"}
+    out = str(tmp_path / "out")
+    from move2kube_amd.utils import log
+    errors = []
+    saved = log.error
+    log.error = lambda *a, **k: errors.append(a[0] % a[1:] if len(a) > 1 else a[0])
+    try:
+        assert transformer.write_containers([manual, built], out, str(tmp_path), "docker.io", "ns") is True
+    finally:
+        log.error = saved
+    readme = os.path.join(out, "Manualimages.md")
+    push = open(os.path.join(out, "pushimages.sh")).read()
+    assert "web:latest" in push
+    if mode == "reference":
+        assert not os.path.exists(readme)
+        assert any("can't evaluate field Images" in e for e in errors)
+        assert "legacy:latest" in push
+    else:
+        assert "legacy:latest" in open(readme).read()
+        assert "legacy:latest" not in push
