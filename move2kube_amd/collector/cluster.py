@@ -1,12 +1,14 @@
 """Target-cluster metadata (reference ``internal/collector/clustercollector.go``).
 
 Storage classes come from ``<kubectl|oc> get sc -o yaml``.  The kind ->
-group/version map is taken from the discovery API first (here: the raw
-``/api`` + ``/apis`` discovery documents fetched with ``kubectl get --raw``,
-i.e. the same kubeconfig client-go would use) and, if that fails, from the
-CLI (``api-resources -o name`` + ``explain``).  Versions are finally ordered
-by the global group policy: ``*.openshift.io``, ``*.k8s.io``, ``apps``,
-``extensions``, other named groups, then the core group.
+group/version map is taken from the discovery API first - one in-process pass
+over ``/api``, ``/apis`` and every group/version document, straight to the
+API server named by the kubeconfig (``kubeapi.py``; a single ``kubectl
+proxy`` process when the kubeconfig needs a credential plugin) - and, if
+that fails, from the CLI (``api-resources -o name`` + ``explain``).
+Versions are finally ordered by the global group policy: ``*.openshift.io``,
+``*.k8s.io``, ``apps``, ``extensions``, other named groups, then the core
+group.
 """
 
 import json
@@ -18,7 +20,7 @@ from ..k8s import scheme
 from ..models import collection
 from ..utils import common, log, yamlio
 from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
-from . import Collector, CommandError, run
+from . import Collector, CommandError, kubeapi, run
 
 GLOBAL_GROUP_ORDER = [r"^.+\.openshift\.io$", r"^.+\.k8s\.io$", r"^apps$", r"^extensions$"]
 
@@ -88,17 +90,14 @@ class ClusterCollector(Collector):
         return names
 
     # -- discovery API -----------------------------------------------------
-    def _raw(self, path):
-        return json.loads(self._run("get", "--raw", path))
-
-    def get_server_groups(self):
+    def get_server_groups(self, client):
         """[(name, preferred_gv, [gv...])] like ``ServerGroups()`` (core group first)."""
         groups = []
-        core = self._raw("/api")
+        core = client.get_json("/api")
         versions = core.get("versions") or []
         if versions:
             groups.append(("", versions[0], list(versions)))
-        for g in self._raw("/apis").get("groups") or []:
+        for g in client.get_json("/apis").get("groups") or []:
             gvs = [v.get("groupVersion", "") for v in g.get("versions") or []]
             pref = (g.get("preferredVersion") or {}).get("groupVersion", gvs[0] if gvs else "")
             groups.append((g.get("name", ""), pref, gvs))
@@ -120,22 +119,26 @@ class ClusterCollector(Collector):
                     gv_list.append(gv)
         return gv_list
 
-    def get_kinds_for_groups(self, groups):
+    def get_kinds_for_groups(self, client, groups):
+        """``ServerGroupsAndResources``: every group/version document, fetched
+        concurrently.  Subresources count too (``deployments/scale`` makes
+        ``Scale`` an apps/v1 kind), as in the reference.  A failed group makes
+        client-go return an error and the reference fall back to the CLI;
+        "fixed" compat keeps the groups that answered."""
+        gvs_all = [gv for _n, _p, gvs in groups for gv in gvs]
+        docs = client.get_many(["/api/" + gv if "/" not in gv else "/apis/" + gv for gv in gvs_all])
         kinds = {}
-        for _name, _pref, gvs in groups:
-            for gv in gvs:
-                path = "/api/" + gv if "/" not in gv else "/apis/" + gv
-                try:
-                    res = self._raw(path)
-                except (CommandError, ValueError) as e:
-                    log.warning("Ignoring group-version [%s]. %s", gv, e)
-                    continue
-                for r in res.get("resources") or []:
-                    if "/" in r.get("name", ""):
-                        continue  # subresources
-                    lst = kinds.setdefault(r.get("kind", ""), [])
-                    if gv not in lst:
-                        lst.append(gv)
+        for gv in gvs_all:
+            res = docs["/api/" + gv if "/" not in gv else "/apis/" + gv]
+            if isinstance(res, Exception):
+                if not settings.fixed:
+                    raise RuntimeError("unable to retrieve the complete list of server APIs: %s" % res)
+                log.warning("Ignoring group-version [%s]. %s", gv, res)
+                continue
+            for r in res.get("resources") or []:
+                lst = kinds.setdefault(r.get("kind", ""), [])
+                if gv not in lst:
+                    lst.append(gv)
         return kinds
 
     def sort_gv_by_preference(self, pref, kinds):
@@ -148,15 +151,17 @@ class ClusterCollector(Collector):
             kinds[kind] = ordered
 
     def collect_using_api(self):
-        if not self.get_cluster_command():
-            raise RuntimeError("no cluster CLI")
-        groups = self.get_server_groups()
-        gv_list = self.get_preferred_resources_using_api(groups)
-        if not gv_list:
-            raise RuntimeError("Failed to retrieve preferred group information from cluster")
-        kinds = self.get_kinds_for_groups(groups)
-        if not kinds:
-            raise RuntimeError("Failed to retrieve <kind, group-version> information from cluster")
+        client = kubeapi.open_client(self.get_cluster_command())
+        try:
+            groups = self.get_server_groups(client)
+            gv_list = self.get_preferred_resources_using_api(groups)
+            if not gv_list:
+                raise RuntimeError("Failed to retrieve preferred group information from cluster")
+            kinds = self.get_kinds_for_groups(client, groups)
+            if not kinds:
+                raise RuntimeError("Failed to retrieve <kind, group-version> information from cluster")
+        finally:
+            client.close()
         self.sort_gv_by_preference(gv_list, kinds)
         return kinds
 

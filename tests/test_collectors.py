@@ -17,6 +17,9 @@ STUBS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "st
 @pytest.fixture
 def stub_path(monkeypatch, tmp_path):
     monkeypatch.setenv("PATH", STUBS + os.pathsep + "/usr/bin:/bin")
+    # never a real cluster: no kubeconfig unless a test writes one
+    monkeypatch.setenv("KUBECONFIG", str(tmp_path / "no-kubeconfig"))
+    monkeypatch.setenv("M2K_STUB_LOG", str(tmp_path / "stub.log"))
     return tmp_path
 
 
@@ -38,6 +41,8 @@ def test_cluster_collector_via_discovery(stub_path):
     assert m["Ingress"] == ["networking.k8s.io/v1", "networking.k8s.io/v1beta1", "extensions/v1beta1"]
     assert m["Route"] == ["route.openshift.io/v1"]
     assert m["Pod"] == ["v1"] and m["Service"] == ["v1"]
+    # subresources count as in client-go's ServerGroupsAndResources
+    assert m["Scale"] == ["apps/v1"]
 
 
 def test_cluster_collector_fixed_mode_strips_context(stub_path):
@@ -102,3 +107,120 @@ def test_collect_orchestrator_filters_by_annotation(stub_path):
     out = stub_path / "m2k_collect"
     collector.collect("", str(out), ["CF"])
     assert sorted(os.listdir(str(out))) == ["cf"]
+
+
+# ---------------------------------------------------------------------------
+# discovery transport: one pass, no process per group/version
+# ---------------------------------------------------------------------------
+
+FAKE_API = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "fake_apiserver.py")
+
+
+class _FakeAPI:
+    def __init__(self, tmp_path, *args):
+        import subprocess
+        import sys
+        self.log = str(tmp_path / "api.log")
+        env = dict(os.environ, M2K_FAKE_API_LOG=self.log)
+        self.p = subprocess.Popen([sys.executable, FAKE_API] + list(args), stdout=subprocess.PIPE, env=env)
+        line = self.p.stdout.readline().decode()
+        self.port = int(line.rsplit(":", 1)[1])
+
+    def requests(self):
+        return open(self.log).read().splitlines() if os.path.exists(self.log) else []
+
+    def stop(self):
+        self.p.terminate()
+        self.p.wait(timeout=10)
+        self.p.stdout.close()
+
+
+def _kubeconfig(path, server, user):
+    import json
+    path.write_text(json.dumps({
+        "apiVersion": "v1", "kind": "Config", "current-context": "c",
+        "contexts": [{"name": "c", "context": {"cluster": "k", "user": "u"}}],
+        "clusters": [{"name": "k", "cluster": server}],
+        "users": [{"name": "u", "user": user}]}))
+    return str(path)
+
+
+def _stub_calls(stub_path):
+    p = stub_path / "stub.log"
+    return p.read_text().splitlines() if p.exists() else []
+
+
+def _collect_map(stub_path, out="out"):
+    ClusterCollector().collect("", str(stub_path / out))
+    (f,) = os.listdir(str(stub_path / out / "clusters"))
+    return _read(str(stub_path / out / "clusters" / f))
+
+
+def test_discovery_direct_from_kubeconfig_spawns_no_process(stub_path, monkeypatch):
+    """Token auth straight to the API server: the only CLI calls are the context
+    name and the storage classes; discovery itself forks nothing, and the
+    result equals the proxy path's."""
+    via_proxy = _collect_map(stub_path, "o1")
+    api = _FakeAPI(stub_path, "--token", "s3cret")
+    try:
+        monkeypatch.setenv("KUBECONFIG", _kubeconfig(stub_path / "kc", {"server": "http://127.0.0.1:%d" % api.port},
+                                                     {"token": "s3cret"}))
+        (stub_path / "stub.log").write_text("")
+        direct = _collect_map(stub_path, "o2")
+    finally:
+        api.stop()
+    assert _stub_calls(stub_path) == ["kubectl config current-context", "kubectl get sc -o yaml"]
+    reqs = api.requests()
+    assert len(reqs) == 2 + 6 and all(r.endswith("Bearer s3cret") for r in reqs)
+    assert direct == via_proxy
+
+
+def test_discovery_over_tls_with_ca_and_client_cert(stub_path, monkeypatch):
+    import base64
+    import shutil
+    import subprocess
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl not available")
+    key, crt = str(stub_path / "k.pem"), str(stub_path / "c.pem")
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", key, "-out", crt,
+                    "-days", "1", "-subj", "/CN=127.0.0.1", "-addext", "subjectAltName=IP:127.0.0.1"],
+                   check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    api = _FakeAPI(stub_path, "--tls", crt, key)
+    try:
+        b64 = lambda p: base64.b64encode(open(p, "rb").read()).decode()  # noqa: E731
+        monkeypatch.setenv("KUBECONFIG", _kubeconfig(
+            stub_path / "kc", {"server": "https://127.0.0.1:%d" % api.port, "certificate-authority-data": b64(crt)},
+            {"client-certificate-data": b64(crt), "client-key-data": b64(key)}))
+        m = _collect_map(stub_path)["spec"]["apiKindVersionMap"]
+    finally:
+        api.stop()
+    assert m["Deployment"] == ["apps/v1", "extensions/v1beta1"]
+    assert not any("proxy" in c for c in _stub_calls(stub_path))
+
+
+def test_discovery_exec_plugin_uses_one_proxy_process(stub_path, monkeypatch):
+    monkeypatch.setenv("KUBECONFIG", _kubeconfig(stub_path / "kc", {"server": "https://example.invalid"},
+                                                 {"exec": {"command": "get-token", "apiVersion": "x"}}))
+    m = _collect_map(stub_path)["spec"]["apiKindVersionMap"]
+    assert m["Route"] == ["route.openshift.io/v1"]
+    calls = _stub_calls(stub_path)
+    assert sum(1 for c in calls if c.startswith("kubectl proxy")) == 1
+    assert not any("--raw" in c for c in calls)
+
+
+def test_discovery_failed_group_falls_back_to_cli_in_reference_mode(stub_path, monkeypatch):
+    """client-go's ServerGroupsAndResources errors when a group fails, so the
+    reference falls back to the CLI; "fixed" keeps the groups that answered."""
+    api = _FakeAPI(stub_path, "--fail", "/apis/route.openshift.io/v1")
+    try:
+        monkeypatch.setenv("KUBECONFIG", _kubeconfig(stub_path / "kc", {"server": "http://127.0.0.1:%d" % api.port}, {}))
+        m = _collect_map(stub_path, "ref")["spec"]["apiKindVersionMap"]
+        assert any(c.startswith("kubectl api-resources") for c in _stub_calls(stub_path))
+        assert "Route" not in m and m["Deployment"] == ["apps/v1"]
+        settings.compat = "fixed"
+        (stub_path / "stub.log").write_text("")
+        m = _collect_map(stub_path, "fixed")["spec"]["apiKindVersionMap"]
+        assert not any(c.startswith("kubectl api-resources") for c in _stub_calls(stub_path))
+        assert "Route" not in m and m["Ingress"][0] == "networking.k8s.io/v1"
+    finally:
+        api.stop()
