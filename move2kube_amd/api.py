@@ -3,10 +3,10 @@ process-global leftovers between runs).  Used by tests, ``bench.py`` and
 embedding applications."""
 
 import os
+import sys
 
 from . import assets, move2kube, qaengine
 from .containerizer import cnb
-from .containerizer.cnb import providers
 from .models import plan as plantypes
 from .utils import sshkeys, yamlio
 from .utils.constants import QA_CACHE_FILE, settings
@@ -16,7 +16,9 @@ def reset_state():
     """Forget engines, caches and provider probes from a previous run."""
     qaengine.reset()
     cnb.reset_cache()
-    providers.reset_providers()
+    providers = sys.modules.get("move2kube_amd.containerizer.cnb.providers")
+    if providers is not None:
+        providers.reset_providers()
     sshkeys.reset()
 
 

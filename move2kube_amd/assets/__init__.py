@@ -14,7 +14,6 @@
 import json
 import os
 import shutil
-import tempfile
 
 from ..utils import log
 from ..utils.constants import ASSETS_DIR, TEMP_DIR_PREFIX, settings
@@ -63,9 +62,21 @@ def _copy_tree(src, dst):
 
 
 def create_assets_data():
-    """Create ``<tmp>/m2kassets`` populated with the detector assets.
+    """Point at the detector assets.
+
+    The reference unpacks its embedded asset tar into a fresh
+    ``<tmp>/m2kassets`` on every run (``internal/common/utils.go:550-582``).
+    The installed package already holds that tree, and nothing writes into it
+    (the runc CNB provider gets its own :func:`scratch_dir`), so it is used in
+    place: ``temp_path`` is this package directory and plans keep the same
+    portable ``m2kassets/...`` paths.  Set ``M2K_UNPACK_ASSETS=1`` to copy into
+    a temp dir like the reference; single-file distributions, which carry the
+    assets as an embedded tar (``make generate``), always unpack.
 
     Returns (assets_path, temp_path)."""
+    if os.path.isdir(ASSETS_SRC) and os.environ.get("M2K_UNPACK_ASSETS", "") in ("", "0"):
+        return ASSETS_SRC, HERE
+    import tempfile
     temp_path = os.path.abspath(settings.temp_path)
     assets_path = os.path.abspath(settings.assets_path)
     try:
@@ -76,12 +87,21 @@ def create_assets_data():
     if os.path.isdir(ASSETS_SRC):
         _copy_tree(ASSETS_SRC, assets_path)
     else:
-        # single-file / zipapp distributions carry the assets as an embedded tar
-        # (``make generate``), like the reference's go:generate'd asset tar
         from ..utils import tarutil
         from . import _embedded_assets  # noqa: F401 - generated module
         tarutil.untar_string(_embedded_assets.TAR, assets_path)
     return assets_path, temp_path
+
+
+_scratch = []
+
+
+def scratch_dir():
+    """A writable per-command temp dir (created on first use, removed by :func:`cleanup`)."""
+    if not _scratch:
+        import tempfile
+        _scratch.append(tempfile.mkdtemp(prefix=TEMP_DIR_PREFIX + "scratch-"))
+    return _scratch[0]
 
 
 def setup():
@@ -93,4 +113,9 @@ def setup():
 
 
 def cleanup(temp_path=None):
-    shutil.rmtree(temp_path or settings.temp_path, ignore_errors=True)
+    temp_path = temp_path or settings.temp_path
+    # never the package's own asset tree (used in place, see create_assets_data)
+    if temp_path and os.path.realpath(temp_path) != os.path.realpath(HERE):
+        shutil.rmtree(temp_path, ignore_errors=True)
+    while _scratch:
+        shutil.rmtree(_scratch.pop(), ignore_errors=True)

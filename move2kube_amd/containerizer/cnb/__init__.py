@@ -8,7 +8,6 @@ from ...models import plan as plantypes
 from ...utils import common
 from ...utils.constants import DEFAULT_SERVICE_PORT
 from ..base import Containerizer, ContainerizerError
-from . import providers
 
 DEFAULT_BUILDERS = ["cloudfoundry/cnb:cflinuxfs3", "gcr.io/buildpacks/builder"]
 
@@ -34,6 +33,7 @@ class CNBContainerizer(Containerizer):
         with _cache_lock:
             if path in _cache:
                 return list(_cache[path])
+        from . import providers  # docker API / podman / pack / runc: only when CNB is probed
         supported = [b for b in self.builders if providers.is_builder_supported(path, b)]
         with _cache_lock:
             _cache[path] = supported
@@ -58,4 +58,5 @@ class CNBContainerizer(Containerizer):
         return container
 
     def get_all_buildpacks(self):
+        from . import providers
         return providers.get_all_buildpacks(self.builders)

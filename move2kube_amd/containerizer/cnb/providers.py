@@ -14,9 +14,7 @@ import io
 import json
 import os
 import shutil
-import socket
 import subprocess
-import tarfile
 import threading
 import urllib.parse
 
@@ -73,6 +71,7 @@ def _UnixHTTPConnection(path, timeout=60):
                 self._path = path
 
             def connect(self):
+                import socket
                 s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
                 s.settimeout(self.timeout)
                 s.connect(self._path)
@@ -121,6 +120,7 @@ class DockerAPIProvider:
 
     def _copy_dir(self, cid, src, dst):
         buf = io.BytesIO()
+        import tarfile
         with tarfile.open(fileobj=buf, mode="w") as tw:
             for root, dirs, files in os.walk(src):
                 dirs.sort()
@@ -332,8 +332,10 @@ class PackProvider:
 class RuncProvider:
     @staticmethod
     def _paths():
-        # resolved at call time (the reference captured AssetsPath at package init - SURVEY 2.13 #11)
-        base = os.path.join(settings.assets_path, "cnb")
+        # resolved at call time (the reference captured AssetsPath at package init -
+        # SURVEY 2.13 #11); a writable scratch dir, the asset tree is used read-only
+        from ... import assets
+        base = os.path.join(assets.scratch_dir(), "cnb")
         return os.path.join(base, "images"), os.path.join(base, "bundles")
 
     def is_available(self):

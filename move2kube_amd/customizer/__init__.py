@@ -5,7 +5,6 @@ PVC, storage classes) -> ingress host/TLS (QA)."""
 import base64
 import json
 import os
-import urllib.parse
 
 from .. import qaengine
 from ..models import ir as irtypes
@@ -53,6 +52,7 @@ class RegistryCustomizer:
             for regurl in sorted(load_docker_auths()):
                 auth = load_docker_auths()[regurl]
                 try:
+                    import urllib.parse
                     u = urllib.parse.urlparse(regurl)
                     if u.netloc:
                         regurl = u.netloc

@@ -3,7 +3,7 @@
 
 import os
 
-from . import collector, customizer, metadata, optimizer, parameterizer, qaengine, transformer
+from . import customizer, metadata, optimizer, parameterizer, qaengine, transformer
 from .ops import native
 from .models import info, qa
 from .models import plan as plantypes
@@ -14,6 +14,7 @@ from .utils.constants import DEFAULT_CLUSTER_TYPE
 
 def collect(input_path, output_path, annotations=()):
     """``Collect`` (collector.go): run the annotation-selected collectors."""
+    from . import collector
     collector.collect(input_path, output_path, list(annotations))
 
 

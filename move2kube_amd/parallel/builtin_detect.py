@@ -18,7 +18,6 @@ detectors report the lexically first one, while ``grep -R`` reports the first
 in readdir order (file-system dependent in the reference too).
 """
 
-import hashlib
 import os
 import re
 
@@ -176,17 +175,24 @@ DETECTORS = {
 }
 
 
-def _sha(path):
+def _read(path):
     with open(path, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()
+        return f.read()
 
 
-_PACKAGED = {}
-for (_rel, _script) in DETECTORS:
-    try:
-        _PACKAGED[(_rel, _script)] = _sha(os.path.join(_ASSETS_SRC, _rel, _script))
-    except OSError:
-        pass
+_MISSING = object()
+_packaged = {}  # (rel, script) -> bytes of the packaged original (read on first use)
+
+
+def _packaged_bytes(key):
+    b = _packaged.get(key)
+    if b is None:
+        try:
+            b = _read(os.path.join(_ASSETS_SRC, key[0], key[1]))
+        except OSError:
+            b = _MISSING
+        _packaged[key] = b
+    return None if b is _MISSING else b
 
 _verified = {}  # (path, mtime_ns, size) -> bool
 
@@ -219,8 +225,10 @@ def _lookup(script_dir, script):
     rel = os.path.relpath(d, assets)
     key = (rel, script)
     fn = DETECTORS.get(key)
-    want = _PACKAGED.get(key)
-    if fn is None or want is None:
+    if fn is None:
+        return None
+    want = _packaged_bytes(key)
+    if want is None:
         return None
     path = os.path.join(d, script)
     try:
@@ -231,7 +239,7 @@ def _lookup(script_dir, script):
     ok = _verified.get(vk)
     if ok is None:
         try:
-            ok = _sha(path) == want
+            ok = _read(path) == want  # byte-identical to the packaged detector
         except OSError:
             ok = False
         _verified[vk] = ok

@@ -13,8 +13,6 @@ are evaluated in-process (:mod:`.builtin_detect`) without spawning anything.
 """
 
 import os
-import subprocess
-from concurrent.futures import ThreadPoolExecutor
 
 from ..ops import native
 from . import builtin_detect
@@ -40,6 +38,7 @@ def _run_py(jobs):
     def one(job):
         script_dir, script, target = job
         try:
+            import subprocess
             p = subprocess.run(["/bin/sh", script, target], cwd=script_dir, stdout=subprocess.PIPE,
                                stdin=subprocess.DEVNULL, timeout=DETECT_TIMEOUT_S)
             return DetectResult(p.returncode, p.stdout.decode("utf-8", "replace"))
@@ -48,6 +47,7 @@ def _run_py(jobs):
             return DetectResult(-1, "")
     if len(jobs) == 1:
         return [one(jobs[0])]
+    from concurrent.futures import ThreadPoolExecutor  # imports logging: keep it off the start-up path
     with ThreadPoolExecutor(max_workers=settings.workers) as ex:
         return list(ex.map(one, jobs))
 

@@ -15,7 +15,6 @@ marshaller + go-yaml emitter (``transformer.go:153-200``).
 
 import os
 import shutil
-import subprocess
 
 from .. import assets
 from ..apiresource.base import GOTYPE
@@ -253,6 +252,7 @@ class K8sTransformer(Transformer):
             log.warning("Unable to find operator-sdk. Skipping operator generation : exec: \"operator-sdk\": "
                         "executable file not found in $PATH")
             return False
+        import subprocess
         opath = os.path.join(basepath, project + "-operator")
         if os.path.exists(opath):
             shutil.rmtree(opath, ignore_errors=True)

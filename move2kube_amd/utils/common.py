@@ -6,7 +6,6 @@ indexed walk shared by every planner instead of the reference's >=8 serial
 the reference (CRC-64/ECMA, FNV-64a, SHA-256 truncation).
 """
 
-import hashlib
 import json
 import os
 import re
@@ -69,6 +68,7 @@ def fnv64a(data):
 
 
 def get_sha256_hash(s):
+    import hashlib  # OpenSSL start-up cost; only long names need it
     return hashlib.sha256(s.encode()).hexdigest()
 
 

@@ -5,10 +5,8 @@ Replaces the reference's go-git calls (``internal/common/utils.go:636-718``):
 tree root, read directly from ``.git/config`` and ``.git/HEAD``.
 """
 
-import configparser
 import os
 import re
-import urllib.parse
 
 from . import fsindex
 
@@ -71,6 +69,7 @@ def _read_config(git_dir):
     if not os.path.exists(cfg) and os.path.exists(common_file):
         with open(common_file) as f:
             cfg = os.path.join(os.path.normpath(os.path.join(git_dir, f.read().strip())), "config")
+    import configparser
     parser = configparser.RawConfigParser(strict=False, allow_no_value=True)
     try:
         with open(cfg) as f:
@@ -127,6 +126,7 @@ def repo_name(path):
             return "", ""
         u = parts[1]
     try:
+        import urllib.parse
         parsed = urllib.parse.urlparse(u)
     except ValueError:
         return "", ""
@@ -145,6 +145,7 @@ def url_hostname(giturl):
     if m and "://" not in giturl:
         return m.group(1)
     try:
+        import urllib.parse
         return urllib.parse.urlparse(giturl).hostname or ""
     except ValueError:
         return ""

@@ -18,11 +18,9 @@ slice, print, printf, println, eq, ne, lt, le, gt, ge, html, js, urlquery,
 call).  Values print with Go ``fmt`` ``%v`` semantics.
 """
 
-import html as _html
 import json
 import math
 import re
-import urllib.parse
 
 from .yamlio import go_format_float
 
@@ -877,6 +875,7 @@ def _printf(fmt, *args):
 
 
 def _html_escape(*args):
+    import html as _html
     return _html.escape(_print(*args), quote=True).replace("&#x27;", "&#39;")
 
 
@@ -894,6 +893,7 @@ def _js_escape(*args):
 
 
 def _urlquery(*args):
+    import urllib.parse
     return urllib.parse.quote_plus(_print(*args))
 
 

@@ -6,53 +6,96 @@ raises :class:`FatalError` (the CLI turns it into exit code 1) instead of
 calling ``os.Exit`` so that the library is usable in-process and in tests.
 """
 
-import logging
 import sys
+import threading
 import time
 
 _START = time.time()
-_LEVEL_NAMES = {
-    logging.DEBUG: "DEBU",
-    logging.INFO: "INFO",
-    logging.WARNING: "WARN",
-    logging.ERROR: "ERRO",
-    logging.CRITICAL: "FATA",
-}
+DEBUG, INFO, WARNING, ERROR, CRITICAL = 10, 20, 30, 40, 50
+_LEVEL_NAMES = {DEBUG: "DEBU", INFO: "INFO", WARNING: "WARN", ERROR: "ERRO", CRITICAL: "FATA"}
 
 
 class FatalError(RuntimeError):
     """Raised where the reference calls ``log.Fatalf``."""
 
 
-class _LogrusFormatter(logging.Formatter):
-    def format(self, record):
-        elapsed = int(record.created - _START)
-        lvl = _LEVEL_NAMES.get(record.levelno, record.levelname[:4])
-        return "%s[%04d] %s" % (lvl, elapsed, record.getMessage())
+class _Logger:
+    """Minimal logrus-style logger (``LEVL[ssss] message`` on stderr).  The
+    stdlib ``logging`` package is not imported: it is a measurable part of a
+    cold CLI start and nothing here needs handlers or hierarchies."""
+
+    def __init__(self):
+        self.level = INFO
+        self.stream = None  # None = the current sys.stderr
+        self._lock = threading.Lock()
+
+    def isEnabledFor(self, level):
+        return level >= self.level
+
+    def setLevel(self, level):
+        self.level = level
+
+    def log(self, level, msg, *args):
+        if level < self.level:
+            return
+        try:
+            text = msg % args if args else msg
+        except (TypeError, ValueError):
+            text = "%s %r" % (msg, args)
+        line = "%s[%04d] %s\n" % (_LEVEL_NAMES.get(level, "INFO"), int(time.time() - _START), text)
+        stream = self.stream or sys.stderr
+        with self._lock:
+            stream.write(line)
+            stream.flush()
+
+    def debug(self, msg, *args):
+        if DEBUG >= self.level:
+            self.log(DEBUG, msg, *args)
+
+    def info(self, msg, *args):
+        if INFO >= self.level:
+            self.log(INFO, msg, *args)
+
+    def warning(self, msg, *args):
+        if WARNING >= self.level:
+            self.log(WARNING, msg, *args)
+
+    def error(self, msg, *args):
+        if ERROR >= self.level:
+            self.log(ERROR, msg, *args)
+
+    def critical(self, msg, *args):
+        self.log(CRITICAL, msg, *args)
 
 
-logger = logging.getLogger("move2kube")
-if not logger.handlers:
-    _h = logging.StreamHandler(sys.stderr)
-    _h.setFormatter(_LogrusFormatter())
-    logger.addHandler(_h)
-    logger.setLevel(logging.INFO)
-    logger.propagate = False
+logger = _Logger()
 
 
 def set_verbose(verbose=True):
-    logger.setLevel(logging.DEBUG if verbose else logging.INFO)
+    logger.setLevel(DEBUG if verbose else INFO)
 
 
 def set_quiet():
-    logger.setLevel(logging.ERROR)
+    logger.setLevel(ERROR)
 
 
-debug = logger.debug
-info = logger.info
-warning = logger.warning
-warn = logger.warning
-error = logger.error
+def debug(msg, *args):
+    logger.debug(msg, *args)
+
+
+def info(msg, *args):
+    logger.info(msg, *args)
+
+
+def warning(msg, *args):
+    logger.warning(msg, *args)
+
+
+warn = warning
+
+
+def error(msg, *args):
+    logger.error(msg, *args)
 
 
 def fatal(msg, *args):

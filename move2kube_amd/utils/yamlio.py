@@ -25,14 +25,21 @@ import math
 import re
 import threading
 
-import yaml
+# PyYAML is imported on the first parse (``_lz()``), not at start-up: a CLI
+# run over a source tree without YAML files never pays for it.
 
 __all__ = [
     "GoMap", "dump", "dumps_k8s", "load", "load_raw", "load_all", "go_key_sorted",
     "YAMLError",
 ]
 
-YAMLError = yaml.YAMLError
+
+def __getattr__(name):
+    # ``except yamlio.YAMLError`` only evaluates the name when an exception
+    # reaches the clause, i.e. after a parse has imported PyYAML
+    if name == "YAMLError":
+        return _lz().yaml.YAMLError
+    raise AttributeError(name)
 
 
 class GoMap(dict):
@@ -579,19 +586,6 @@ def dumps_k8s(obj):
 # Loading
 # ---------------------------------------------------------------------------
 
-_BaseLoader = getattr(yaml, "CSafeLoader", yaml.SafeLoader)
-
-
-def _make_loader(name, keep_resolvers):
-    cls = type(name, (_BaseLoader,), {})
-    cls.yaml_implicit_resolvers = {}
-    for ch, resolvers in yaml.SafeLoader.yaml_implicit_resolvers.items():
-        kept = [(tag, rx) for tag, rx in resolvers if tag in keep_resolvers]
-        if kept:
-            cls.yaml_implicit_resolvers[ch] = kept
-    return cls
-
-
 _INT64_MIN, _INT64_MAX, _UINT64_MAX = -(1 << 63), (1 << 63) - 1, (1 << 64) - 1
 _DOT_FLOAT = re.compile(r"^\.[0-9][0-9_]*(?:[eE][-+]?[0-9]+)?$")
 
@@ -649,23 +643,6 @@ _GONUM_TAG = "tag:move2kube:go-number"
 _GONUM_FIRST = re.compile(r"^[-+0-9.]")
 
 
-def _add_go_scalars(cls, bools):
-    cls.add_implicit_resolver("tag:yaml.org,2002:bool", re.compile("^(?:" + "|".join(bools) + ")$"),
-                              sorted({b[0] for b in bools}))
-    cls.add_implicit_resolver(_GONUM_TAG, _GONUM_FIRST, list("-+0123456789."))
-    cls.add_constructor(_GONUM_TAG, _construct_go_number)
-
-
-# go-yaml v3 into interface{}: bools are only true/false, no timestamps (kept
-# as strings for interface{} targets), go-yaml's int/float rules.
-_TypedLoader = _make_loader("_TypedLoader", {"tag:yaml.org,2002:null", "tag:yaml.org,2002:merge"})
-_add_go_scalars(_TypedLoader, ["true", "True", "TRUE", "false", "False", "FALSE"])
-
-# go-yaml v2 (what docker/cli's compose v3 loader and libcompose parse compose
-# files with): v3's rules plus the YAML 1.1 y/yes/on and n/no/off bools.
-_V2Loader = _make_loader("_V2Loader", {"tag:yaml.org,2002:null", "tag:yaml.org,2002:merge"})
-_add_go_scalars(_V2Loader, ["y", "Y", "yes", "Yes", "YES", "true", "True", "TRUE", "on", "On", "ON",
-                            "n", "N", "no", "No", "NO", "false", "False", "FALSE", "off", "Off", "OFF"])
 _TRUE_WORDS = {"y", "Y", "yes", "Yes", "YES", "true", "True", "TRUE", "on", "On", "ON"}
 
 
@@ -673,20 +650,62 @@ def _construct_v2_bool(loader, node):
     return node.value in _TRUE_WORDS
 
 
-_V2Loader.add_constructor("tag:yaml.org,2002:bool", _construct_v2_bool)
-
-# Every scalar is kept as its source text (what go-yaml does when decoding a
-# scalar into a Go string field); only nulls resolve.
-_RawLoader = _make_loader("_RawLoader", {"tag:yaml.org,2002:null"})
-
-
 def _construct_raw_scalar(loader, node):
     return node.value
 
 
-for _tag in ("tag:yaml.org,2002:int", "tag:yaml.org,2002:float", "tag:yaml.org,2002:bool",
-             "tag:yaml.org,2002:timestamp"):
-    _RawLoader.add_constructor(_tag, _construct_raw_scalar)
+class _Loaders:
+    """PyYAML plus the three go-yaml flavoured loaders, built once."""
+
+    def __init__(self):
+        import yaml
+        self.yaml = yaml
+        base = getattr(yaml, "CSafeLoader", yaml.SafeLoader)
+
+        def make(name, keep_resolvers):
+            cls = type(name, (base,), {})
+            cls.yaml_implicit_resolvers = {}
+            for ch, resolvers in yaml.SafeLoader.yaml_implicit_resolvers.items():
+                kept = [(tag, rx) for tag, rx in resolvers if tag in keep_resolvers]
+                if kept:
+                    cls.yaml_implicit_resolvers[ch] = kept
+            return cls
+
+        def go_scalars(cls, bools):
+            cls.add_implicit_resolver("tag:yaml.org,2002:bool", re.compile("^(?:" + "|".join(bools) + ")$"),
+                                      sorted({b[0] for b in bools}))
+            cls.add_implicit_resolver(_GONUM_TAG, _GONUM_FIRST, list("-+0123456789."))
+            cls.add_constructor(_GONUM_TAG, _construct_go_number)
+
+        # go-yaml v3 into interface{}: bools are only true/false, no timestamps
+        # (kept as strings for interface{} targets), go-yaml's int/float rules.
+        self.typed = make("_TypedLoader", {"tag:yaml.org,2002:null", "tag:yaml.org,2002:merge"})
+        go_scalars(self.typed, ["true", "True", "TRUE", "false", "False", "FALSE"])
+        # go-yaml v2 (what docker/cli's compose v3 loader and libcompose parse
+        # compose files with): v3's rules plus the YAML 1.1 y/yes/on, n/no/off bools.
+        self.v2 = make("_V2Loader", {"tag:yaml.org,2002:null", "tag:yaml.org,2002:merge"})
+        go_scalars(self.v2, ["y", "Y", "yes", "Yes", "YES", "true", "True", "TRUE", "on", "On", "ON",
+                             "n", "N", "no", "No", "NO", "false", "False", "FALSE", "off", "Off", "OFF"])
+        self.v2.add_constructor("tag:yaml.org,2002:bool", _construct_v2_bool)
+        # Every scalar is kept as its source text (what go-yaml does when decoding
+        # a scalar into a Go string field); only nulls resolve.
+        self.raw = make("_RawLoader", {"tag:yaml.org,2002:null"})
+        for tag in ("tag:yaml.org,2002:int", "tag:yaml.org,2002:float", "tag:yaml.org,2002:bool",
+                    "tag:yaml.org,2002:timestamp"):
+            self.raw.add_constructor(tag, _construct_raw_scalar)
+
+
+_loaders = None
+_loaders_lock = threading.Lock()
+
+
+def _lz():
+    global _loaders
+    if _loaders is None:
+        with _loaders_lock:
+            if _loaders is None:
+                _loaders = _Loaders()
+    return _loaders
 
 
 # Command-scoped parse memo.  Every planner/loader of the reference decodes
@@ -740,7 +759,7 @@ def _memoized(kind, text, parse):
     if hit is _MISS:
         try:
             hit = (True, parse(text))
-        except yaml.YAMLError as e:
+        except _lz().yaml.YAMLError as e:
             hit = (False, e)
         memo[key] = hit
     ok, val = hit
@@ -757,11 +776,11 @@ _MISS = object()
 
 def load(text):
     """Decode like go-yaml v3 into ``interface{}``."""
-    return _memoized("typed", text, lambda t: yaml.load(t, Loader=_TypedLoader))
+    return _memoized("typed", text, lambda t: _lz().yaml.load(t, Loader=_lz().typed))
 
 
 def load_all(text):
-    return _memoized("typed*", text, lambda t: list(yaml.load_all(t, Loader=_TypedLoader)))
+    return _memoized("typed*", text, lambda t: list(_lz().yaml.load_all(t, Loader=_lz().typed)))
 
 
 _V2_ONLY_WORDS = re.compile(r"\b(?:[yYnN]|yes|Yes|YES|no|No|NO|on|On|ON|off|Off|OFF)\b")
@@ -773,15 +792,15 @@ def load_v2(text):
     not contain one anywhere shares the v3 parse (and its memo entry)."""
     if isinstance(text, str) and not _V2_ONLY_WORDS.search(text):
         return load(text)
-    return _memoized("typed-v2", text, lambda t: yaml.load(t, Loader=_V2Loader))
+    return _memoized("typed-v2", text, lambda t: _lz().yaml.load(t, Loader=_lz().v2))
 
 
 def load_all_v2(text):
     if isinstance(text, str) and not _V2_ONLY_WORDS.search(text):
         return load_all(text)
-    return _memoized("typed-v2*", text, lambda t: list(yaml.load_all(t, Loader=_V2Loader)))
+    return _memoized("typed-v2*", text, lambda t: list(_lz().yaml.load_all(t, Loader=_lz().v2)))
 
 
 def load_raw(text):
     """Decode keeping scalars as raw strings (for typed struct decoding)."""
-    return _memoized("raw", text, lambda t: yaml.load(t, Loader=_RawLoader))
+    return _memoized("raw", text, lambda t: _lz().yaml.load(t, Loader=_lz().raw))

@@ -41,10 +41,12 @@ def _fresh_state():
 
 
 @pytest.fixture
-def assets_dir():
-    """Unpacked m2kassets (like every CLI command does at start-up)."""
+def assets_dir(monkeypatch):
+    """A private unpacked copy of m2kassets (tests may edit detectors; the CLI
+    itself uses the packaged tree read-only)."""
     from move2kube_amd import assets
     from move2kube_amd.utils.constants import settings
+    monkeypatch.setenv("M2K_UNPACK_ASSETS", "1")
     tmp = assets.setup()
     yield settings.assets_path
     assets.cleanup(tmp)

@@ -136,3 +136,22 @@ def test_detectors_match_reference_scripts(tmp_path, assets_dir):
             if (rc == 0) != (a.code == 0) or (rc == 0 and out != a.stdout)]
     assert mism == []
     assert sum(1 for rc, _ in ref if rc == 0) > 20  # the corpus really exercises the detectors
+
+
+def test_packaged_assets_used_in_place_and_never_removed(tmp_path):
+    """Without M2K_UNPACK_ASSETS the packaged detector tree is used read-only
+    (no per-run copy); cleanup never deletes it and plans keep m2kassets/ paths."""
+    from move2kube_amd import assets
+    from move2kube_amd.utils.constants import ASSETS_DIR, settings
+    saved = (settings.temp_path, settings.assets_path)
+    try:
+        tmp = assets.setup()
+        assert settings.assets_path == assets.ASSETS_SRC
+        assert os.path.relpath(settings.assets_path, settings.temp_path) == ASSETS_DIR
+        scratch = assets.scratch_dir()
+        assert os.path.isdir(scratch) and not scratch.startswith(assets.HERE)
+        assets.cleanup(tmp)
+        assert os.path.isfile(os.path.join(assets.ASSETS_SRC, "dockerfiles", "nodejs", "m2kdfdetect.sh"))
+        assert not os.path.exists(scratch)
+    finally:
+        settings.temp_path, settings.assets_path = saved
