@@ -186,15 +186,53 @@ def _to_ir(p):
     return ir
 
 
+def _remove_output(outpath):
+    """``os.RemoveAll(out)`` (translator.go:64).  The old tree is renamed out of
+    the way (one syscall) and deleted on a thread - the native delete releases
+    the GIL - while the new artifacts are generated; :func:`_emit` joins it
+    before returning, so nothing is left behind.  Falls back to a synchronous
+    delete when the rename is not possible."""
+    import threading
+    parent, base = os.path.split(os.path.abspath(outpath))
+    trash = os.path.join(parent, ".%s.m2k-old-%d-%d" % (base, os.getpid(), threading.get_ident()))
+    try:
+        if os.path.lexists(trash):
+            native.remove_tree(trash)
+        os.rename(outpath, trash)
+    except OSError:
+        native.remove_tree(outpath)
+        return None
+    errors = []
+
+    def work():
+        try:
+            native.remove_tree(trash)
+        except OSError as e:
+            errors.append(e)
+    t = threading.Thread(target=work, name="m2k-remove-old-output", daemon=True)
+    t.start()
+    return t, errors
+
+
 def _emit(p, ir, outpath, qadisablecli):
+    remover = None
     if os.path.lexists(outpath):
         qaengine.before_remove(outpath)
         try:
-            native.remove_tree(outpath)
+            remover = _remove_output(outpath)
         except OSError as e:
             log.error("Failed to remove the existing file/directory at the output path %r Error: %r", outpath, str(e))
             log.error("Anything in the output path will get overwritten.")
+    try:
+        _emit_artifacts(p, ir, outpath, qadisablecli)
+    finally:
+        if remover is not None:
+            remover[0].join()
+            for e in remover[1]:
+                log.warning("Failed to remove the previous output: %s", e)
 
+
+def _emit_artifacts(p, ir, outpath, qadisablecli):
     dct = transformer.ComposeTransformer()
     try:
         with trace.span("ComposeTransformer", "transform"):

@@ -66,3 +66,19 @@ def test_translate_is_repeatable_in_process(samples_copy, tmp_path):
         o1 = s.translate(samples_copy, str(tmp_path / "o1"), name="samples")
         o2 = s.translate(samples_copy, str(tmp_path / "o2"), name="samples")
     assert _diff(o1, o2) == []
+
+
+def test_retranslate_replaces_output_and_leaves_nothing_behind(tmp_path):
+    """The previous output tree is removed (RemoveAll, translator.go:64) - on a
+    background thread that is joined before translate returns."""
+    src = tmp_path / "nodejs"
+    shutil.copytree(os.path.join(ROOT, "samples", "nodejs"), str(src))
+    outdir = tmp_path / "out"
+    with api.Session() as s:
+        out = s.translate(str(src), str(outdir), name="p")
+        stale = os.path.join(out, "p", "stale-file.yaml")
+        with open(stale, "w") as f:
+            f.write("x")
+        s.translate(str(src), str(outdir), name="p")
+    assert not os.path.exists(stale)
+    assert sorted(os.listdir(str(outdir))) == ["p"]
