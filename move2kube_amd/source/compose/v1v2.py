@@ -283,6 +283,7 @@ def parse_v2(path):
             raise ComposeError("Failed to load service %s in %s: %s" % (name, path, e))
     services.sort(key=lambda s: s["name"])
     networks = {}
+    project = _project_name(base)
     if version:
         nets = parsed.get("networks") or {}
         if not isinstance(nets, dict):
@@ -295,8 +296,39 @@ def parse_v2(path):
             if external and isinstance(ext, dict) and ext.get("name"):
                 real = ext["name"]
             networks[nname] = {"external": external, "real": real}
-    return {"version": version, "project": _normalize_project_name(os.path.basename(base)),
-            "services": services, "networks": networks}
+        _consolidate_volume_names(parsed.get("volumes"), services, project)
+    return {"version": version, "project": project, "services": services, "networks": networks}
+
+
+def _project_name(base):
+    """libcompose ``lookupProjectName`` + ``normalizeName``: ``COMPOSE_PROJECT_NAME``,
+    else the compose file's directory name; lower-cased, ``[^a-z0-9]`` dropped."""
+    return _normalize_project_name(os.environ.get("COMPOSE_PROJECT_NAME") or os.path.basename(base))
+
+
+def _consolidate_volume_names(vols, services, project):
+    """libcompose ``Project.handleVolumeConfig``: a named volume declared in the
+    top-level ``volumes:`` becomes ``<project>_<name>``, or its ``external.name``
+    when external; a declaration without a body (``name:``) is left alone.
+    Parity unpinned: this follows libcompose's project loader, which is not in
+    the reference tree (tests/golden/reference/DEVIATIONS.md §4)."""
+    if not isinstance(vols, dict):
+        return
+    renames = {}
+    for vname, spec in vols.items():
+        if not isinstance(spec, dict):
+            continue
+        ext = spec.get("external")
+        if ext:
+            if isinstance(ext, dict) and ext.get("name"):
+                renames[vname] = _scalar_str(ext["name"])
+        else:
+            renames[vname] = "%s_%s" % (project, vname)
+    for s in services:
+        for v in s["volumes"]:
+            src = v["source"]
+            if src and src[0] not in "./~" and src in renames:
+                v["source"] = renames[src]
 
 
 def _resolve(p, base):

@@ -22,7 +22,7 @@ from ..apiresourceset import K8sAPIResourceSet, KnativeAPIResourceSet, TektonAPI
 from ..k8s import convert, schema
 from ..ops import native
 from ..models import plan as plantypes
-from ..utils import common, log, yamlio
+from ..utils import common, log, trace, yamlio
 from ..utils.constants import (DEFAULT_DIRECTORY_PERMISSION, DEFAULT_EXECUTABLE_PERMISSION, DEFAULT_FILE_PERMISSION,
                                EXPOSE_SELECTOR, settings)
 
@@ -259,9 +259,10 @@ class K8sTransformer(Transformer):
         _mkdir(opath)
         chart = os.path.abspath(os.path.join(basepath, project))
         try:
-            p = subprocess.run([sdk, "init", "--plugins=helm", "--helm-chart=" + chart, "--domain=io",
-                                "--group=" + project, "--version=v1alpha1"], cwd=opath, stdout=subprocess.PIPE,
-                               stderr=subprocess.PIPE, stdin=subprocess.DEVNULL, timeout=600)
+            with trace.span("operator-sdk init (external tool)", "external"):
+                p = subprocess.run([sdk, "init", "--plugins=helm", "--helm-chart=" + chart, "--domain=io",
+                                    "--group=" + project, "--version=v1alpha1"], cwd=opath, stdout=subprocess.PIPE,
+                                   stderr=subprocess.PIPE, stdin=subprocess.DEVNULL, timeout=600)
         except (OSError, subprocess.SubprocessError) as e:
             log.warning("Error during operator creation : %s", e)
             return False

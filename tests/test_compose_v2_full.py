@@ -4,7 +4,8 @@ container name lower-casing, entrypoint/command, ``k=v`` / ``k:v`` / bare env,
 (ignored), capabilities, group_add (never attached in the reference),
 stop_grace_period, mem_limit, unless-stopped, networks (libcompose real
 names), tmpfs, bind volumes (hostPath ``vol<fnv64a>``, read-only) and named
-volumes (PVC + RWX/ROX storage)."""
+volumes (PVC + RWX/ROX storage; libcompose prefixes top-level declared ones
+with the project name)."""
 
 import os
 import shutil
@@ -47,20 +48,21 @@ def test_compose_v2_full(tmp_path, monkeypatch):
     assert c["volumeMounts"] == [
         {"mountPath": "/scratch", "name": "app-tmpfs-0"},
         {"mountPath": "/var/log/app", "name": vol, "readOnly": True},
-        {"mountPath": "/data", "name": "appdata"},
-        {"mountPath": "/shared", "name": "shared", "readOnly": True},
+        {"mountPath": "/data", "name": "proj_appdata"},
+        {"mountPath": "/shared", "name": "proj_shared", "readOnly": True},
     ]
     assert pod["volumes"] == [
         {"emptyDir": {"medium": "Memory"}, "name": "app-tmpfs-0"},
         {"hostPath": {"path": logs}, "name": vol},
-        {"name": "appdata", "persistentVolumeClaim": {"claimName": "appdata"}},
-        {"name": "shared", "persistentVolumeClaim": {"claimName": "shared", "readOnly": True}},
+        {"name": "proj_appdata", "persistentVolumeClaim": {"claimName": "proj_appdata"}},
+        {"name": "proj_shared", "persistentVolumeClaim": {"claimName": "proj_shared", "readOnly": True}},
     ]
     svc = objs["app-service.yaml"]
     assert [(p["port"], p["targetPort"]) for p in svc["spec"]["ports"]] == [(8001, 8001), (9000, 90), (3000, 3000),
                                                                            (4000, 4000)]
-    assert objs["appdata-persistentvolumeclaim.yaml"]["spec"]["accessModes"] == ["ReadWriteMany"]
-    assert objs["shared-persistentvolumeclaim.yaml"]["spec"]["accessModes"] == ["ReadOnlyMany"]
+    # named volumes declared at the top level get libcompose's project prefix
+    assert objs["proj_appdata-persistentvolumeclaim.yaml"]["spec"]["accessModes"] == ["ReadWriteMany"]
+    assert objs["proj_shared-persistentvolumeclaim.yaml"]["spec"]["accessModes"] == ["ReadOnlyMany"]
     assert objs["proj_backend-networkpolicy.yaml"]["metadata"]["name"] == "proj_backend"
 
 
@@ -224,3 +226,19 @@ def test_v2_extends_build_context_plans_reuse_dockerfile(tmp_path):
     reuse_df = [o for o in opts if o.container_build_type == plantypes.REUSE_DOCKERFILE and o.service_name == "web"]
     assert len(reuse_df) == 1
     assert reuse_df[0].target_options == [os.path.join(root, "sub", "app", "Dockerfile")]
+
+
+def test_v2_named_volume_names(tmp_path, monkeypatch):
+    """handleVolumeConfig: declared with a body -> <project>_<name>; external
+    with a name -> that name; external without, bare declaration, or not
+    declared -> unchanged.  COMPOSE_PROJECT_NAME overrides the directory name."""
+    root = str(tmp_path / "My-App")
+    _write(root, {"docker-compose.yml": 'version: "2"\nservices:\n  s:\n    image: x\n    volumes:\n'
+                                        '      - a:/a\n      - b:/b\n      - c:/c\n      - d:/d\n      - e:/e\n'
+                                        '      - ./f:/f\n'
+                                        'volumes:\n  a: {driver: local}\n  b:\n    external:\n      name: real-b\n'
+                                        '  c: {external: true}\n  d:\n'})
+    srcs = [v["source"] for v in _v2_services(root)["s"]["volumes"]]
+    assert srcs == ["myapp_a", "real-b", "c", "d", "e", os.path.join(root, "f")]
+    monkeypatch.setenv("COMPOSE_PROJECT_NAME", "Other_Name")
+    assert _v2_services(root)["s"]["volumes"][0]["source"] == "othername_a"
