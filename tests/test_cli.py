@@ -136,3 +136,28 @@ def test_version(capsys):
 def test_no_command_prints_help(capsys):
     assert cli.main([]) == 0
     assert "translate" in capsys.readouterr().out
+
+
+def test_two_step_flow_matches_one_step_on_reference_samples(tmp_path, monkeypatch):
+    """USAGE.md's two flows on the reference's samples/: ``translate -s src``
+    (plan + curate inline) and ``plan -s src`` then ``translate`` (the plan is
+    used uncurated, translate.go:151-172).  With default answers both write
+    the same artifacts; only the QA cache (no curation questions) and
+    copysources.sh (output location relative to the sources) differ."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+    import refconfigs
+    monkeypatch.setenv("M2K_NO_NETWORK", "1")
+    monkeypatch.setenv("M2K_DISABLE_CNB", "1")
+    monkeypatch.setenv("HOME", str(tmp_path))
+    shutil.copytree(os.path.join(ROOT, "samples"), str(tmp_path / "samples"))
+    monkeypatch.chdir(tmp_path)
+    assert cli.main(["translate", "-s", "samples", "--qaskip", "-o", "one"]) == 0
+    assert cli.main(["plan", "-s", "samples"]) == 0
+    assert cli.main(["translate", "--qaskip"]) == 0
+    diff = refconfigs.diff_files(str(tmp_path / "myproject"), str(tmp_path / "one" / "myproject"))
+    assert diff == ["copysources.sh", "m2kqacache.yaml"]
+    two = yamlio.load(open(str(tmp_path / "myproject" / "m2kqacache.yaml")).read())
+    descs = [s["description"] for s in two["spec"]["solutions"]]
+    assert "Select all services that are needed:" not in descs
+    assert "Select all services that should be exposed:" in descs
