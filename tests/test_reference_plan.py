@@ -82,3 +82,27 @@ def test_create_plan_for_reference_nodejs_sample(tmp_path, monkeypatch):
     for name in want.services:
         want.services[name] = [s for s in want.services[name] if s.container_build_type != plantypes.CNB]
     assert _dump(actual) == _dump(want)
+
+
+def test_create_plan_for_reference_nodejs_sample_with_cnb(tmp_path, monkeypatch):
+    """The whole fixture, CNB option included: the ``podman`` stand-in
+    (tests/fixtures/configs/bin) answers the reference's container-runtime
+    provider (containerruntimeprovider.go) the way a machine with podman and
+    both builder images would, so both builders support the nodejs sample."""
+    from move2kube_amd.containerizer import cnb
+    cwd = tmp_path / "internal" / "move2kube"
+    cwd.mkdir(parents=True)
+    shutil.copytree(ref_path("samples", "nodejs"), str(tmp_path / "samples" / "nodejs"))
+    monkeypatch.chdir(cwd)
+    stubs = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "configs", "bin")
+    monkeypatch.setenv("PATH", stubs + os.pathsep + os.environ.get("PATH", ""))
+    monkeypatch.setenv("M2K_DISABLE_CNB", "0")
+    cnb.reset_cache()
+    with api.Session() as s:
+        want = plantypes.read_plan(ref_path("internal", "move2kube", "testdata", "expectedplanfornodejsapp.yaml"))
+        actual = s.plan(os.path.abspath("../../samples/nodejs"), "nodejs-app")
+    for services in actual.services.values():
+        for svc in services:
+            svc.repo_info = plantypes.RepoInfo()
+    assert [s.container_build_type for s in actual.services["nodejs"]] == ["NewDockerfile", "S2I", "CNB"]
+    assert _dump(actual) == _dump(want)
