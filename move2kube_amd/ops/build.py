@@ -93,6 +93,27 @@ def build_all(force=False):
     return outs
 
 
+def build_report(force=True):
+    """Build every native target and describe what happened: one JSON-able
+    dict per target with whether it was compiled in this call, the wall time
+    and the output's size and SHA-256 (``__graft_entry__.build`` prints it)."""
+    import hashlib
+    import time
+    report = []
+    for name, fn, target in (("_m2k_native (g++, C++17/pybind11)", build_native, native_target()),
+                             ("libm2k_ed_hip (hipcc --offload-arch=gfx950)", build_hip, hip_target())):
+        before = os.path.getmtime(target) if os.path.exists(target) else None
+        t0 = time.perf_counter()
+        out = fn(force)
+        dt = time.perf_counter() - t0
+        with open(out, "rb") as f:
+            digest = hashlib.sha256(f.read()).hexdigest()
+        report.append({"target": name, "path": os.path.relpath(out, os.path.dirname(os.path.dirname(HERE))),
+                       "compiled": before is None or os.path.getmtime(out) != before,
+                       "seconds": round(dt, 2), "bytes": os.path.getsize(out), "sha256": digest})
+    return report
+
+
 if __name__ == "__main__":
     force = "--force" in sys.argv
     for o in build_all(force):
