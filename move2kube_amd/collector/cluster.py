@@ -20,7 +20,7 @@ from ..k8s import scheme
 from ..models import collection
 from ..utils import common, log, yamlio
 from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
-from . import Collector, CommandError, kubeapi, run
+from . import Collector, CommandError, run
 
 GLOBAL_GROUP_ORDER = [r"^.+\.openshift\.io$", r"^.+\.k8s\.io$", r"^apps$", r"^extensions$"]
 
@@ -151,6 +151,7 @@ class ClusterCollector(Collector):
             kinds[kind] = ordered
 
     def collect_using_api(self):
+        from . import kubeapi  # http.client/ssl: only when the k8s collector runs
         client = kubeapi.open_client(self.get_cluster_command())
         try:
             groups = self.get_server_groups(client)

@@ -40,7 +40,8 @@ def _run(cmd):
     subprocess.run(cmd, check=True)
 
 
-NATIVE_SOURCES = [os.path.join(CSRC, "m2k_native.cpp"), os.path.join(CSRC, "yaml_emit.cpp")]
+NATIVE_SOURCES = [os.path.join(CSRC, "m2k_native.cpp"), os.path.join(CSRC, "yaml_emit.cpp"),
+                  os.path.join(CSRC, "yaml_parse.cpp")]
 SANITIZERS = {"address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"],
               "thread": ["-fsanitize=thread"]}
 

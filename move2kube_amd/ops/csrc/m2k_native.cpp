@@ -514,14 +514,11 @@ std::tuple<py::bytes, py::array_t<int64_t>, int64_t> pack_strings(const py::list
 }
 
 // For every query: (first index of the minimum distance, that distance); (-1, -1) without options.
-std::pair<py::array_t<int32_t>, py::array_t<int32_t>> closest_batch(const py::list &as_list, const py::list &bs_list,
-                                                                    int nthreads) {
-  const std::vector<std::string_view> as = views_of(as_list), bs = views_of(bs_list);
+// Runs without the GIL; pi/pd have nb entries.
+static void closest_core(const std::vector<std::string_view> &as, const std::vector<std::string_view> &bs,
+                         int nthreads, int32_t *pi, int32_t *pd) {
   const size_t na = as.size(), nb = bs.size();
-  py::array_t<int32_t> idx(nb), dist(nb);
-  int32_t *pi = idx.mutable_data(), *pd = dist.mutable_data();
   {
-    py::gil_scoped_release nogil;
     const int nt = threads_for(na * nb, nthreads);
     std::vector<QueryMasks> qm(nb);
     for (size_t j = 0; j < nb; j++) qm[j] = make_masks(bs[j]);
@@ -570,7 +567,35 @@ std::pair<py::array_t<int32_t>, py::array_t<int32_t>> closest_batch(const py::li
       }
     }
   }
+}
+
+std::pair<py::array_t<int32_t>, py::array_t<int32_t>> closest_batch(const py::list &as_list, const py::list &bs_list,
+                                                                    int nthreads) {
+  const std::vector<std::string_view> as = views_of(as_list), bs = views_of(bs_list);
+  py::array_t<int32_t> idx(bs.size()), dist(bs.size());
+  int32_t *pi = idx.mutable_data(), *pd = dist.mutable_data();
+  {
+    py::gil_scoped_release nogil;
+    closest_core(as, bs, nthreads, pi, pd);
+  }
   return {idx, dist};
+}
+
+// Same as closest_batch with plain lists: the CLI's handful of fuzzy matches
+// (collect -a cf) then never imports numpy, which costs more than the matching.
+std::pair<py::list, py::list> closest_list(const py::list &as_list, const py::list &bs_list, int nthreads) {
+  const std::vector<std::string_view> as = views_of(as_list), bs = views_of(bs_list);
+  std::vector<int32_t> vi(bs.size()), vd(bs.size());
+  {
+    py::gil_scoped_release nogil;
+    closest_core(as, bs, nthreads, vi.data(), vd.data());
+  }
+  py::list li(bs.size()), ld(bs.size());
+  for (size_t j = 0; j < bs.size(); j++) {
+    li[j] = py::int_(vi[j]);
+    ld[j] = py::int_(vd[j]);
+  }
+  return {li, ld};
 }
 
 // ----------------------------------------------------------------------------
@@ -834,6 +859,15 @@ static py::str yaml_dump(py::object data, bool sort_maps, py::object gomap, py::
   return py::reinterpret_steal<py::str>(r);
 }
 
+extern "C" PyObject* m2k_yaml_load(PyObject* text, int mode, int multi, PyObject* resolve_number,
+                                   PyObject* unsupported);
+
+static py::object yaml_load(py::object text, int mode, bool multi, py::object resolve_number, py::object unsupported) {
+  PyObject* r = m2k_yaml_load(text.ptr(), mode, multi ? 1 : 0, resolve_number.ptr(), unsupported.ptr());
+  if (!r) throw py::error_already_set();
+  return py::reinterpret_steal<py::object>(r);
+}
+
 PYBIND11_MODULE(_m2k_native, m) {
   m.doc() = "move2kube_amd native runtime (walk, sniff, spawn pool, hashes, edit distance)";
   m.def("walk", &walk, py::arg("root"));
@@ -846,10 +880,13 @@ PYBIND11_MODULE(_m2k_native, m) {
         py::arg("dcost") = 1, py::arg("scost") = 2, py::arg("nthreads") = 8);
   m.def("pack_strings", &pack_strings, py::arg("items"));
   m.def("closest_batch", &closest_batch, py::arg("as"), py::arg("bs"), py::arg("nthreads") = 8);
+  m.def("closest_list", &closest_list, py::arg("as"), py::arg("bs"), py::arg("nthreads") = 8);
   m.def("remove_tree", &remove_tree, py::arg("path"));
   m.def("write_files", &write_files, py::arg("paths"), py::arg("datas"), py::arg("modes"), py::arg("nthreads") = 8);
   m.def("yaml_dump", &yaml_dump, py::arg("data"), py::arg("sort_maps"), py::arg("gomap"), py::arg("scalar_fn"),
         py::arg("style_fn"), py::arg("sort_fn"));
+  m.def("yaml_load", &yaml_load, py::arg("text"), py::arg("mode"), py::arg("multi"), py::arg("resolve_number"),
+        py::arg("unsupported"));
   m.def("run_commands", &run_commands, py::arg("argvs"), py::arg("cwds"), py::arg("parallel") = 8,
         py::arg("timeout_s") = 0.0);
 }

@@ -9,9 +9,21 @@ builder buildpack lists) are offloaded to the MI355X kernel in
 import os
 import sys
 
-import numpy as np
+from . import native
 
-from . import gpu, native
+# numpy and the HIP wrapper (which needs numpy) are imported on first use:
+# importing numpy costs more than the handful of matches a CLI run makes
+# (``closest_index_list``).
+
+
+def _np():
+    import numpy
+    return numpy
+
+
+def _gpu():
+    from . import gpu
+    return gpu
 
 # Crossover measured on MI355X (profiles/r01_ed_crossover.log): once the HIP
 # runtime is up, the GPU wins from ~8k pairs (0.09 ms vs 0.09-0.22 ms on 16
@@ -24,7 +36,7 @@ GPU_MIN_PAIRS_COLD = int(os.environ.get("M2K_GPU_MIN_PAIRS_COLD", "100000000"))
 def _gpu_warm():
     """True when this process already paid the HIP start-up (our library ran,
     or torch initialised the device)."""
-    if gpu.warm():
+    if "move2kube_amd.ops.gpu" in sys.modules and _gpu().warm():
         return True
     torch = sys.modules.get("torch")
     try:
@@ -62,6 +74,9 @@ def wagner_fischer_py(a, b, icost=1, dcost=1, scost=2):
 def _use_gpu(pairs, device, queries):
     if device == "cpu":
         return False
+    if device != "gpu" and pairs < GPU_MIN_PAIRS:
+        return False
+    gpu = _gpu()
     fits = all(len(q.encode() if isinstance(q, str) else q) <= 64 for q in queries)
     if device == "gpu":
         if not fits:
@@ -83,6 +98,7 @@ def matrix(options, queries, device="auto"):
     device: "auto" | "cpu" | "gpu"."""
     na, nb = len(options), len(queries)
     if _use_gpu(na * nb, device, queries):
+        gpu = _gpu()
         try:
             return gpu.ed_matrix(options, queries)
         except gpu.GpuUnsupportedInput:
@@ -91,6 +107,7 @@ def matrix(options, queries, device="auto"):
     m = native.module()
     if m is not None:
         return m.edit_distance_batch(list(options), list(queries), 1, 1, 2, _threads())
+    np = _np()
     return np.array([[wagner_fischer_py(o, q) for q in queries] for o in options], dtype=np.int32).reshape(na, nb)
 
 
@@ -99,9 +116,11 @@ def closest_indices(options, queries, device="auto"):
     and that distance (int32 arrays; -1 when there are no options).  The argmin
     is fused into the distance computation (GPU kernel or native CPU)."""
     na, nb = len(options), len(queries)
+    np = _np()
     if na == 0 or nb == 0:
         return np.full(nb, -1, dtype=np.int32), np.full(nb, -1, dtype=np.int32)
     if _use_gpu(na * nb, device, queries):
+        gpu = _gpu()
         try:
             return gpu.ed_closest(options, queries)
         except gpu.GpuUnsupportedInput:
@@ -110,16 +129,36 @@ def closest_indices(options, queries, device="auto"):
     m = native.module()
     if m is not None:
         return m.closest_batch(list(options), list(queries), _threads())
-    idx = np.empty(nb, dtype=np.int32)
-    dist = np.empty(nb, dtype=np.int32)
-    for j, q in enumerate(queries):
+    idx, dist = _closest_py(options, queries)
+    return np.array(idx, dtype=np.int32), np.array(dist, dtype=np.int32)
+
+
+def _closest_py(options, queries):
+    idx, dist = [], []
+    for q in queries:
         bi, bd = -1, -1
         for i, o in enumerate(options):
             d = wagner_fischer_py(o, q)
             if bi < 0 or d < bd:
                 bi, bd = i, d
-        idx[j], dist[j] = bi, bd
+        idx.append(bi)
+        dist.append(bd)
     return idx, dist
+
+
+def closest_index_list(options, queries, device="auto"):
+    """:func:`closest_indices` as two Python lists.  Below the GPU threshold
+    this path never imports numpy (the native ``closest_list``)."""
+    na, nb = len(options), len(queries)
+    if na == 0 or nb == 0:
+        return [-1] * nb, [-1] * nb
+    if _use_gpu(na * nb, device, queries):
+        idx, dist = closest_indices(options, queries, device)
+        return [int(i) for i in idx], [int(d) for d in dist]
+    m = native.module()
+    if m is not None:
+        return m.closest_list(list(options), list(queries), _threads())
+    return _closest_py(options, queries)
 
 
 def distances(options, search):
@@ -130,5 +169,5 @@ def distances(options, search):
 def closest(options, search):
     if not options:
         return ""
-    idx, _ = closest_indices(options, [search])
-    return options[int(idx[0])]
+    idx, _ = closest_index_list(options, [search])
+    return options[idx[0]]

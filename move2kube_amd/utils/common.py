@@ -431,5 +431,5 @@ def get_closest_matching_strings(options, searches):
         return [""] * len(searches)
     toks = [_TOKEN_RE.sub("", o).lower() for o in options]
     qs = [_TOKEN_RE.sub("", s).lower() for s in searches]
-    idx, _ = editdistance.closest_indices(toks, qs)
-    return [options[int(i)] for i in idx]
+    idx, _ = editdistance.closest_index_list(toks, qs)
+    return [options[i] for i in idx]

@@ -774,13 +774,48 @@ def _memoized(kind, text, parse):
 _MISS = object()
 
 
+# Native decode (ops/csrc/yaml_parse.cpp): a strict block-YAML subset parser
+# that resolves scalars like the three loader classes above and answers
+# _UNSUPPORTED for anything else (anchors, tags, multi-line flow/quoted/plain
+# scalars, malformed input, ...), which then goes through PyYAML.  Most files a
+# command reads never import PyYAML.  M2K_NATIVE_YAML=0 turns it off.
+_TYPED, _V2, _RAW = 0, 1, 2
+_UNSUPPORTED = object()
+_native_load = None
+
+
+def _native_loader():
+    global _native_load
+    if _native_load is None:
+        import os
+        fn = False
+        if os.environ.get("M2K_NATIVE_YAML", "1") != "0":
+            from ..ops import native
+            fn = getattr(native.module(), "yaml_load", None) or False
+        _native_load = fn
+    return _native_load
+
+
+def _parse(text, mode, multi):
+    nl = _native_loader()
+    if nl and isinstance(text, str):
+        r = nl(text, mode, multi, go_resolve_number, _UNSUPPORTED)
+        if r is not _UNSUPPORTED:
+            return r
+    lz = _lz()
+    loader = (lz.typed, lz.v2, lz.raw)[mode]
+    if multi:
+        return list(lz.yaml.load_all(text, Loader=loader))
+    return lz.yaml.load(text, Loader=loader)
+
+
 def load(text):
     """Decode like go-yaml v3 into ``interface{}``."""
-    return _memoized("typed", text, lambda t: _lz().yaml.load(t, Loader=_lz().typed))
+    return _memoized("typed", text, lambda t: _parse(t, _TYPED, False))
 
 
 def load_all(text):
-    return _memoized("typed*", text, lambda t: list(_lz().yaml.load_all(t, Loader=_lz().typed)))
+    return _memoized("typed*", text, lambda t: _parse(t, _TYPED, True))
 
 
 _V2_ONLY_WORDS = re.compile(r"\b(?:[yYnN]|yes|Yes|YES|no|No|NO|on|On|ON|off|Off|OFF)\b")
@@ -792,15 +827,15 @@ def load_v2(text):
     not contain one anywhere shares the v3 parse (and its memo entry)."""
     if isinstance(text, str) and not _V2_ONLY_WORDS.search(text):
         return load(text)
-    return _memoized("typed-v2", text, lambda t: _lz().yaml.load(t, Loader=_lz().v2))
+    return _memoized("typed-v2", text, lambda t: _parse(t, _V2, False))
 
 
 def load_all_v2(text):
     if isinstance(text, str) and not _V2_ONLY_WORDS.search(text):
         return load_all(text)
-    return _memoized("typed-v2*", text, lambda t: list(_lz().yaml.load_all(t, Loader=_lz().v2)))
+    return _memoized("typed-v2*", text, lambda t: _parse(t, _V2, True))
 
 
 def load_raw(text):
     """Decode keeping scalars as raw strings (for typed struct decoding)."""
-    return _memoized("raw", text, lambda t: _lz().yaml.load(t, Loader=_lz().raw))
+    return _memoized("raw", text, lambda t: _parse(t, _RAW, False))

@@ -4,6 +4,7 @@ mkdir -p gpurun_out/cold
 export M2K_NO_NETWORK=1 M2K_DISABLE_CNB=1
 cp -r samples/golang /tmp/golang_src
 cd /tmp
+export PYTHONPATH=$GRAFT_REPO_ROOT
 for i in 1 2 3; do python -X importtime -c "pass" 2> $GRAFT_REPO_ROOT/gpurun_out/cold/floor_imp$i.txt; done
 for i in 1 2 3; do timeout -k 5 60 python -X importtime -m move2kube_amd translate -s golang_src -o out$i --qaskip > /dev/null 2> $GRAFT_REPO_ROOT/gpurun_out/cold/imp$i.txt; done
 timeout -k 5 60 python -c "
