@@ -1,7 +1,7 @@
 """Host-code sanitizers for the native runtime (the reference's ``go test -race``,
 ``Makefile:92``): ``_m2k_native`` is rebuilt with ASan+UBSan and with TSan and
 every multi-threaded entry point (walk, Dockerfile sniffing, edit distance,
-closest match, batched writes, the spawn pool, the YAML emitter) is driven in
+closest match, batched writes, the spawn pool, the YAML emitter and loader) is driven in
 a child interpreter with the sanitizer runtime preloaded; any report fails the
 test (``halt_on_error``).  GPU code is not involved (GPU sanitizers are not
 available on the target pool)."""
@@ -68,6 +68,16 @@ DRIVER = textwrap.dedent(r'''
     ts = [threading.Thread(target=emit) for _ in range(4)]
     for t in ts: t.start()
     for t in ts: t.join()
+    # the YAML loader on well-formed, truncated and malformed inputs (every prefix
+    # of a document exercises each end-of-input path of the line scanner)
+    unsup = object()
+    text = m.yaml_dump(doc, True, yamlio.GoMap, yamlio._scalar_lines, yamlio._string_style, yamlio.go_key_sorted)
+    text += "---\nk: 'q''s'\nl: [1, \"x\\u00e9\", {a: b}]\nb: |+\n  x\n\n  y\nf: >-\n  p\n   q\n"
+    for i in range(len(text) + 1):
+        for mode in (0, 1, 2):
+            m.yaml_load(text[:i], mode, True, yamlio.go_resolve_number, unsup)
+            m.yaml_load(text[:i], mode, False, yamlio.go_resolve_number, unsup)
+    assert m.yaml_load(text, 0, True, yamlio.go_resolve_number, unsup)[0] == doc
     print("SANITIZER-DRIVER-OK")
 ''')
 
@@ -88,8 +98,12 @@ def test_native_runtime_under_sanitizer(kind, lib, tmp_path):
     so = str(moddir / ("_m2k_native" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")))
     build.build_native(force=True, out=so, sanitize=kind)
     env = dict(os.environ)
+    # libstdc++ is preloaded too: python itself does not link it, and without it
+    # the runtime's __cxa_throw interceptor has no real function to forward
+    # to, so the first C++ exception (the YAML loader's bail-out) aborts
+    cxx = _runtime("libstdc++.so.6")
     env.update({
-        "LD_PRELOAD": rt,
+        "LD_PRELOAD": rt + (" " + cxx if cxx else ""),
         "M2K_DISABLE_NATIVE": "1",  # the package itself must not load the uninstrumented build
         "ASAN_OPTIONS": "detect_leaks=0:halt_on_error=1:abort_on_error=0",
         "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1",
