@@ -149,44 +149,69 @@ def version_handler(a):
     print(move2kube.get_version(a.long))
 
 
-def build_parser():
+_VERBS = ("collect", "plan", "translate", "version")
+
+
+def _verb_of(argv):
+    """The sub-command named on the command line (after the root flags), or None."""
+    for arg in argv:
+        if arg in ("-v", "--verbose"):
+            continue
+        return arg if arg in _VERBS else None
+    return None
+
+
+def build_parser(only=None):
+    """The cobra command tree as argparse.  ``only`` = the verb being run: its
+    arguments are the only ones built (argparse translates every help string
+    through gettext as it is added, a measurable share of a cold run); the
+    other verbs stay registered, so choices and errors are unchanged."""
     root = argparse.ArgumentParser(prog="move2kube", description="A tool to modernize to kubernetes/openshift")
     root.add_argument("-v", "--verbose", action="store_true", help="Enable verbose output")
     sub = root.add_subparsers(dest="command")
 
+    def wanted(verb):
+        return only is None or only == verb
+
     c = sub.add_parser("collect", help="Collect and process metadata from multiple sources.")
-    c.add_argument("-a", "--annotations", default="", help="Specify annotations to select collector subset.")
-    c.add_argument("-o", "--outpath", default=".", help="Specify output directory for collect.")
-    c.add_argument("-s", "--source", default="", help="Specify source directory for the artifacts to be considered while collecting.")
-    c.set_defaults(func=collect_handler)
+    if wanted("collect"):
+        c.add_argument("-a", "--annotations", default="", help="Specify annotations to select collector subset.")
+        c.add_argument("-o", "--outpath", default=".", help="Specify output directory for collect.")
+        c.add_argument("-s", "--source", default="", help="Specify source directory for the artifacts to be considered while collecting.")
+        c.set_defaults(func=collect_handler)
 
     p = sub.add_parser("plan", help="Plan out a move")
-    p.add_argument("-s", "--source", required=True, help="Specify source directory.")
-    p.add_argument("-p", "--plan", default=DEFAULT_PLAN_FILE, help="Specify a file path to save plan to.")
-    p.add_argument("-n", "--name", default=DEFAULT_PROJECT_NAME, help="Specify the project name.")
-    p.set_defaults(func=plan_handler)
+    if wanted("plan"):
+        p.add_argument("-s", "--source", required=True, help="Specify source directory.")
+        p.add_argument("-p", "--plan", default=DEFAULT_PLAN_FILE, help="Specify a file path to save plan to.")
+        p.add_argument("-n", "--name", default=DEFAULT_PROJECT_NAME, help="Specify the project name.")
+        p.set_defaults(func=plan_handler)
 
     t = sub.add_parser("translate", help="Translate using move2kube plan")
-    t.add_argument("-p", "--plan", default=None, help="Specify a plan file to execute.")
-    t.add_argument("-c", "--curate", action="store_true", help="Specify whether to curate the plan with a q/a.")
-    t.add_argument("-s", "--source", default=None, help="Specify source directory to translate.")
-    t.add_argument("-o", "--outpath", default=".", help="Path for output. Default will be directory with the project name.")
-    t.add_argument("-n", "--name", default=None, help="Specify the project name.")
-    t.add_argument("-q", "--qacache", action=_StringSlice, default=[], help="Specify qa cache file locations")
-    t.add_argument("--ignoreenv", action="store_true", help="Ignore data from local machine.")
-    t.add_argument("--qadisablecli", action="store_true", help=argparse.SUPPRESS)
-    t.add_argument("--qaskip", action="store_true", help=argparse.SUPPRESS)
-    t.add_argument("--qaport", type=int, default=0, help=argparse.SUPPRESS)
-    t.set_defaults(func=translate_handler)
+    if wanted("translate"):
+        t.add_argument("-p", "--plan", default=None, help="Specify a plan file to execute.")
+        t.add_argument("-c", "--curate", action="store_true", help="Specify whether to curate the plan with a q/a.")
+        t.add_argument("-s", "--source", default=None, help="Specify source directory to translate.")
+        t.add_argument("-o", "--outpath", default=".", help="Path for output. Default will be directory with the project name.")
+        t.add_argument("-n", "--name", default=None, help="Specify the project name.")
+        t.add_argument("-q", "--qacache", action=_StringSlice, default=[], help="Specify qa cache file locations")
+        t.add_argument("--ignoreenv", action="store_true", help="Ignore data from local machine.")
+        t.add_argument("--qadisablecli", action="store_true", help=argparse.SUPPRESS)
+        t.add_argument("--qaskip", action="store_true", help=argparse.SUPPRESS)
+        t.add_argument("--qaport", type=int, default=0, help=argparse.SUPPRESS)
+        t.set_defaults(func=translate_handler)
 
     v = sub.add_parser("version", help="Print the client version information")
-    v.add_argument("-l", "--long", action="store_true", help="print the version details")
-    v.set_defaults(func=version_handler)
+    if wanted("version"):
+        v.add_argument("-l", "--long", action="store_true", help="print the version details")
+        v.set_defaults(func=version_handler)
     return root
 
 
 def main(argv=None):
-    parser = build_parser()
+    if argv is None:
+        argv = sys.argv[1:]
+    parser = build_parser(_verb_of(argv))
     a = parser.parse_args(argv)
     if a.verbose:
         log.set_verbose(True)

@@ -2,14 +2,14 @@
 
 import json
 import os
-import re
 
 from ..models.collection import ImageInfo
 from ..utils import common, log
 from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
 from . import Collector, CommandError, run
+from ..utils.lazyre import lazy as _lazy_re
 
-_NUM = re.compile(r"[0-9]+")
+_NUM = _lazy_re(r"[0-9]+")
 
 
 def cast_to_int_e(s):

@@ -14,12 +14,13 @@ import io
 import json
 import os
 import shutil
-import subprocess
 import threading
-import urllib.parse
 
 from ...utils import common, log
 from ...utils.constants import settings
+from ...utils.lazyre import LazyModule
+
+subprocess = LazyModule("subprocess")
 
 ORDER_LABEL = "io.buildpacks.buildpack.order"
 # bounds for external tools (the reference waits forever; a hung pull or
@@ -113,9 +114,11 @@ class DockerAPIProvider:
 
     def pull_image(self, image):
         name, tag = (image.rsplit(":", 1) + ["latest"])[:2] if ":" in image.rsplit("/", 1)[-1] else (image, "latest")
+        import urllib.parse
         self._request("POST", "/images/create?" + urllib.parse.urlencode({"fromImage": name, "tag": tag}), raw=True)
 
     def inspect_image(self, image):
+        import urllib.parse
         return self._request("GET", "/images/%s/json" % urllib.parse.quote(image, safe=""))
 
     def _copy_dir(self, cid, src, dst):

@@ -1,8 +1,8 @@
 """Version information (reference ``types/info/versioninfo.go``)."""
 
-import re
 
 from ..utils import log
+from ..utils.lazyre import lazy as _lazy_re
 
 VERSION = "v0.1.0"
 BUILD_METADATA = ""
@@ -61,7 +61,7 @@ def get_version_info():
     return VersionInfo(get_version(), GIT_COMMIT, GIT_TREE_STATE, "python" + platform.python_version())
 
 
-_SEMVER = re.compile(r"^v?(\d+)(?:\.(\d+))?(?:\.(\d+))?(?:-([0-9A-Za-z\-.]+))?(?:\+([0-9A-Za-z\-.]+))?$")
+_SEMVER = _lazy_re(r"^v?(\d+)(?:\.(\d+))?(?:\.(\d+))?(?:-([0-9A-Za-z\-.]+))?(?:\+([0-9A-Za-z\-.]+))?$")
 
 
 def _parse_semver(s):

@@ -164,22 +164,107 @@ class Problem:
         return "Problem(%r)" % (self.to_json(),)
 
 
+_NOT_COMPILED = object()
+_QUANTIFIERS = "*?{"
+
+
+def required_literals(pattern):
+    """Literal substrings every match of ``pattern`` must contain (a
+    conservative subset), or None when the pattern has alternation or inline
+    flags and no such guarantee is cheap to give.
+
+    Only runs outside groups and character classes count, and a character
+    followed by ``*``, ``?`` or ``{`` is dropped: so if one of them is missing
+    from a string, ``re.search(pattern, string)`` is None for certain and the
+    pattern need not be compiled (question descriptions in a QA cache are
+    prose; almost none of them match each other)."""
+    if "|" in pattern or "(?" in pattern:
+        return None
+    out, seg, depth, i, n = [], [], 0, 0, len(pattern)
+
+    def flush():
+        if seg and depth == 0:
+            out.append("".join(seg))
+        seg.clear()
+
+    while i < n:
+        c = pattern[i]
+        if c == "\\":
+            nxt = pattern[i + 1] if i + 1 < n else ""
+            if nxt == "" or nxt.isalnum():
+                flush()  # class, anchor or back-reference
+                i += 2
+                continue
+            if i + 2 < n and pattern[i + 2] in _QUANTIFIERS:
+                flush()
+            else:
+                seg.append(nxt)
+            i += 2
+            continue
+        if c == "[":
+            flush()
+            j = i + 1
+            if j < n and pattern[j] == "^":
+                j += 1
+            if j < n and pattern[j] == "]":
+                j += 1
+            while j < n and pattern[j] != "]":
+                j += 2 if pattern[j] == "\\" else 1
+            i = j + 1
+            continue
+        if c == "(":
+            flush()
+            depth += 1
+        elif c == ")":
+            flush()
+            depth = max(0, depth - 1)
+        elif c in ".^$+":
+            flush()
+        elif c == "{":
+            # a repeat count (or a literal brace): nothing up to "}" is required
+            flush()
+            j = pattern.find("}", i)
+            i = n if j < 0 else j + 1
+            continue
+        elif c in _QUANTIFIERS:
+            flush()
+        elif i + 1 < n and pattern[i + 1] in _QUANTIFIERS:
+            flush()
+        else:
+            seg.append(c)
+        i += 1
+    flush()
+    return out
+
+
 @functools.lru_cache(maxsize=4096)
 def _matcher(s1):
-    """(casefolded s1, compiled regex or None) - cache lookups compare every
-    new problem against every cached one, so both are computed once."""
-    try:
-        rx = re.compile(_go_regex(s1))
-    except re.error as e:
-        log.debug("Unable to compile string %s : %s", s1, e)
-        rx = None
-    return s1.casefold(), rx
+    """[casefolded s1, required literals, regex] - cache lookups compare every
+    new problem against every cached one.  The regex is compiled on the first
+    comparison its literals do not rule out (``_NOT_COMPILED`` until then,
+    None if it does not compile)."""
+    return [s1.casefold(), required_literals(s1), _NOT_COMPILED]
 
 
 def _match_string(s1, s2):
-    folded, rx = _matcher(s1)
-    if folded == s2.casefold():
+    """``strings.EqualFold(s1, s2)`` or ``regexp.MatchString(s1, s2)``
+    (reference ``internal/types/qaengine/problem.go:matchString``)."""
+    m = _matcher(s1)
+    if m[0] == s2.casefold():
         return True
+    lits = m[1]
+    if lits is not None:
+        for lit in lits:
+            if lit not in s2:
+                return False
+    rx = m[2]
+    if rx is _NOT_COMPILED:
+        try:
+            rx = re.compile(_go_regex(s1))
+        except re.error as e:
+            log.debug("Unable to compile string %s : %s", s1, e)
+            rx = None
+        m[2] = rx
     return rx is not None and rx.search(s2) is not None
 
 

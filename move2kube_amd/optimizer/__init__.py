@@ -9,9 +9,10 @@ from ..models import ir as irtypes
 from ..models import qa
 from ..utils import common, log, trace
 from ..utils.constants import ANNOTATION_LABEL_VALUE, DEFAULT_SERVICE_PORT, EXPOSE_SELECTOR
+from ..utils.lazyre import lazy as _lazy_re
 
 MIN_REPLICAS = 2
-_QUOTES = re.compile(r"^[',\"](.*)[',\"]$", re.S)
+_QUOTES = _lazy_re(r"^[',\"](.*)[',\"]$", re.S)
 
 
 def strip_quotation(s):

@@ -13,8 +13,9 @@ import re
 from ..models import plan as plantypes
 from ..utils import common, yamlio
 from ..utils.gotemplate import go_sprint
+from ..utils.lazyre import lazy as _lazy_re
 
-_VAR_RE = re.compile(r"\(\((!?[-/\.\w]+)\)\)", re.UNICODE)
+_VAR_RE = _lazy_re(r"\(\((!?[-/\.\w]+)\)\)", re.UNICODE)
 
 
 class ManifestError(ValueError):

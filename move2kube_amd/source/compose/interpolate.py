@@ -13,8 +13,9 @@ import os
 import re
 
 from ...utils import log
+from ...utils.lazyre import lazy as _lazy_re
 
-_PATTERN = re.compile(
+_PATTERN = _lazy_re(
     r"\$(?:(?P<escaped>\$)|(?P<named>[_a-zA-Z][_a-zA-Z0-9]*)|\{(?P<braced>[_a-zA-Z][_a-zA-Z0-9]*(?::?[-?][^}]*)?)\}|(?P<invalid>))")
 
 

@@ -8,6 +8,7 @@ import shlex
 
 from ...utils import common, log
 from ...utils.constants import settings
+from ...utils.lazyre import lazy as _lazy_re
 
 MODE_READ_ONLY = "ro"
 TMPFS_PATH = "tmpfs"
@@ -55,7 +56,7 @@ def check_for_dockerfile(path):
 
 _DUR_UNITS = {"ns": 1, "us": 1000, "µs": 1000, "μs": 1000, "ms": 10 ** 6, "s": 10 ** 9,
               "m": 60 * 10 ** 9, "h": 3600 * 10 ** 9}
-_DUR_RE = re.compile(r"(\d+\.?\d*|\.\d+)(ns|us|µs|μs|ms|s|m|h)")
+_DUR_RE = _lazy_re(r"(\d+\.?\d*|\.\d+)(ns|us|µs|μs|ms|s|m|h)")
 
 
 def parse_duration(s):
@@ -84,7 +85,7 @@ def parse_duration(s):
     return -v if neg else v
 
 
-_RAM_RE = re.compile(r"^(\d+(?:\.\d+)*) ?([kKmMgGtTpP])?[iI]?[bB]?$")
+_RAM_RE = _lazy_re(r"^(\d+(?:\.\d+)*) ?([kKmMgGtTpP])?[iI]?[bB]?$")
 _RAM_MULT = {"k": 1024, "m": 1024 ** 2, "g": 1024 ** 3, "t": 1024 ** 4, "p": 1024 ** 5}
 
 

@@ -3,7 +3,8 @@
 Every ``.yml``/``.yaml`` file is tried as compose v3 first and v1/v2 second.
 For each compose service a ReuseDockerfile option (when ``build.context`` is
 set) and a Reuse option are planned; image-info YAMLs (``ImageMetadata`` from
-``collect``) are attached by image tag.
+``collect``) are attached by image tag.  The compose loaders are imported on
+the first YAML file, so a tree without one never loads them.
 """
 
 import os
@@ -12,8 +13,6 @@ from ..models import collection
 from ..models import ir as irtypes
 from ..models import plan as plantypes
 from ..utils import common, log
-from .compose.v1v2 import V1V2Loader, parse_v2
-from .compose.v3 import ComposeError, V3Loader, parse_v3
 from .translator import Translator
 
 
@@ -63,6 +62,8 @@ class ComposeTranslator(Translator):
         return out
 
     def services_from_compose_file(self, path, image_meta):
+        from .compose.v1v2 import parse_v2
+        from .compose.v3 import ComposeError, parse_v3
         try:
             cfg = parse_v3(path)
         except ComposeError as e3:
@@ -100,6 +101,8 @@ class ComposeTranslator(Translator):
         return services
 
     def translate(self, services, plan):
+        from .compose.v1v2 import V1V2Loader
+        from .compose.v3 import ComposeError, V3Loader
         ir = irtypes.new_ir(plan)
         for service in services:
             if service.translation_type != self.translation_type:

@@ -9,11 +9,11 @@ parallel by ``ops/csrc/m2k_native.cpp:sniff_dockerfiles``; this module holds the
 exact pure-Python equivalent and the final regex check.
 """
 
-import re
+from ..utils.lazyre import lazy as _lazy_re
 
-FROM_RE = re.compile(r"(?i)FROM\s+(--platform=[^\s]+)?[^\s]+(\s+AS\s+[^\s]+)?\s*(#.+)?$")
+FROM_RE = _lazy_re(r"(?i)FROM\s+(--platform=[^\s]+)?[^\s]+(\s+AS\s+[^\s]+)?\s*(#.+)?$")
 _MAX_LINE = 64 * 1024
-_DIRECTIVE_RE = re.compile(r"^#\s*([a-zA-Z][a-zA-Z0-9]*)\s*=\s*(.+?)\s*$")
+_DIRECTIVE_RE = _lazy_re(r"^#\s*([a-zA-Z][a-zA-Z0-9]*)\s*=\s*(.+?)\s*$")
 
 
 def _trim_continuation(line, esc):

@@ -13,6 +13,7 @@ import shutil
 
 from . import log, yamlio
 from .constants import (DEFAULT_FILE_PERMISSION, GROUP_NAME, SCHEME_VERSION)
+from .lazyre import lazy as _lazy_re
 
 # ---------------------------------------------------------------------------
 # hashing primitives (native when available; pure-python fallback is exact)
@@ -202,7 +203,7 @@ def normalize_for_filename(name):
     return processed + "-" + format(crc64_ecma(name.encode()), "x")
 
 
-_SVC_RE = re.compile(r"[._]")
+_SVC_RE = _lazy_re(r"[._]")
 
 
 def normalize_for_service_name(svc_name):
@@ -258,7 +259,7 @@ def write_template_to_file(tpl, config, write_path, mode):
     write_text(write_path, get_string_from_template(tpl, config), mode)
 
 
-_TOKEN_RE = re.compile(r"[^a-zA-Z0-9]+")
+_TOKEN_RE = _lazy_re(r"[^a-zA-Z0-9]+")
 
 
 def get_closest_matching_string(options, search):
@@ -269,7 +270,7 @@ def get_closest_matching_string(options, search):
     return get_closest_matching_strings(options, [search])[0]
 
 
-_FILENAME_INVALID = re.compile(r"[^a-zA-Z0-9\-.]+")
+_FILENAME_INVALID = _lazy_re(r"[^a-zA-Z0-9\-.]+")
 
 
 def make_file_name_compliant(name):
@@ -283,7 +284,7 @@ def make_file_name_compliant(name):
     return processed
 
 
-_DNS_INVALID = re.compile(r"[^a-z0-9\-.]")
+_DNS_INVALID = _lazy_re(r"[^a-z0-9\-.]")
 
 
 def make_string_dns_name_compliant(s):

@@ -21,10 +21,11 @@ import re
 import threading
 
 from . import log
+from .lazyre import lazy as _lazy_re
 
 FILE, DIR, SYMLINK, OTHER = 0, 1, 2, 3
 MISSING = -1
-_SUFFIX_PATTERN = re.compile(r"^\*\.[A-Za-z0-9_+-]+$")
+_SUFFIX_PATTERN = _lazy_re(r"^\*\.[A-Za-z0-9_+-]+$")
 
 _local = threading.local()
 

@@ -9,6 +9,7 @@ import os
 import re
 
 from . import fsindex
+from .lazyre import lazy as _lazy_re
 
 
 class GitError(Exception):
@@ -59,7 +60,7 @@ def find_repo(path):
     return result
 
 
-_REMOTE_RE = re.compile(r'^remote\s+"(.*)"$')
+_REMOTE_RE = _lazy_re(r'^remote\s+"(.*)"$')
 
 
 def _read_config(git_dir):

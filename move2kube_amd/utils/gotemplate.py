@@ -23,6 +23,7 @@ import math
 import re
 
 from .yamlio import go_format_float
+from .lazyre import lazy as _lazy_re
 
 
 class TemplateError(Exception):
@@ -226,7 +227,7 @@ def go_sprintf(fmt, args):
 # Lexer
 # ---------------------------------------------------------------------------
 
-_TOKEN_RE = re.compile(r"""
+_TOKEN_RE = _lazy_re(r"""
     (?P<ws>\s+)
   | (?P<comment>/\*.*?\*/)
   | (?P<str>"(?:[^"\\]|\\.)*")
@@ -244,6 +245,8 @@ _TOKEN_RE = re.compile(r"""
   | (?P<num>[-+]?(?:0[xX][0-9a-fA-F_]+|0[bB][01_]+|0[oO][0-7_]+|(?:\d[\d_]*)?\.?\d[\d_]*(?:[eE][-+]?\d+)?)i?)
   | (?P<ident>[A-Za-z_][A-Za-z0-9_]*)
 """, re.S | re.X)
+
+_FIELD_CHAIN_RE = _lazy_re(r"(?:\.[A-Za-z_][A-Za-z0-9_]*)+")
 
 
 def _lex_action(src, pos, right_delim):
@@ -276,7 +279,7 @@ def _lex_action(src, pos, right_delim):
             continue
         if kind == "var" and pos < n and src[pos] == ".":
             # $x.Field.Sub
-            m2 = re.compile(r"(?:\.[A-Za-z_][A-Za-z0-9_]*)+").match(src, pos)
+            m2 = _FIELD_CHAIN_RE.match(src, pos)
             if m2:
                 text += m2.group(0)
                 pos = m2.end()

@@ -24,6 +24,7 @@ import functools
 import math
 import re
 import threading
+from .lazyre import lazy as _lazy_re
 
 # PyYAML is imported on the first parse (``_lz()``), not at start-up: a CLI
 # run over a source tree without YAML files never pays for it.
@@ -122,11 +123,11 @@ def go_key_sorted(keys):
 # Plain-scalar resolution (what a plain scalar would decode to)
 # ---------------------------------------------------------------------------
 
-_YAML_FLOAT = re.compile(r"^[-+]?(\.[0-9]+|[0-9]+(\.[0-9]*)?)([eE][-+]?[0-9]+)?$")
+_YAML_FLOAT = _lazy_re(r"^[-+]?(\.[0-9]+|[0-9]+(\.[0-9]*)?)([eE][-+]?[0-9]+)?$")
 _TIMESTAMP_FORMATS = [
-    re.compile(r"^\d{4}-\d{1,2}-\d{1,2}[Tt]\d{1,2}:\d{1,2}:\d{1,2}(\.\d+)?(Z|[+-]\d{1,2}(:\d{2})?)$"),
-    re.compile(r"^\d{4}-\d{1,2}-\d{1,2} \d{1,2}:\d{1,2}:\d{1,2}(\.\d+)?$"),
-    re.compile(r"^\d{4}-\d{1,2}-\d{1,2}$"),
+    _lazy_re(r"^\d{4}-\d{1,2}-\d{1,2}[Tt]\d{1,2}:\d{1,2}:\d{1,2}(\.\d+)?(Z|[+-]\d{1,2}(:\d{2})?)$"),
+    _lazy_re(r"^\d{4}-\d{1,2}-\d{1,2} \d{1,2}:\d{1,2}:\d{1,2}(\.\d+)?$"),
+    _lazy_re(r"^\d{4}-\d{1,2}-\d{1,2}$"),
 ]
 _NULLS = {"", "~", "null", "Null", "NULL"}
 _BOOLS = {"true", "True", "TRUE", "false", "False", "FALSE"}
@@ -134,7 +135,7 @@ _OLD_BOOLS = {"y", "Y", "yes", "Yes", "YES", "on", "On", "ON",
               "n", "N", "no", "No", "NO", "off", "Off", "OFF"}
 _SPECIAL_FLOATS = {".inf", ".Inf", ".INF", "+.inf", "+.Inf", "+.INF",
                    "-.inf", "-.Inf", "-.INF", ".nan", ".NaN", ".NAN"}
-_BASE60 = re.compile(r"^[-+]?[0-9][0-9_]*(?::[0-5]?[0-9])+(?:\.[0-9_]*)?$")
+_BASE60 = _lazy_re(r"^[-+]?[0-9][0-9_]*(?::[0-5]?[0-9])+(?:\.[0-9_]*)?$")
 
 
 def _go_parse_int(s):
@@ -329,7 +330,7 @@ PLAIN, SINGLE, DOUBLE, LITERAL = range(4)
 
 # strings that libyaml's analysis always allows as block plain scalars: no
 # indicators, no leading/trailing space, no breaks, printable ASCII only
-_SIMPLE_SCALAR = re.compile(r"[A-Za-z0-9_/](?:[A-Za-z0-9_./ -]*[A-Za-z0-9_./-])?\Z")
+_SIMPLE_SCALAR = _lazy_re(r"[A-Za-z0-9_/](?:[A-Za-z0-9_./ -]*[A-Za-z0-9_./-])?\Z")
 _style_cache = {}
 
 
@@ -587,7 +588,7 @@ def dumps_k8s(obj):
 # ---------------------------------------------------------------------------
 
 _INT64_MIN, _INT64_MAX, _UINT64_MAX = -(1 << 63), (1 << 63) - 1, (1 << 64) - 1
-_DOT_FLOAT = re.compile(r"^\.[0-9][0-9_]*(?:[eE][-+]?[0-9]+)?$")
+_DOT_FLOAT = _lazy_re(r"^\.[0-9][0-9_]*(?:[eE][-+]?[0-9]+)?$")
 
 
 def _go_int_value(t):
@@ -640,7 +641,7 @@ def _construct_go_number(loader, node):
 
 
 _GONUM_TAG = "tag:move2kube:go-number"
-_GONUM_FIRST = re.compile(r"^[-+0-9.]")
+_GONUM_FIRST = _lazy_re(r"^[-+0-9.]")
 
 
 _TRUE_WORDS = {"y", "Y", "yes", "Yes", "YES", "true", "True", "TRUE", "on", "On", "ON"}
@@ -818,7 +819,7 @@ def load_all(text):
     return _memoized("typed*", text, lambda t: _parse(t, _TYPED, True))
 
 
-_V2_ONLY_WORDS = re.compile(r"\b(?:[yYnN]|yes|Yes|YES|no|No|NO|on|On|ON|off|Off|OFF)\b")
+_V2_ONLY_WORDS = _lazy_re(r"\b(?:[yYnN]|yes|Yes|YES|no|No|NO|on|On|ON|off|Off|OFF)\b")
 
 
 def load_v2(text):
