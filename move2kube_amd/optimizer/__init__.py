@@ -2,21 +2,24 @@
 normalize characters -> ingress exposure (QA) -> minimum replicas ->
 imagePullPolicy Always -> port merge (QA)."""
 
-import re
-
 from .. import qaengine
 from ..models import ir as irtypes
 from ..models import qa
 from ..utils import common, log, trace
 from ..utils.constants import ANNOTATION_LABEL_VALUE, DEFAULT_SERVICE_PORT, EXPOSE_SELECTOR
-from ..utils.lazyre import lazy as _lazy_re
 
 MIN_REPLICAS = 2
-_QUOTES = _lazy_re(r"^[',\"](.*)[',\"]$", re.S)
+_QUOTE_CHARS = "',\""
 
 
 def strip_quotation(s):
-    return _QUOTES.sub(r"\1", s)
+    """``regexp.MustCompile(`^[',"](.*)[',"]$`).ReplaceAllString(s, "$1")``
+    (normalizecharactersoptimizer.go:48-52) without a regex.  RE2's ``.`` does
+    not match a newline and its ``$`` is the end of the text, so a value with a
+    line break inside keeps its quotes."""
+    if len(s) >= 2 and s[0] in _QUOTE_CHARS and s[-1] in _QUOTE_CHARS and "\n" not in s:
+        return s[1:-1]
+    return s
 
 
 class NormalizeCharacterOptimizer:

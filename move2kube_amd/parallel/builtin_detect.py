@@ -19,7 +19,6 @@ in readdir order (file-system dependent in the reference too).
 """
 
 import os
-import re
 
 from ..utils import fsindex
 from ..utils.constants import settings
@@ -57,12 +56,11 @@ def _find_main(src):
         idx = fsindex.get_index(src)
     except (OSError, FileNotFoundError):
         return ""
-    rx = re.compile(r".py$")
     for p, k in zip(idx.paths, idx.kinds):
         if k == fsindex.DIR:
             continue
         shown = src + p[len(idx.root):] if p.startswith(idx.root) else p
-        if not rx.search(shown):
+        if len(shown) < 3 or not shown.endswith("py"):  # awk '/.py$/': any character, then "py"
             continue
         try:
             with open(p, "rb") as f:

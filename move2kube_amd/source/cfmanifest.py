@@ -60,6 +60,8 @@ class Application:
 
 def _var_names(obj, out):
     if isinstance(obj, str):
+        if "((" not in obj:
+            return
         for m in _VAR_RE.finditer(obj):
             out.add(m.group(1).lstrip("!").split(".")[0])
     elif isinstance(obj, dict):
@@ -75,6 +77,8 @@ def _evaluate(obj, values):
     """bosh template evaluation: a scalar that is exactly ((var)) is replaced by the
     value; embedded placeholders are string-interpolated."""
     if isinstance(obj, str):
+        if "((" not in obj:
+            return obj
         m = _VAR_RE.fullmatch(obj)
         if m:
             name = m.group(1).lstrip("!")

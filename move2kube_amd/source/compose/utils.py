@@ -4,7 +4,6 @@ specs, volume specs, Kubernetes quantity formatting)."""
 
 import os
 import re
-import shlex
 
 from ...utils import common, log
 from ...utils.constants import settings
@@ -140,6 +139,7 @@ def format_milli_quantity(milli):
 def shell_split(s):
     """docker/cli ``ShellCommand`` (mattn/go-shellwords) for string commands."""
     try:
+        import shlex  # its module regex compiles at import: only for string commands
         return shlex.split(s)
     except ValueError:
         return s.split()

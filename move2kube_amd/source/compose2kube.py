@@ -101,14 +101,14 @@ class ComposeTranslator(Translator):
         return services
 
     def translate(self, services, plan):
-        from .compose.v1v2 import V1V2Loader
-        from .compose.v3 import ComposeError, V3Loader
         ir = irtypes.new_ir(plan)
         for service in services:
             if service.translation_type != self.translation_type:
                 continue
             for path in service.source_artifacts.get(plantypes.COMPOSE_FILE_ARTIFACT) or []:
                 log.debug("File %s being loaded from compose service : %s", path, service.service_name)
+                from .compose.v1v2 import V1V2Loader
+                from .compose.v3 import ComposeError, V3Loader
                 try:
                     cir = V3Loader().convert_to_ir(path, plan, service)
                 except ComposeError as e3:

@@ -203,11 +203,8 @@ def normalize_for_filename(name):
     return processed + "-" + format(crc64_ecma(name.encode()), "x")
 
 
-_SVC_RE = _lazy_re(r"[._]")
-
-
 def normalize_for_service_name(svc_name):
-    new = _SVC_RE.sub("-", svc_name).lower()
+    new = svc_name.replace(".", "-").replace("_", "-").lower()  # [._] -> "-" (utils.go:297-305)
     if new != svc_name:
         log.info("Changing service name to %s from %s", svc_name, new)
     return new
@@ -271,6 +268,11 @@ def get_closest_matching_string(options, search):
 
 
 _FILENAME_INVALID = _lazy_re(r"[^a-zA-Z0-9\-.]+")
+_ASCII_ALNUM = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789"
+# str.translate tables deleting the allowed characters: an empty result means
+# there is nothing to replace, and the regex is never compiled
+_DROP_FILENAME_OK = str.maketrans("", "", _ASCII_ALNUM + "-.")
+_DROP_DNS_OK = str.maketrans("", "", _ASCII_ALNUM[:26] + _ASCII_ALNUM[52:] + "-.")
 
 
 def make_file_name_compliant(name):
@@ -278,7 +280,7 @@ def make_file_name_compliant(name):
         log.error("The input name is empty.")
         return ""
     base = os.path.basename(name.rstrip("/")) or "/"
-    processed = _FILENAME_INVALID.sub("-", base)
+    processed = _FILENAME_INVALID.sub("-", base) if base.translate(_DROP_FILENAME_OK) else base
     if len(processed) > 63:
         log.debug("Warning: The processed name %r is longer than 63 characters long.", processed)
     return processed
@@ -288,7 +290,8 @@ _DNS_INVALID = _lazy_re(r"[^a-z0-9\-.]")
 
 
 def make_string_dns_name_compliant(s):
-    name = _DNS_INVALID.sub("-", s.lower())
+    low = s.lower()
+    name = _DNS_INVALID.sub("-", low) if low.translate(_DROP_DNS_OK) else low
     if name and (name[0] in "-." or name[-1] in "-."):
         log.warning("The first and/or last characters of the string %r are not alphanumeric.", s)
     return name

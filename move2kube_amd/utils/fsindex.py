@@ -21,11 +21,15 @@ import re
 import threading
 
 from . import log
-from .lazyre import lazy as _lazy_re
 
 FILE, DIR, SYMLINK, OTHER = 0, 1, 2, 3
 MISSING = -1
-_SUFFIX_PATTERN = _lazy_re(r"^\*\.[A-Za-z0-9_+-]+$")
+# "*.<ext>" with ext in [A-Za-z0-9_+-]: characters deleted by this table
+_DROP_SUFFIX_CHARS = str.maketrans("", "", "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_+-")
+
+
+def _is_suffix_pattern(pattern):
+    return len(pattern) > 2 and pattern.startswith("*.") and not pattern[2:].translate(_DROP_SUFFIX_CHARS)
 
 _local = threading.local()
 
@@ -216,7 +220,7 @@ class FileIndex:
             self._match = {}
         pos = self._match.get(pattern)
         if pos is None:
-            if _SUFFIX_PATTERN.match(pattern):
+            if _is_suffix_pattern(pattern):
                 # "*.go"-style: the basename ends with the suffix iff the path does
                 suffix = pattern[1:]
                 pos = [i for i, p in enumerate(self.paths) if p.endswith(suffix)]

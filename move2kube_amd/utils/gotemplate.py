@@ -227,6 +227,8 @@ def go_sprintf(fmt, args):
 # Lexer
 # ---------------------------------------------------------------------------
 
+# The token grammar; _scan_token implements it by hand (compiling this costs a
+# cold process ~1 ms) and tests/test_gotemplate_lexer.py checks the two agree.
 _TOKEN_RE = _lazy_re(r"""
     (?P<ws>\s+)
   | (?P<comment>/\*.*?\*/)
@@ -246,7 +248,116 @@ _TOKEN_RE = _lazy_re(r"""
   | (?P<ident>[A-Za-z_][A-Za-z0-9_]*)
 """, re.S | re.X)
 
-_FIELD_CHAIN_RE = _lazy_re(r"(?:\.[A-Za-z_][A-Za-z0-9_]*)+")
+
+_IDENT_START = frozenset("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ_")
+_IDENT_CHARS = _IDENT_START | frozenset("0123456789")
+_HEX_ = frozenset("0123456789abcdefABCDEF_")
+_BIN_ = frozenset("01_")
+_OCT_ = frozenset("01234567_")
+_SINGLE = {":=": "decl"}
+_PUNCT = {"=": "assign", "|": "pipe", "(": "lparen", ")": "rparen", ",": "comma"}
+
+
+def _skip_digits(src, i, n, underscore=True):
+    while i < n and (src[i].isdecimal() or (underscore and src[i] == "_")):
+        i += 1
+    return i
+
+
+def _scan_quoted(src, pos, n, quote, at_least_one):
+    i = pos + 1
+    while i < n:
+        c = src[i]
+        if c == "\\":
+            if i + 1 >= n:
+                return -1
+            i += 2
+            continue
+        if c == quote:
+            return -1 if (at_least_one and i == pos + 1) else i + 1
+        i += 1
+    return -1
+
+
+def _scan_num(src, pos, n):
+    i = pos
+    if i < n and src[i] in "+-":
+        i += 1
+    if i + 2 < n and src[i] == "0" and src[i + 1] in "xXbBoO":
+        digits = _HEX_ if src[i + 1] in "xX" else _BIN_ if src[i + 1] in "bB" else _OCT_
+        if src[i + 2] in digits:
+            j = i + 3
+            while j < n and src[j] in digits:
+                j += 1
+            return j + 1 if j < n and src[j] == "i" else j
+    if i < n and src[i].isdecimal():
+        j = _skip_digits(src, i + 1, n)
+        if j + 1 < n and src[j] == "." and src[j + 1].isdecimal():
+            j = _skip_digits(src, j + 2, n)
+    elif i + 1 < n and src[i] == "." and src[i + 1].isdecimal():
+        j = _skip_digits(src, i + 2, n)
+    else:
+        return -1
+    if j < n and src[j] in "eE":
+        k = j + 1
+        if k < n and src[k] in "+-":
+            k += 1
+        if k < n and src[k].isdecimal():
+            j = _skip_digits(src, k + 1, n, underscore=False)
+    return j + 1 if j < n and src[j] == "i" else j
+
+
+def _scan_token(src, pos):
+    """(kind, end) of the action token at ``pos``, or None: the first
+    alternative of ``_TOKEN_RE`` that matches, without compiling it."""
+    n = len(src)
+    c = src[pos]
+    if c.isspace():
+        j = pos + 1
+        while j < n and src[j].isspace():
+            j += 1
+        return "ws", j
+    if c == "/":
+        if src.startswith("/*", pos):
+            e = src.find("*/", pos + 2)
+            if e >= 0:
+                return "comment", e + 2
+        return None
+    if c == '"':
+        e = _scan_quoted(src, pos, n, '"', False)
+        return ("str", e) if e >= 0 else None
+    if c == "`":
+        e = src.find("`", pos + 1)
+        return ("raw", e + 1) if e >= 0 else None
+    if c == "'":
+        e = _scan_quoted(src, pos, n, "'", True)
+        return ("char", e) if e >= 0 else None
+    if c == ":":
+        return ("decl", pos + 2) if src.startswith(":=", pos) else None
+    kind = _PUNCT.get(c)
+    if kind is not None:
+        return kind, pos + 1
+    if c == "$":
+        j = pos + 1
+        while j < n and src[j] in _IDENT_CHARS:
+            j += 1
+        return "var", j
+    if c == ".":
+        j = pos
+        while j + 1 < n and src[j] == "." and src[j + 1] in _IDENT_START:
+            j += 2
+            while j < n and src[j] in _IDENT_CHARS:
+                j += 1
+        return ("field", j) if j > pos else ("dot", pos + 1)
+    if c in "+-" or c.isdecimal():
+        e = _scan_num(src, pos, n)
+        return ("num", e) if e >= 0 else None
+    if c in _IDENT_START:
+        j = pos + 1
+        while j < n and src[j] in _IDENT_CHARS:
+            j += 1
+        return "ident", j
+    return None
 
 
 def _lex_action(src, pos, right_delim):
@@ -262,16 +373,17 @@ def _lex_action(src, pos, right_delim):
             return toks, pos + off + len(right_delim), True
         if src.startswith(right_delim, pos):
             return toks, pos + len(right_delim), False
-        m = _TOKEN_RE.match(src, pos)
-        if not m:
+        tok = _scan_token(src, pos)
+        if tok is None:
             raise TemplateError("unexpected %r in action" % src[pos:pos + 10])
-        kind = m.lastgroup
-        text = m.group(kind)
-        pos = m.end()
+        kind, end = tok
         if kind == "ws":
+            pos = end
             continue
+        start, pos = pos, end
+        text = src[start:end]
         # a field chain directly after a closing paren or variable: (x).Field, $x.Field
-        if kind == "field" and toks and toks[-1][0] in ("rparen", "var") and src[m.start()] == ".":
+        if kind == "field" and toks and toks[-1][0] in ("rparen", "var") and src[start] == ".":
             if toks[-1][0] == "var":
                 toks[-1] = ("var", toks[-1][1] + text)
             else:
@@ -279,10 +391,10 @@ def _lex_action(src, pos, right_delim):
             continue
         if kind == "var" and pos < n and src[pos] == ".":
             # $x.Field.Sub
-            m2 = _FIELD_CHAIN_RE.match(src, pos)
-            if m2:
-                text += m2.group(0)
-                pos = m2.end()
+            kind2, end2 = _scan_token(src, pos)
+            if kind2 == "field":
+                text += src[pos:end2]
+                pos = end2
         toks.append((kind, text))
 
 

@@ -135,7 +135,20 @@ _OLD_BOOLS = {"y", "Y", "yes", "Yes", "YES", "on", "On", "ON",
               "n", "N", "no", "No", "NO", "off", "Off", "OFF"}
 _SPECIAL_FLOATS = {".inf", ".Inf", ".INF", "+.inf", "+.Inf", "+.INF",
                    "-.inf", "-.Inf", "-.INF", ".nan", ".NaN", ".NAN"}
+# characters a _YAML_FLOAT match can contain ("$" also matches before a final
+# newline); a string with any other character is ruled out without the regex
+_DROP_FLOAT_CHARS = str.maketrans("", "", "0123456789.eE+-\n")
+
+
+def _maybe_float(s):
+    return not s.translate(_DROP_FLOAT_CHARS)
+
+
 _BASE60 = _lazy_re(r"^[-+]?[0-9][0-9_]*(?::[0-5]?[0-9])+(?:\.[0-9_]*)?$")
+
+
+def _is_base60(s):
+    return ":" in s and _BASE60.match(s) is not None
 
 
 def _go_parse_int(s):
@@ -176,14 +189,14 @@ def resolves_to_string(s):
     if c.isdigit() or c in "+-.":
         if s in _SPECIAL_FLOATS:
             return False
-        if c.isdigit():
+        if c.isdigit() and len(s) >= 8 and s[4] == "-":  # every format starts \d{4}-
             for rx in _TIMESTAMP_FORMATS:
                 if rx.match(s):
                     return False
         plain = s.replace("_", "")
         if _go_parse_int(plain):
             return False
-        if _YAML_FLOAT.match(plain):
+        if _maybe_float(plain) and _YAML_FLOAT.match(plain):
             return False
         if c == "." :
             try:
@@ -331,6 +344,12 @@ PLAIN, SINGLE, DOUBLE, LITERAL = range(4)
 # strings that libyaml's analysis always allows as block plain scalars: no
 # indicators, no leading/trailing space, no breaks, printable ASCII only
 _SIMPLE_SCALAR = _lazy_re(r"[A-Za-z0-9_/](?:[A-Za-z0-9_./ -]*[A-Za-z0-9_./-])?\Z")
+_DROP_SIMPLE_CHARS = str.maketrans("", "", "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_./ -")
+
+
+def _is_simple_scalar(s):
+    """``_SIMPLE_SCALAR.match(s)`` with string operations (no compile in a cold process)."""
+    return (s != "" and not s.translate(_DROP_SIMPLE_CHARS) and s[0] not in ". -" and s[-1] != " ")
 _style_cache = {}
 
 
@@ -339,8 +358,8 @@ def _string_style(s, key=False):
     k = (s, key)
     st = _style_cache.get(k)
     if st is None:
-        if _SIMPLE_SCALAR.match(s):
-            can_plain = resolves_to_string(s) and not _BASE60.match(s) and s not in _OLD_BOOLS
+        if _is_simple_scalar(s):
+            can_plain = resolves_to_string(s) and not _is_base60(s) and s not in _OLD_BOOLS
             st = PLAIN if can_plain else DOUBLE
         else:
             st = _string_style_slow(s, key)
@@ -351,7 +370,7 @@ def _string_style(s, key=False):
 
 
 def _string_style_slow(s, key=False):
-    can_plain = resolves_to_string(s) and not _BASE60.match(s) and s not in _OLD_BOOLS
+    can_plain = resolves_to_string(s) and not _is_base60(s) and s not in _OLD_BOOLS
     if "\n" in s:
         style = LITERAL
     elif can_plain:
@@ -629,7 +648,7 @@ def go_resolve_number(s):
         v = _go_int_value(plain)
         if _INT64_MIN <= v <= _INT64_MAX or (0 <= v <= _UINT64_MAX and plain[:1] not in "+-"):
             return v
-    if _YAML_FLOAT.match(plain):
+    if _maybe_float(plain) and _YAML_FLOAT.match(plain):
         v = float(plain)
         if not math.isinf(v):
             return v
