@@ -15,6 +15,8 @@ this reports:
   (``python -m move2kube_amd collect|translate ...``: interpreter start,
   imports, asset unpack, the command, cleanup) - what a user of the Go binary
   compares against; byte-compiled modules cached as in an installed package;
+  ``cold_cpu_p50_ms`` is their CPU time and ``cold_over_floor_p50_ms`` the
+  time above a bare ``python -c pass`` per process, paired run by run;
 * ``python_emulation_of_reference_fork_model_p50_ms`` - p50 of in-process runs
   with every detector forked as ``/bin/sh`` one at a time on one worker, the
   way ``dockerfilecontainerizer.go:76-83`` runs them.  This is a Python
@@ -95,9 +97,18 @@ def warm_runs(name, runs, emulation_runs=0):
     return res
 
 
-def cold_runs(name, runs):
-    """``runs`` sets of CLI processes (plus one untimed priming run); returns
-    (p50 ms, total manifest diff vs ref)."""
+def _children_cpu_ms():
+    import resource
+    r = resource.getrusage(resource.RUSAGE_CHILDREN)
+    return (r.ru_utime + r.ru_stime) * 1e3
+
+
+def cold_stats(name, runs):
+    """``runs`` sets of CLI processes (plus one untimed priming run), each
+    preceded by a bare interpreter start in the same environment, so a noisy
+    host shows up in both.  Returns p50 wall and CPU (user+sys of the child
+    processes, stand-in tools included) of the sets, p50 of the per-pair
+    difference to the bare interpreter, and the total manifest diff."""
     work = tempfile.mkdtemp(prefix="m2k-cfgcold-")
     try:
         run = refconfigs.Run(name, work).prepare()
@@ -105,22 +116,39 @@ def cold_runs(name, runs):
         # run - the state of an installed package (pip / scripts/install.sh
         # byte-compile at install time).
         extra = {"PYTHONPYCACHEPREFIX": os.path.join(work, "pycache")}
-        times, diff = [], 0
+        env = run.env()
+        env.update(extra)
+        walls, cpus, over, diff = [], [], [], 0
         for i in range(-1, runs):
             t0 = time.perf_counter()
+            subprocess.run([sys.executable, "-c", "pass"], env=env)
+            floor = (time.perf_counter() - t0) * 1e3
+            c0 = _children_cpu_ms()
+            t0 = time.perf_counter()
             out = run.run_cli(extra_env=extra)
+            wall = (time.perf_counter() - t0) * 1e3
             if i >= 0:
-                times.append((time.perf_counter() - t0) * 1e3)
+                walls.append(wall)
+                cpus.append(_children_cpu_ms() - c0)
+                over.append(wall - floor * len(run.cli_commands()))
             diff += refconfigs.manifest_diff_vs_ref(name, out) or 0
-        return _p50(times), diff
+        return {"cold_p50_ms": _p50(walls), "cold_cpu_p50_ms": _p50(cpus), "cold_over_floor_p50_ms": _p50(over),
+                "manifest_diff_vs_ref": diff}
     finally:
         shutil.rmtree(work, ignore_errors=True)
 
 
+def cold_runs(name, runs):
+    """(cold p50 ms, total manifest diff vs ref) - see :func:`cold_stats`."""
+    st = cold_stats(name, runs)
+    return st["cold_p50_ms"], st["manifest_diff_vs_ref"]
+
+
 def bench_config(name, runs, emulation_runs):
     res = warm_runs(name, runs, emulation_runs)
-    res["cold_p50_ms"], cold_diff = cold_runs(name, runs)
-    res["manifest_diff_vs_ref"] += cold_diff
+    cold = cold_stats(name, runs)
+    res["manifest_diff_vs_ref"] += cold.pop("manifest_diff_vs_ref")
+    res.update(cold)
     return res
 
 

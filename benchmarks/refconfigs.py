@@ -118,12 +118,11 @@ class Run:
                     os.environ[k] = v
         return restore
 
-    def collect_inprocess(self):
-        from move2kube_amd import move2kube
+    def collect_inprocess(self, session):
         # what `collect -o <work>/collect` does (cmd/move2kube/collect.go:41-73)
         cdir = os.path.join(self.work, "collect", "m2k_collect")
         shutil.rmtree(cdir, ignore_errors=True)
-        move2kube.collect(self.src, cdir, self.collect_annotations)
+        session.collect(self.src, os.path.dirname(cdir), self.collect_annotations)
         dst = os.path.join(self.src, "m2k_collect")
         shutil.rmtree(dst, ignore_errors=True)
         shutil.copytree(cdir, dst)
@@ -132,7 +131,7 @@ class Run:
         """One in-process run of the configuration's commands (``session`` is an
         ``api.Session(qaskip=True, qacaches=run.caches, ignore_env=False)``)."""
         if self.collect_annotations:
-            self.collect_inprocess()
+            self.collect_inprocess(session)
         return session.translate(self.src, self.outdir, name=PROJECT)
 
     def session(self):

@@ -47,6 +47,12 @@ class Session:
         qaengine.start_engine(self.qaskip, 0, False)
         qaengine.add_caches(list(reversed(self.qacaches)))
 
+    def collect(self, src, outdir, annotations=()):
+        """``move2kube collect -s src -o outdir -a ...``: metadata under
+        ``outdir/m2k_collect``; no provider probe of an earlier run is reused."""
+        reset_state()
+        move2kube.collect(os.path.abspath(src) if src else "", os.path.join(outdir, "m2k_collect"), list(annotations))
+
     def plan(self, src, name="myproject"):
         self._start()
         with yamlio.parse_cache():

@@ -408,18 +408,19 @@ class RuncProvider:
 
 
 _providers = None
+_providers_switch = None
 
 
 def providers():
     """Provider chain dockerAPI -> podman/docker CLI -> pack -> runc.  ``M2K_DISABLE_CNB=1``
-    empties it (deterministic offline runs: benches, golden tests)."""
-    global _providers
+    empties it (deterministic offline runs: benches, golden tests); the chain
+    is rebuilt when the switch changes within a process."""
+    global _providers, _providers_switch
+    switch = os.environ.get("M2K_DISABLE_CNB", "") not in ("", "0")
     with _lock:
-        if _providers is None:
-            if os.environ.get("M2K_DISABLE_CNB", "") not in ("", "0"):
-                _providers = []
-            else:
-                _providers = [DockerAPIProvider(), ContainerRuntimeProvider(), PackProvider(), RuncProvider()]
+        if _providers is None or _providers_switch != switch:
+            _providers_switch = switch
+            _providers = [] if switch else [DockerAPIProvider(), ContainerRuntimeProvider(), PackProvider(), RuncProvider()]
         return _providers
 
 

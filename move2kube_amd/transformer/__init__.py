@@ -211,8 +211,12 @@ class K8sTransformer(Transformer):
         return objs
 
     def write_objects(self, outpath):
-        new_images = write_containers(self.containers, outpath, self.root_dir, self.values.registry_url,
-                                      self.values.registry_namespace)
+        """``Kubernetes.WriteObjects`` (k8stransformer.go:100-146).  For a Helm
+        chart the operator-sdk run (seconds for the real tool) starts as soon
+        as the chart is complete and overlaps the container build files and the
+        readme, which it does not read; it is waited for before returning."""
+        if not self.helm:
+            new_images = self._write_containers(outpath)
         artifacts = os.path.join(outpath, self.name)
         if self.helm:
             try:
@@ -226,10 +230,19 @@ class K8sTransformer(Transformer):
         except OSError as e:
             log.error("Error occurred while writing transformed objects %s", e)
         if self.helm:
-            self.create_operator(self.name, outpath)
-        else:
-            self.write_deploy_script(self.name, outpath)
+            operator = self.start_operator(self.name, outpath)
+            try:
+                new_images = self._write_containers(outpath)
+                self.write_readme(self.name, new_images, self.helm, self.add_copy_sources_warning, outpath)
+            finally:
+                self.finish_operator(operator)
+            return
+        self.write_deploy_script(self.name, outpath)
         self.write_readme(self.name, new_images, self.helm, self.add_copy_sources_warning, outpath)
+
+    def _write_containers(self, outpath):
+        return write_containers(self.containers, outpath, self.root_dir, self.values.registry_url,
+                                self.values.registry_namespace)
 
     def generate_helm_metadata(self, d):
         _mkdir(d)
@@ -245,31 +258,64 @@ class K8sTransformer(Transformer):
         common.write_template_to_file(assets.template("helminstall.sh.tpl"), {"Project": base},
                                       os.path.join(os.path.dirname(d), "helminstall.sh"), DEFAULT_EXECUTABLE_PERMISSION)
 
+    @classmethod
+    def create_operator(cls, project, basepath):
+        """``createOperator`` (k8stransformer.go:226-247): ``operator-sdk init
+        --plugins=helm`` over the chart in ``<out>/<project>-operator``."""
+        return cls.finish_operator(cls.start_operator(project, basepath))
+
     @staticmethod
-    def create_operator(project, basepath):
+    def start_operator(project, basepath):
+        """Launch operator-sdk without waiting; None if it cannot run."""
         sdk = shutil.which("operator-sdk")
         if sdk is None:
             log.warning("Unable to find operator-sdk. Skipping operator generation : exec: \"operator-sdk\": "
                         "executable file not found in $PATH")
-            return False
+            return None
         import subprocess
+        import tempfile
         opath = os.path.join(basepath, project + "-operator")
         if os.path.exists(opath):
             shutil.rmtree(opath, ignore_errors=True)
         _mkdir(opath)
         chart = os.path.abspath(os.path.join(basepath, project))
+        span = trace.span("operator-sdk init (external tool)", "external")
+        span.__enter__()
+        out = tempfile.TemporaryFile()  # not a pipe: nothing reads it until the tool exits
         try:
-            with trace.span("operator-sdk init (external tool)", "external"):
-                p = subprocess.run([sdk, "init", "--plugins=helm", "--helm-chart=" + chart, "--domain=io",
-                                    "--group=" + project, "--version=v1alpha1"], cwd=opath, stdout=subprocess.PIPE,
-                                   stderr=subprocess.PIPE, stdin=subprocess.DEVNULL, timeout=600)
-        except (OSError, subprocess.SubprocessError) as e:
+            p = subprocess.Popen([sdk, "init", "--plugins=helm", "--helm-chart=" + chart, "--domain=io",
+                                  "--group=" + project, "--version=v1alpha1"], cwd=opath, stdout=out,
+                                 stderr=subprocess.DEVNULL, stdin=subprocess.DEVNULL)
+        except OSError as e:
+            out.close()
+            span.__exit__(None, None, None)
             log.warning("Error during operator creation : %s", e)
+            return None
+        return p, out, span
+
+    @staticmethod
+    def finish_operator(started):
+        if started is None:
             return False
-        if p.returncode != 0:
-            log.warning("Error during operator creation : exit status %d, %s", p.returncode, p.stdout.decode("utf-8", "replace"))
-            return False
-        return True
+        import subprocess
+        p, out, span = started
+        try:
+            try:
+                rc = p.wait(timeout=600)
+            except subprocess.TimeoutExpired as e:
+                p.kill()
+                p.wait()
+                log.warning("Error during operator creation : %s", e)
+                return False
+            finally:
+                span.__exit__(None, None, None)
+            if rc != 0:
+                out.seek(0)
+                log.warning("Error during operator creation : exit status %d, %s", rc, out.read().decode("utf-8", "replace"))
+                return False
+            return True
+        finally:
+            out.close()
 
     def write_deploy_script(self, proj, outpath):
         common.write_template_to_file(assets.template("deploy.sh.tpl"), {"Project": proj},

@@ -50,6 +50,15 @@ def test_config_matches_reference_tree(name, tmp_path):
     assert refconfigs.diff_files(out, golden) == []
 
 
+def test_configs_back_to_back_in_one_process(tmp_path):
+    """No state of one run leaks into the next: configurations with CNB probing
+    off (golang, helm-openshift) alternate with ones that probe it through the
+    podman stand-in (cf collects buildpacks in process, java-cnb plans CNB)."""
+    for i, name in enumerate(["golang", "cf", "helm-openshift", "java-cnb", "docker-compose", "cf"]):
+        out = _run_inprocess(name, tmp_path / str(i), steps=1)
+        assert refconfigs.diff_files(out, os.path.join(refconfigs.GOLDEN_REF, name)) == [], name
+
+
 @pytest.mark.parametrize("name", [refconfigs.HEADLINE, "cf"])
 def test_config_as_cli_processes(name, tmp_path):
     """The same trees from separate ``python -m move2kube_amd`` processes
