@@ -1,15 +1,52 @@
-"""cProfile of warm bench steps (translate of samples/), sorted by argv[1] (default tottime)."""
-import os, sys, time, tempfile, shutil, cProfile, pstats
-sys.path.insert(0, os.environ.get('GRAFT_REPO_ROOT', '/root/repo'))
-os.environ["M2K_NO_NETWORK"]="1"; os.environ["M2K_DISABLE_CNB"]="1"
-from move2kube_amd import api
-from move2kube_amd.utils import log
-log.set_quiet()
-work=tempfile.mkdtemp(); src=os.path.join(work,"samples"); shutil.copytree(os.path.join(os.environ.get('GRAFT_REPO_ROOT', '/root/repo'), 'samples'),src,symlinks=True)
-with api.Session(qaskip=True) as s:
-    for _ in range(5): s.translate(src, os.path.join(work,"out"), name="samples")
-    pr=cProfile.Profile(); pr.enable()
-    for _ in range(20): s.translate(src, os.path.join(work,"out"), name="samples")
-    pr.disable()
-    st=pstats.Stats(pr); st.sort_stats(sys.argv[1] if len(sys.argv)>1 else 'tottime').print_stats(40)
-shutil.rmtree(work)
+"""cProfile of warm in-process steps of one BASELINE configuration.
+
+usage: python scripts/profile_step.py [config=helm-openshift] [sort=tottime] [steps=20]
+"""
+import cProfile
+import os
+import pstats
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+
+import refconfigs  # noqa: E402
+from move2kube_amd.utils import log  # noqa: E402
+
+
+def main():
+    name = sys.argv[1] if len(sys.argv) > 1 else refconfigs.HEADLINE
+    sort = sys.argv[2] if len(sys.argv) > 2 else "tottime"
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    log.set_quiet()
+    work = tempfile.mkdtemp(prefix="m2k-prof-")
+    run = refconfigs.Run(name, work).prepare()
+    undo = run.apply_env()
+    try:
+        with run.session() as s:
+            for _ in range(5):
+                run.step(s)
+            times = []
+            for _ in range(steps):
+                t0 = time.perf_counter()
+                run.step(s)
+                times.append((time.perf_counter() - t0) * 1e3)
+            times.sort()
+            print("%s: p50 %.3f ms, min %.3f ms over %d steps" % (name, times[len(times) // 2], times[0], steps))
+            pr = cProfile.Profile()
+            pr.enable()
+            for _ in range(steps):
+                run.step(s)
+            pr.disable()
+            pstats.Stats(pr).sort_stats(sort).print_stats(45)
+    finally:
+        undo()
+        shutil.rmtree(work, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
