@@ -718,8 +718,10 @@ std::vector<std::pair<int, py::bytes>> run_commands(const std::vector<std::vecto
 // the GIL released; different directories are written by different threads.  Returns errno per file (0 = ok).  A path
 // listed twice keeps its last content (written once, like sequential writes).
 // ---------------------------------------------------------------------------
+// ioutil.WriteFile(path, data, perm): a new file gets perm & ~umask, an
+// existing one is truncated and keeps its permissions (no chmod).
 static int write_one(const std::string &path, const std::string &data, int mode) {
-  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, static_cast<mode_t>(mode));
   if (fd < 0) return errno;
   const char *p = data.data();
   size_t left = data.size();
@@ -734,7 +736,6 @@ static int write_one(const std::string &path, const std::string &data, int mode)
     p += w;
     left -= static_cast<size_t>(w);
   }
-  (void)::fchmod(fd, static_cast<mode_t>(mode));  // best effort, like os.chmod after write
   if (::close(fd) != 0) return errno;
   return 0;
 }

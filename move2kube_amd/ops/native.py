@@ -93,12 +93,8 @@ def write_files(items, nthreads=8):
     out = []
     for (p, _, md), data in zip(items, datas):
         try:
-            with open(p, "wb") as f:
+            with open(os.open(p, os.O_WRONLY | os.O_CREAT | os.O_TRUNC | os.O_CLOEXEC, md), "wb") as f:
                 f.write(data)
-            try:
-                os.chmod(p, md)
-            except OSError:
-                pass
             out.append(None)
         except OSError as e:
             out.append(e)

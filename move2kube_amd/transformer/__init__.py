@@ -27,6 +27,7 @@ from ..utils.constants import (DEFAULT_DIRECTORY_PERMISSION, DEFAULT_EXECUTABLE_
                                EXPOSE_SELECTOR, settings)
 
 HELM_TEMPLATES_REL_PATH = "templates"
+OPERATOR_SDK_TIMEOUT_S = 600  # the reference waits forever
 CONTAINERS_DIR = "containers"
 KNATIVE_GROUP = "serving.knative.dev"
 
@@ -297,18 +298,23 @@ class K8sTransformer(Transformer):
     def finish_operator(started):
         if started is None:
             return False
-        import subprocess
+        import threading
         p, out, span = started
+        # a blocking waitpid wakes when the tool exits; Popen.wait(timeout=)
+        # polls with sleeps of up to 50 ms.  A timer bounds the run instead.
+        timed_out = []
+        timer = threading.Timer(OPERATOR_SDK_TIMEOUT_S, lambda: (timed_out.append(True), p.kill()))
+        timer.daemon = True
+        timer.start()
         try:
             try:
-                rc = p.wait(timeout=600)
-            except subprocess.TimeoutExpired as e:
-                p.kill()
-                p.wait()
-                log.warning("Error during operator creation : %s", e)
-                return False
+                rc = p.wait()
             finally:
+                timer.cancel()
                 span.__exit__(None, None, None)
+            if timed_out:
+                log.warning("Error during operator creation : timed out after %d seconds", OPERATOR_SDK_TIMEOUT_S)
+                return False
             if rc != 0:
                 out.seek(0)
                 log.warning("Error during operator creation : exit status %d, %s", rc, out.read().decode("utf-8", "replace"))

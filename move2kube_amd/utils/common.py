@@ -100,13 +100,12 @@ def read_text(path):
 
 
 def write_text(path, text, mode=DEFAULT_FILE_PERMISSION):
+    """``ioutil.WriteFile(path, data, mode)``: a new file is created with
+    ``mode & ~umask``; an existing one is truncated and keeps its permissions."""
     data = text.encode("utf-8", errors="surrogateescape") if isinstance(text, str) else text
-    with open(path, "wb") as f:
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC | os.O_CLOEXEC, mode)
+    with open(fd, "wb") as f:
         f.write(data)
-    try:
-        os.chmod(path, mode)
-    except OSError:
-        pass
 
 
 def yaml_attr_present(path, attr):

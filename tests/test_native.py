@@ -78,6 +78,8 @@ def test_python_fallback_distance_is_weighted():
 
 def test_write_files_batch(tmp_path, monkeypatch):
     from move2kube_amd.ops import native as nat
+    umask = os.umask(0o022)
+    os.umask(umask)
     d = tmp_path / "o"
     d.mkdir()
     items = [(str(d / "a.yaml"), "x: 1\n", 0o644), (str(d / "b.sh"), b"#!/bin/sh\n", 0o744),
@@ -86,8 +88,12 @@ def test_write_files_batch(tmp_path, monkeypatch):
     assert errs[:3] == [None, None, None]
     assert isinstance(errs[3], OSError) and errs[3].errno == 2 and str(tmp_path / "missing" / "c") in str(errs[3])
     assert (d / "a.yaml").read_text() == "x: 2\n"               # last write wins
-    assert (d / "a.yaml").stat().st_mode & 0o777 == 0o600
-    assert (d / "b.sh").stat().st_mode & 0o777 == 0o744
+    assert (d / "a.yaml").stat().st_mode & 0o777 == 0o600 & ~umask
+    assert (d / "b.sh").stat().st_mode & 0o777 == 0o744 & ~umask
+    # ioutil.WriteFile: an existing file is truncated and keeps its permissions
+    os.chmod(str(d / "b.sh"), 0o700)
+    assert nat.write_files([(str(d / "b.sh"), "echo\n", 0o644)]) == [None]
+    assert (d / "b.sh").stat().st_mode & 0o777 == 0o700 and (d / "b.sh").read_text() == "echo\n"
     # the pure-Python fallback behaves the same
     monkeypatch.setattr(nat, "_load", lambda: None)
     errs2 = nat.write_files(items)
