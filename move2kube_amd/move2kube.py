@@ -4,7 +4,7 @@
 import os
 
 from . import customizer, metadata, optimizer, parameterizer, qaengine, transformer
-from .ops import native, writebehind
+from .ops import native
 from .models import info, qa
 from .models import plan as plantypes
 from .source import translator as source_translator
@@ -224,8 +224,7 @@ def _emit(p, ir, outpath, qadisablecli):
             log.error("Failed to remove the existing file/directory at the output path %r Error: %r", outpath, str(e))
             log.error("Anything in the output path will get overwritten.")
     try:
-        with writebehind.scope():  # output files written behind the serialisation
-            _emit_artifacts(p, ir, outpath, qadisablecli)
+        _emit_artifacts(p, ir, outpath, qadisablecli)
     finally:
         if remover is not None:
             remover[0].join()

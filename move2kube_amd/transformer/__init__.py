@@ -20,7 +20,7 @@ from .. import assets
 from ..apiresource.base import GOTYPE
 from ..apiresourceset import K8sAPIResourceSet, KnativeAPIResourceSet, TektonAPIResourceSet
 from ..k8s import convert, schema
-from ..ops import writebehind
+from ..ops import native
 from ..models import plan as plantypes
 from ..utils import common, log, trace, yamlio
 from ..utils.constants import (DEFAULT_DIRECTORY_PERMISSION, DEFAULT_EXECUTABLE_PERMISSION, DEFAULT_FILE_PERMISSION,
@@ -72,11 +72,9 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
                 mode = DEFAULT_EXECUTABLE_PERMISSION
                 buildscripts.append(os.path.join(CONTAINERS_DIR, rel))
             batch.append((wp, c.new_files[rel], mode))
-    def report(errs):
-        for (wp, _, _), err in zip(batch, errs):
-            if err is not None:
-                log.warning("Error writing file at %s : %s", wp, err)
-    writebehind.write(batch, report)
+    for (wp, _, _), err in zip(batch, native.write_files(batch)):
+        if err is not None:
+            log.warning("Error writing file at %s : %s", wp, err)
     if manualimages:
         wp = os.path.join(outpath, "Manualimages.md")
         if settings.fixed:
@@ -117,32 +115,13 @@ def serialize_object(obj):
     return yamlio.dumps_k8s(schema.marshal(clean))
 
 
-WRITE_CHUNK = 16  # objects serialised per write-behind batch
-
-
 def write_transformed_objects(path, objs):
-    """One ``<name>-<kind>.yaml`` per object.  Objects are serialised in chunks
-    and every chunk goes to the write-behind writer (``ops/writebehind.py``,
-    native parallel ``write_files``), so the files of one chunk are created
-    while the next is serialised.  The returned list of written paths is
-    complete once the write-behind scope is drained."""
     written = []
     try:
         _mkdir(path)
     except OSError as e:
         log.error("Unable to create directory %s : %s", path, e)
         raise
-
-    def flush(batch, kinds):
-        def report(errs):
-            for (f, _, _), kind, err in zip(batch, kinds, errs):
-                if err is not None:
-                    log.error("Failed to write %r Error: %r", kind, str(err))
-                    continue
-                written.append(f)
-                log.debug("%r created", f)
-        writebehind.write(batch, report)
-
     batch, kinds = [], []
     for obj in objs:
         try:
@@ -154,11 +133,13 @@ def write_transformed_objects(path, objs):
         batch.append((os.path.join(path, "%s-%s.yaml" % (name, obj.get("kind", "").lower())), data,
                       DEFAULT_FILE_PERMISSION))
         kinds.append(obj.get("kind"))
-        if len(batch) == WRITE_CHUNK:
-            flush(batch, kinds)
-            batch, kinds = [], []
-    if batch:
-        flush(batch, kinds)
+    # one batched, parallel write (ops/csrc/m2k_native.cpp:write_files)
+    for (f, _, _), kind, err in zip(batch, kinds, native.write_files(batch)):
+        if err is not None:
+            log.error("Failed to write %r Error: %r", kind, str(err))
+            continue
+        written.append(f)
+        log.debug("%r created", f)
     return written
 
 
@@ -250,7 +231,6 @@ class K8sTransformer(Transformer):
         except OSError as e:
             log.error("Error occurred while writing transformed objects %s", e)
         if self.helm:
-            writebehind.drain()  # operator-sdk reads the complete chart
             operator = self.start_operator(self.name, outpath)
             try:
                 new_images = self._write_containers(outpath)
