@@ -22,6 +22,11 @@ this reports:
   way ``dockerfilecontainerizer.go:76-83`` runs them.  This is a Python
   emulation of the reference's execution model, not the Go tool (no Go
   toolchain here); it is reported for context only;
+* ``samples_yamls_warm_p50_ms`` / ``helm_openshift_over_samples_yamls`` -
+  the headline corpus translated with every default (Yamls, Kubernetes
+  profile, no operator) and the headline configuration's warm p50 over it: the
+  cost of the Helm chart, the Openshift group/versions and the operator-sdk
+  run per service of the same corpus;
 * ``manifest_diff_vs_ref`` - files differing from the reference-derived
   expected tree ``tests/golden/reference/<config>`` (0 = identical), checked
   on the first warm run, every emulation run and every cold run.
@@ -171,11 +176,18 @@ def main():
     ap.add_argument("--json", default=None, help="also write the results here")
     args = ap.parse_args()
     results = {"runs": args.runs, "python_floor_ms": interpreter_floor(args.runs), "configs": []}
+    # the headline corpus with default answers (Yamls, Kubernetes): what the
+    # Helm + Openshift + operator output of the same 15 services costs on top
+    yamls = warm_runs("samples-yamls", args.runs)
+    results["samples_yamls_warm_p50_ms"] = yamls["warm_p50_ms"]
     for name in args.configs.split(","):
         r = bench_config(name, args.runs, args.emulation_runs)
         results["configs"].append(r)
         print(json.dumps(r), flush=True)
-    print(json.dumps({"python_floor_ms": results["python_floor_ms"]}), flush=True)
+    ho = [r for r in results["configs"] if r["config"] == refconfigs.HEADLINE]
+    if ho and yamls["warm_p50_ms"]:
+        results["helm_openshift_over_samples_yamls"] = round(ho[0]["warm_p50_ms"] / yamls["warm_p50_ms"], 3)
+    print(json.dumps({k: v for k, v in results.items() if k != "configs"}), flush=True)
     if args.json:
         with open(args.json, "w") as f:
             json.dump(results, f, indent=1)

@@ -59,6 +59,12 @@ CONFIGS = {
     "helm-openshift": ("samples", "samples", ["helm-openshift-qacache.yaml"], False, None),
 }
 HEADLINE = "helm-openshift"
+# Not a BASELINE configuration: the headline corpus with every default
+# (Yamls, Kubernetes profile, no operator) - the per-service reference point
+# for the cost of the Helm/Openshift output.
+EXTRA_CONFIGS = {
+    "samples-yamls": ("samples", "samples", [], False, None),
+}
 
 
 class Run:
@@ -67,7 +73,7 @@ class Run:
     def __init__(self, name, work):
         self.name = name
         self.work = os.path.abspath(work)
-        layout, src, caches, cnb, collect = CONFIGS[name]
+        layout, src, caches, cnb, collect = CONFIGS[name] if name in CONFIGS else EXTRA_CONFIGS[name]
         self.layout = layout
         self.src = os.path.join(self.work, src)
         self.caches = [os.path.join(CONFIG_FIXTURES, c) for c in caches]
