@@ -57,6 +57,31 @@ class CNBContainerizer(Containerizer):
         container.add_exposed_port(DEFAULT_SERVICE_PORT)
         return container
 
+    def get_target_options_batch(self, plan, paths):
+        """Builders whose detector accepts each path; the uncached (path,
+        builder) probes of the whole batch go to the providers at once."""
+        out = [None] * len(paths)
+        todo = []
+        with _cache_lock:
+            for k, p in enumerate(paths):
+                if p in _cache:
+                    out[k] = list(_cache[p])
+                elif p not in todo:
+                    todo.append(p)
+        if todo:
+            from . import providers
+            pairs = [(p, b) for p in todo for b in self.builders]
+            ok = providers.is_builder_supported_batch(pairs)
+            nb = len(self.builders)
+            with _cache_lock:
+                for j, p in enumerate(todo):
+                    _cache[p] = [b for b, good in zip(self.builders, ok[j * nb:(j + 1) * nb]) if good]
+            with _cache_lock:
+                for k, p in enumerate(paths):
+                    if out[k] is None:
+                        out[k] = list(_cache[p])
+        return out
+
     def get_all_buildpacks(self):
         from . import providers
         return providers.get_all_buildpacks(self.builders)

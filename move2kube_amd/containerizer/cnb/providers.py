@@ -218,6 +218,42 @@ class DockerAPIProvider:
 # podman CLI
 # ---------------------------------------------------------------------------
 
+def parallel_map(fn, items, workers=None):
+    """[fn(x) for x in items] on up to ``workers`` threads (child processes
+    run concurrently; the GIL is free while they are waited for).  An
+    exception from fn is returned in its slot, not raised."""
+    items = list(items)
+    if workers is None:
+        workers = settings.workers
+    out = [None] * len(items)
+    if len(items) <= 1 or workers <= 1:
+        for k, x in enumerate(items):
+            try:
+                out[k] = fn(x)
+            except Exception as e:  # noqa: BLE001
+                out[k] = e
+        return out
+    it = iter(range(len(items)))
+    lock = threading.Lock()
+
+    def worker():
+        while True:
+            with lock:
+                k = next(it, None)
+            if k is None:
+                return
+            try:
+                out[k] = fn(items[k])
+            except Exception as e:  # noqa: BLE001
+                out[k] = e
+    threads = [threading.Thread(target=worker, daemon=True) for _ in range(min(workers, len(items)))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    return out
+
+
 def _run(cmd, timeout=600):
     return subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
                           timeout=timeout)
@@ -260,12 +296,30 @@ class ContainerRuntimeProvider:
         self.available.add(builder)
         return True
 
+    def _detect_cmd(self, path, builder):
+        return [self.runtime, "run", "--rm", "--storage-driver=vfs", "-v", os.path.abspath(path) + ":/workspace",
+                builder, "/cnb/lifecycle/detector"]
+
     def is_builder_supported(self, path, builder):
         if not self.is_builder_available(builder):
             raise ProviderError("Builder image not available : %s" % builder)
-        p = _run([self.runtime, "run", "--rm", "--storage-driver=vfs", "-v", os.path.abspath(path) + ":/workspace",
-                  builder, "/cnb/lifecycle/detector"])
+        p = _run(self._detect_cmd(path, builder))
         return p.returncode == 0
+
+    def is_builder_supported_batch(self, pairs):
+        """[(path, builder)] -> [True/False, or None where this provider cannot
+        answer].  Builder availability is settled once per builder (it may
+        pull); the detector containers then run concurrently - the reference
+        runs one at a time, each a container start."""
+        out = [None] * len(pairs)
+        runnable = []
+        for i, (path, builder) in enumerate(pairs):
+            if self.is_builder_available(builder):
+                runnable.append(i)
+        results = parallel_map(lambda i: _run(self._detect_cmd(*pairs[i])).returncode == 0, runnable)
+        for i, r in zip(runnable, results):
+            out[i] = None if isinstance(r, (OSError, subprocess.SubprocessError)) else r
+        return out
 
     def get_all_buildpacks(self, builders):
         rt = self.get_runtime()
@@ -456,6 +510,44 @@ def is_builder_supported(path, builder):
             continue
     _log_not_supported()
     return False
+
+
+def is_builder_supported_batch(pairs):
+    """``[is_builder_supported(path, builder) for path, builder in pairs]``:
+    each pair goes down the provider chain until a provider answers; a
+    provider with a batch method answers its pairs concurrently."""
+    _log_long_wait()
+    results = [False] * len(pairs)
+    todo = list(range(len(pairs)))
+    for p in providers():
+        if not todo:
+            break
+        batch = getattr(p, "is_builder_supported_batch", None)
+        if batch is not None:
+            try:
+                got = batch([pairs[i] for i in todo])
+            except (ProviderError, OSError, subprocess.SubprocessError, ValueError, KeyError) as e:
+                log.debug("CNB provider %s: %s", type(p).__name__, e)
+                continue
+            rest = []
+            for i, r in zip(todo, got):
+                if r is None:
+                    rest.append(i)
+                else:
+                    results[i] = r
+            todo = rest
+            continue
+        rest = []
+        for i in todo:
+            try:
+                results[i] = p.is_builder_supported(*pairs[i])
+            except (ProviderError, OSError, subprocess.SubprocessError, ValueError, KeyError) as e:
+                log.debug("CNB provider %s: %s", type(p).__name__, e)
+                rest.append(i)
+        todo = rest
+    if todo:
+        _log_not_supported()
+    return results
 
 
 def get_all_buildpacks(builders):

@@ -130,3 +130,49 @@ def test_chain_falls_through_to_first_working_provider(monkeypatch, tmp_path):
         assert providers.is_builder_supported(str(app), "b") is True  # docker API fails -> podman answers
     finally:
         providers.reset_providers()
+
+
+_SLOW_PODMAN = """#!/bin/sh
+case "$*" in
+  "run --storage-driver=vfs --rm hello-world") exit 0 ;;
+  "--storage-driver=vfs images -q "*) [ "$4" = missing ] || echo 5f1b ;;
+  "pull --storage-driver=vfs "*) exit 1 ;;
+  "run --rm --storage-driver=vfs -v "*" /cnb/lifecycle/detector")
+    src="${5%:/workspace}"
+    touch "$LOGDIR/running.$$"
+    sleep 0.3
+    ls "$LOGDIR" | grep -c '^running' > "$LOGDIR/seen.$$"
+    rm -f "$LOGDIR/running.$$"
+    [ -f "$src/package.json" ] ;;
+  *) exit 1 ;;
+esac
+"""
+
+
+def test_batched_probes_run_concurrently_and_match_sequential(monkeypatch, tmp_path):
+    """``is_builder_supported_batch`` gives the per-pair answers of the
+    sequential chain, with the detector containers running at the same time;
+    a builder that cannot be pulled falls through the chain to False."""
+    bindir, logdir = tmp_path / "bin", tmp_path / "log"
+    bindir.mkdir()
+    logdir.mkdir()
+    (bindir / "podman").write_text(_SLOW_PODMAN)
+    os.chmod(str(bindir / "podman"), 0o755)
+    monkeypatch.setenv("PATH", str(bindir) + os.pathsep + "/usr/bin:/bin")
+    monkeypatch.setenv("LOGDIR", str(logdir))
+    monkeypatch.setenv("M2K_DISABLE_CNB", "0")
+    monkeypatch.setattr(providers, "DOCKER_SOCK", str(tmp_path / "nosock"))
+    monkeypatch.setattr(providers, "providers", lambda: [providers.ContainerRuntimeProvider()])
+    apps = []
+    for i in range(3):
+        a = tmp_path / ("app%d" % i)
+        a.mkdir()
+        if i != 1:
+            (a / "package.json").write_text("{}")
+        apps.append(str(a))
+    pairs = [(a, b) for a in apps for b in ("b1", "b2", "missing")]
+    got = providers.is_builder_supported_batch(pairs)
+    assert got == [True, True, False, False, False, False, True, True, False]
+    seen = [int((logdir / f).read_text()) for f in os.listdir(str(logdir)) if f.startswith("seen.")]
+    assert len(seen) == 6 and max(seen) >= 2
+    assert [providers.is_builder_supported(a, b) for a, b in pairs] == got
