@@ -43,6 +43,7 @@ def fake_cnb(monkeypatch):
     def supported(path, builder):
         return any(os.path.isfile(os.path.join(path, m)) for m in ("package.json", "pom.xml"))
     monkeypatch.setattr(providers, "is_builder_supported", supported)
+    monkeypatch.setattr(providers, "is_builder_supported_batch", lambda pairs: [supported(p, b) for p, b in pairs])
 
 
 @pytest.fixture
