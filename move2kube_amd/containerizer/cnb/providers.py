@@ -326,9 +326,12 @@ class ContainerRuntimeProvider:
         if rt is None:
             raise ProviderError("Container runtime not supported in this instance")
         out = {}
-        for b in builders:
-            p = _run([rt, "inspect", "--storage-driver=vfs", "--format",
-                      '{{ index .Config.Labels "' + ORDER_LABEL + '"}}', b])
+        # one `inspect` per builder, concurrently
+        procs = parallel_map(lambda b: _run([rt, "inspect", "--storage-driver=vfs", "--format",
+                                             '{{ index .Config.Labels "' + ORDER_LABEL + '"}}', b]), builders)
+        for b, p in zip(builders, procs):
+            if isinstance(p, Exception):
+                raise p
             if p.returncode != 0:
                 continue
             out[b] = get_builders_from_label(p.stdout.decode())
