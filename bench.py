@@ -73,7 +73,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default=refconfigs.HEADLINE, choices=sorted(refconfigs.CONFIGS))
+    ap.add_argument("--config", default=refconfigs.HEADLINE,
+                    choices=sorted(refconfigs.CONFIGS) + sorted(refconfigs.EXTRA_CONFIGS))
     ap.add_argument("--check-runs", type=int, default=3,
                     help="warm/cold runs per configuration in the untimed per-config check (0 = skip)")
     ap.add_argument("--keep", action="store_true", help="keep the work directory")
