@@ -28,6 +28,9 @@ ORDER_LABEL = "io.buildpacks.buildpack.order"
 PULL_TIMEOUT_S = 1800
 RUN_TIMEOUT_S = 600
 DOCKER_SOCK = "/var/run/docker.sock"
+# detector containers started at once (each is a builder image with its own
+# memory footprint; the reference runs one at a time)
+CONTAINER_PARALLEL = int(os.environ.get("M2K_CNB_PARALLEL", "4") or 4)
 
 _warned_not_supported = False
 _warned_long_wait = False
@@ -316,7 +319,8 @@ class ContainerRuntimeProvider:
         for i, (path, builder) in enumerate(pairs):
             if self.is_builder_available(builder):
                 runnable.append(i)
-        results = parallel_map(lambda i: _run(self._detect_cmd(*pairs[i])).returncode == 0, runnable)
+        results = parallel_map(lambda i: _run(self._detect_cmd(*pairs[i])).returncode == 0, runnable,
+                               min(settings.workers, CONTAINER_PARALLEL))
         for i, r in zip(runnable, results):
             out[i] = None if isinstance(r, (OSError, subprocess.SubprocessError)) else r
         return out
