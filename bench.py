@@ -51,6 +51,29 @@ def _dist_env():
     return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def _workdir_root(choice):
+    """Where the inputs and output trees of the run live.  ``auto``: a tmpfs
+    (``/dev/shm``) when one is writable with room to spare, else the default
+    temp dir.  Every step deletes the previous output tree and writes a new one
+    (~500 file creations and deletions per step); on the GPU hosts' ext4 /
+    overlay scratch disks (mounted with ``discard``) that churn builds a
+    backlog that slows every later run on the machine - a 1-rank step went
+    from 20 to 50 ms after a few multi-rank runs - so a disk-backed number
+    depends on what ran before.  ``disk`` forces the default temp dir."""
+    if choice == "disk":
+        return None, "disk"
+    if choice != "auto":
+        return choice, "given"
+    shm = "/dev/shm"
+    try:
+        st = os.statvfs(shm)
+        if os.access(shm, os.W_OK) and st.f_bavail * st.f_frsize >= (512 << 20):
+            return shm, "tmpfs"
+    except OSError:
+        pass
+    return None, "disk"
+
+
 def tree_files(root):
     return refconfigs.tree_files(root)
 
@@ -78,6 +101,8 @@ def main():
     ap.add_argument("--check-runs", type=int, default=3,
                     help="warm/cold runs per configuration in the untimed per-config check (0 = skip)")
     ap.add_argument("--keep", action="store_true", help="keep the work directory")
+    ap.add_argument("--workdir", default="auto",
+                    help="root for the input copies and output trees: auto (tmpfs if available), disk, or a path")
     args = ap.parse_args()
 
     world, rank, local_rank = _dist_env()
@@ -101,6 +126,9 @@ def main():
 
     from move2kube_amd.utils import log
     log.set_quiet()
+    root, workdir_fs = _workdir_root(args.workdir)
+    if root is not None:
+        tempfile.tempdir = root  # also for the per-configuration checks below
 
     work = tempfile.mkdtemp(prefix="m2k-bench-r%d-" % rank)
     run = refconfigs.Run(args.config, work).prepare()
@@ -163,8 +191,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "n/a",
-            "data": "reference samples/ corpus (%d services), in-process plan+curate+translate per step; "
-                    "stand-ins for operator-sdk; no container engine" % n_services,
+            "data": "reference samples/ corpus (%d services), in-process plan+curate+translate per step, "
+                    "output tree rewritten each step on %s; stand-ins for operator-sdk; no container engine"
+                    % (n_services, workdir_fs),
+            "workdir_fs": workdir_fs,
             "manifest_diff_vs_ref": total_diff,
             "manifest_diff_vs_ref_headline": diff_headline,
             "per_config": per_config,
