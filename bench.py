@@ -51,29 +51,6 @@ def _dist_env():
     return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
-def _workdir_root(choice):
-    """Where the inputs and output trees of the run live.  ``auto``: a tmpfs
-    (``/dev/shm``) when one is writable with room to spare, else the default
-    temp dir.  Every step deletes the previous output tree and writes a new one
-    (~500 file creations and deletions per step); on the GPU hosts' ext4 /
-    overlay scratch disks (mounted with ``discard``) that churn builds a
-    backlog that slows every later run on the machine - a 1-rank step went
-    from 20 to 50 ms after a few multi-rank runs - so a disk-backed number
-    depends on what ran before.  ``disk`` forces the default temp dir."""
-    if choice == "disk":
-        return None, "disk"
-    if choice != "auto":
-        return choice, "given"
-    shm = "/dev/shm"
-    try:
-        st = os.statvfs(shm)
-        if os.access(shm, os.W_OK) and st.f_bavail * st.f_frsize >= (512 << 20):
-            return shm, "tmpfs"
-    except OSError:
-        pass
-    return None, "disk"
-
-
 def tree_files(root):
     return refconfigs.tree_files(root)
 
@@ -126,7 +103,7 @@ def main():
 
     from move2kube_amd.utils import log
     log.set_quiet()
-    root, workdir_fs = _workdir_root(args.workdir)
+    root, workdir_fs = refconfigs.workdir_root(args.workdir)
     if root is not None:
         tempfile.tempdir = root  # also for the per-configuration checks below
 

@@ -174,8 +174,13 @@ def main():
                     help="runs of the Python emulation of the reference's fork-per-detector model (0 = skip)")
     ap.add_argument("--configs", default=",".join(refconfigs.CONFIGS))
     ap.add_argument("--json", default=None, help="also write the results here")
+    ap.add_argument("--workdir", default="auto",
+                    help="root for inputs and outputs: auto (tmpfs if available), disk, or a path (see bench.py)")
     args = ap.parse_args()
-    results = {"runs": args.runs, "python_floor_ms": interpreter_floor(args.runs), "configs": []}
+    root, workdir_fs = refconfigs.workdir_root(args.workdir)
+    if root is not None:
+        tempfile.tempdir = root
+    results = {"runs": args.runs, "workdir_fs": workdir_fs, "python_floor_ms": interpreter_floor(args.runs), "configs": []}
     # the headline corpus with default answers (Yamls, Kubernetes): what the
     # Helm + Openshift + operator output of the same 15 services costs on top
     yamls = warm_runs("samples-yamls", args.runs)

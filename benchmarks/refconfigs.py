@@ -175,6 +175,29 @@ class Run:
         return self.out
 
 
+def workdir_root(choice):
+    """Where the inputs and output trees of the run live.  ``auto``: a tmpfs
+    (``/dev/shm``) when one is writable with room to spare, else the default
+    temp dir.  Every step deletes the previous output tree and writes a new one
+    (~500 file creations and deletions per step); on the GPU hosts' ext4 /
+    overlay scratch disks (mounted with ``discard``) that churn builds a
+    backlog that slows every later run on the machine - a 1-rank step went
+    from 20 to 50 ms after a few multi-rank runs - so a disk-backed number
+    depends on what ran before.  ``disk`` forces the default temp dir."""
+    if choice == "disk":
+        return None, "disk"
+    if choice != "auto":
+        return choice, "given"
+    shm = "/dev/shm"
+    try:
+        st = os.statvfs(shm)
+        if os.access(shm, os.W_OK) and st.f_bavail * st.f_frsize >= (512 << 20):
+            return shm, "tmpfs"
+    except OSError:
+        pass
+    return None, "disk"
+
+
 def tree_files(root):
     out = {}
     for dp, _dn, fns in os.walk(root):
