@@ -83,6 +83,7 @@ class APIResource:
         self.handler = handler
         self.cluster = cluster
         self.cached = None
+        self._index = None  # resource key -> position in cached (first occurrence)
 
     def set_cluster_context(self, cluster):
         self.cluster = cluster
@@ -121,13 +122,22 @@ class APIResource:
             return False
         if self.cached is None:
             self.cached = list(sup)
-            return True
-        for s in sup:
+            self._index = {}
             for i, c in enumerate(self.cached):
-                if _same_resource(c, s):
-                    self.cached[i] = s
-                    break
+                k = _resource_key(c)
+                if k is not None:
+                    self._index.setdefault(k, i)
+            return True
+        # merge: an object replaces the first cached one with the same
+        # namespace+name and group/kind (apiresource.go:86-101), else appends
+        for s in sup:
+            k = _resource_key(s)
+            i = self._index.get(k) if k is not None else None
+            if i is not None:
+                self.cached[i] = s
             else:
+                if k is not None:
+                    self._index[k] = len(self.cached)
                 self.cached.append(s)
         return True
 
@@ -141,6 +151,13 @@ def _group_kind(obj):
     gv = obj.get("apiVersion", "")
     group = gv.split("/", 1)[0] if "/" in gv else ""
     return group, obj.get("kind", "")
+
+
+def _resource_key(obj):
+    """What ``_same_resource`` compares, or None for an object without a name
+    (such an object never matches another)."""
+    oid = _object_id(obj)
+    return None if oid == "" else (oid, _group_kind(obj))
 
 
 def _same_resource(a, b):
