@@ -233,48 +233,86 @@ def _emit(p, ir, outpath, qadisablecli):
 
 
 def _emit_artifacts(p, ir, outpath, qadisablecli):
+    # For a Helm chart the main transformer starts operator-sdk once the chart
+    # is written and waits for it at the end; the compose and CI/CD files and
+    # the QA cache do not feed the chart, so they are written in that wait
+    # (same bytes, same files).  Every question is asked before the chart.
+    overlap = [] if p.kubernetes.artifact_type == plantypes.HELM else None
+
+    def later(fn):
+        if overlap is None:
+            fn()
+        else:
+            overlap.append(fn)
+
     dct = transformer.ComposeTransformer()
+
+    def write_compose():
+        try:
+            dct.write_objects(outpath)
+        except Exception as e:  # noqa: BLE001
+            if isinstance(e, log.FatalError):
+                raise
+            log.error("Unable to write docker compose objects : %s", e)
     try:
         with trace.span("ComposeTransformer", "transform"):
             dct.transform(ir)
-            dct.write_objects(outpath)
     except Exception as e:  # noqa: BLE001
         if isinstance(e, log.FatalError):
             raise
         log.error("Unable to write docker compose objects : %s", e)
+    else:
+        later(write_compose)
 
-    ir = customizer.customize(ir)
-    log.debug("Total storages customized : %d", len(ir.storages))
-    if p.kubernetes.artifact_type == plantypes.HELM:
-        ir = parameterizer.parameterize(ir)
+    try:
+        ir = customizer.customize(ir)
+        log.debug("Total storages customized : %d", len(ir.storages))
+        if p.kubernetes.artifact_type == plantypes.HELM:
+            ir = parameterizer.parameterize(ir)
 
-    if any(c.new for c in ir.containers):
-        cicd = transformer.CICDTransformer()
+        if any(c.new for c in ir.containers):
+            cicd = transformer.CICDTransformer()
+
+            def write_cicd():
+                try:
+                    cicd.write_objects(outpath)
+                except Exception as e:  # noqa: BLE001
+                    if isinstance(e, log.FatalError):
+                        raise
+                    log.error("Unable to write the CI/CD artifacts to files. Error: %r", str(e))
+            try:
+                with trace.span("CICDTransformer", "transform"):
+                    cicd.transform(ir)
+            except Exception as e:  # noqa: BLE001
+                if isinstance(e, log.FatalError):
+                    raise
+                log.error("Unable to write the CI/CD artifacts to files. Error: %r", str(e))
+            else:
+                later(write_cicd)
+
+        ir.add_copy_sources_warning = qadisablecli
+        t = transformer.get_transformer(ir)
         try:
-            with trace.span("CICDTransformer", "transform"):
-                cicd.transform(ir)
-                cicd.write_objects(outpath)
+            with trace.span(type(t).__name__ + ".transform", "transform"):
+                t.transform(ir)
         except Exception as e:  # noqa: BLE001
             if isinstance(e, log.FatalError):
                 raise
-            log.error("Unable to write the CI/CD artifacts to files. Error: %r", str(e))
-
-    ir.add_copy_sources_warning = qadisablecli
-    t = transformer.get_transformer(ir)
-    try:
-        with trace.span(type(t).__name__ + ".transform", "transform"):
-            t.transform(ir)
-    except Exception as e:  # noqa: BLE001
-        if isinstance(e, log.FatalError):
-            raise
-        log.fatal("Error during translate. Error: %r", str(e))
-    try:
-        with trace.span(type(t).__name__ + ".write_objects", "transform"):
-            t.write_objects(outpath)
-    except Exception as e:  # noqa: BLE001
-        if isinstance(e, log.FatalError):
-            raise
-        log.fatal("Unable to write objects Error: %r", str(e))
+            log.fatal("Error during translate. Error: %r", str(e))
+        if overlap is not None:
+            overlap.append(qaengine.flush_write_cache)
+            t.overlap_work = overlap
+        try:
+            with trace.span(type(t).__name__ + ".write_objects", "transform"):
+                t.write_objects(outpath)
+        except Exception as e:  # noqa: BLE001
+            if isinstance(e, log.FatalError):
+                raise
+            log.fatal("Unable to write objects Error: %r", str(e))
+    finally:
+        # deferred writes not yet run (no Helm wait reached, or an error before it)
+        while overlap:
+            overlap.pop(0)()
     log.info("Execution completed")
 
 

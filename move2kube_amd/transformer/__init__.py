@@ -169,6 +169,7 @@ class K8sTransformer(Transformer):
         self.ignore_unsupported_kinds = False  # never set by the reference's Transform
         self.exposed_service_paths = {}
         self.add_copy_sources_warning = False
+        self.overlap_work = []  # callables run while operator-sdk runs (Helm only)
 
     def transform(self, ir):
         log.debug("Starting Kubernetes transform")
@@ -214,8 +215,9 @@ class K8sTransformer(Transformer):
     def write_objects(self, outpath):
         """``Kubernetes.WriteObjects`` (k8stransformer.go:100-146).  For a Helm
         chart the operator-sdk run (seconds for the real tool) starts as soon
-        as the chart is complete and overlaps the container build files and the
-        readme, which it does not read; it is waited for before returning."""
+        as the chart is complete and overlaps the container build files, the
+        readme and ``overlap_work`` (the caller's deferred writes), none of
+        which it reads; it is waited for before returning."""
         if not self.helm:
             new_images = self._write_containers(outpath)
         artifacts = os.path.join(outpath, self.name)
@@ -235,6 +237,8 @@ class K8sTransformer(Transformer):
             try:
                 new_images = self._write_containers(outpath)
                 self.write_readme(self.name, new_images, self.helm, self.add_copy_sources_warning, outpath)
+                while self.overlap_work:  # shared with the caller: what is popped has run
+                    self.overlap_work.pop(0)()
             finally:
                 self.finish_operator(operator)
             return
