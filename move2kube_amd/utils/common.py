@@ -331,8 +331,11 @@ def find_common_directory(paths):
 
 
 def copy_file(dst, src):
-    shutil.copyfile(src, dst)
-    os.chmod(dst, DEFAULT_FILE_PERMISSION)
+    """``CopyFile`` (utils.go:587-615): the destination is opened like
+    ``os.OpenFile(dst, O_WRONLY|O_CREATE|O_TRUNC, DefaultFilePermission)``."""
+    with open(src, "rb") as fsrc, open(os.open(dst, os.O_WRONLY | os.O_CREAT | os.O_TRUNC | os.O_CLOEXEC,
+                                               DEFAULT_FILE_PERMISSION), "wb") as fdst:
+        shutil.copyfileobj(fsrc, fdst)
 
 
 def unique_strings(xs):

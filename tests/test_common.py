@@ -155,3 +155,20 @@ def test_untar_reference_tarstring(tmp_path):
     tarutil.untar_string(data["untar_a_valid_tarstring"], str(tmp_path))
     names = sorted(os.path.relpath(os.path.join(dp, f), str(tmp_path)) for dp, _, fs in os.walk(str(tmp_path)) for f in fs)
     assert names
+
+
+def test_copy_file_like_go_copyfile(tmp_path):
+    """``CopyFile`` (utils.go:587-615): new destination gets 0644 & ~umask; an
+    existing one is truncated and keeps its mode."""
+    umask = os.umask(0o022)
+    os.umask(umask)
+    src = tmp_path / "src"
+    src.write_bytes(b"abc" * 1000)
+    dst = tmp_path / "dst"
+    common.copy_file(str(dst), str(src))
+    assert dst.read_bytes() == src.read_bytes()
+    assert dst.stat().st_mode & 0o777 == 0o644 & ~umask
+    os.chmod(str(dst), 0o600)
+    src.write_bytes(b"x")
+    common.copy_file(str(dst), str(src))
+    assert dst.read_bytes() == b"x" and dst.stat().st_mode & 0o777 == 0o600
