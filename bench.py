@@ -88,7 +88,7 @@ def main():
     have_cuda = torch.cuda.is_available()
     if have_cuda:
         torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
-    if world > 1 or "MASTER_ADDR" in os.environ:  # under torchrun, also with one rank: the same RCCL path as N>1
+    if world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ):  # launched by torchrun, one rank too
         import torch.distributed as dist
         dist.init_process_group(backend="nccl" if have_cuda else "gloo")
 
