@@ -27,34 +27,53 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _ASSETS_SRC = os.path.join(os.path.dirname(_HERE), "assets", "m2kassets")
 
 
-def _exists_file(src, name):
+class Dir:
+    """One target directory of a detect batch: its index is looked up once for
+    all the detectors run against it (they run back to back)."""
+
+    __slots__ = ("src", "idx", "_full")
+
+    def __init__(self, src):
+        self.src = src
+        self.idx = fsindex.peek_index(src)  # never walks
+        self._full = False
+
+    def index(self):
+        """``fsindex.get_index(src)`` (walks if the scope does not cover src);
+        None when src cannot be listed."""
+        if self._full is False:
+            try:
+                self._full = fsindex.get_index(self.src)
+            except (OSError, FileNotFoundError):
+                self._full = None
+        return self._full
+
+
+def _exists_file(d, name):
     """``test -f "$src/name"``, answered from the scope's directory index when
     it covers ``src`` (the plan/translate scopes always do) - no stat per
     (detector x directory) pair; symlinks and unknowns still go to the FS."""
-    idx = fsindex.peek_index(src)
+    idx = d.idx
     if idx is not None:
         k = idx.child_kind(name)
         if k == fsindex.FILE:
             return True
         if k in (fsindex.MISSING, fsindex.DIR, fsindex.OTHER):
             return False
-    return os.path.isfile(os.path.join(src, name))
+    return os.path.isfile(os.path.join(d.src, name))
 
 
-def _find_any(src, pattern):
+def _find_any(d, pattern):
     """``find "$src"/. -name pattern -print | head -n1 | wc -l`` == 1."""
-    try:
-        idx = fsindex.get_index(src)
-    except (OSError, FileNotFoundError):
-        return False
-    return idx.has_match(pattern)
+    idx = d.index()
+    return idx is not None and idx.has_match(pattern)
 
 
-def _find_main(src):
+def _find_main(d):
     """``grep -lRe __main__ "$src" | awk '/.py$/' | head -n1`` -> relative path."""
-    try:
-        idx = fsindex.get_index(src)
-    except (OSError, FileNotFoundError):
+    src = d.src
+    idx = d.index()
+    if idx is None:
         return ""
     for p, k in zip(idx.paths, idx.kinds):
         if k == fsindex.DIR:
@@ -83,20 +102,20 @@ _FAIL = (1, b"")
 
 
 def _simple(marker, out):
-    def fn(src):
-        return _ok(out) if _exists_file(src, marker) else _FAIL
+    def fn(d):
+        return _ok(out) if _exists_file(d, marker) else _FAIL
     return fn
 
 
 def _recursive(pattern, out):
-    def fn(src):
-        return _ok(out) if _find_any(src, pattern) else _FAIL
+    def fn(d):
+        return _ok(out) if _find_any(d, pattern) else _FAIL
     return fn
 
 
 def _war(port):
-    def fn(src):
-        idx = fsindex.peek_index(src)
+    def fn(d):
+        src, idx = d.src, d.idx
         if idx is not None and idx.kinds and idx.kinds[0] == fsindex.DIR:
             wars = idx.children_matching("*.war")
         else:
@@ -114,33 +133,33 @@ def _war(port):
 _PY_MARKERS = ("requirements.txt", "setup.py", "environment.yml", "Pipfile")
 
 
-def _python_df(src):
+def _python_df(d):
     for m in _PY_MARKERS:
-        if _exists_file(src, m):
-            return _ok('{"main_script_rel_path": "%s", "app_name": "app", "port": 8080}' % _find_main(src))
+        if _exists_file(d, m):
+            return _ok('{"main_script_rel_path": "%s", "app_name": "app", "port": 8080}' % _find_main(d))
     return _FAIL
 
 
-def _python_s2i(src):
+def _python_s2i(d):
     for m in _PY_MARKERS:
-        if _exists_file(src, m):
+        if _exists_file(d, m):
             return _ok('{"builder": "%s", "app_file": "%s", "app_name": "app", "port": 8080}'
-                       % ("registry.access.redhat.com/rhscl/python-36-rhel7:latest", _find_main(src)))
+                       % ("registry.access.redhat.com/rhscl/python-36-rhel7:latest", _find_main(d)))
     return _FAIL
 
 
-def _golang_s2i(src):
-    if not _exists_file(src, "go.mod") and not _find_any(src, "*.go"):
+def _golang_s2i(d):
+    if not _exists_file(d, "go.mod") and not _find_any(d, "*.go"):
         return _FAIL
     return _ok('{"builder": "%s", "port": 8080}\n' % "registry.access.redhat.com/ubi8/go-toolset:latest")
 
 
-def _java_s2i(src):
-    if _exists_file(src, "build.gradle") or _exists_file(src, "build.xml"):
+def _java_s2i(d):
+    if _exists_file(d, "build.gradle") or _exists_file(d, "build.xml"):
         return _FAIL
-    if _exists_file(src, "pom.xml"):
+    if _exists_file(d, "pom.xml"):
         return _ok('{"builder": "%s", "port": 8080}\n' % "registry.access.redhat.com/jboss-eap-6/eap64-openshift:latest")
-    if not _find_any(src, "*.java"):
+    if not _find_any(d, "*.java"):
         return _FAIL
     return _ok('{"builder": "%s", "port": 8080}\n'
                % "registry.access.redhat.com/redhat-openjdk-18/openjdk18-openshift:latest")

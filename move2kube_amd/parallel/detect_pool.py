@@ -74,6 +74,7 @@ def _run_detect_jobs(jobs):
         spawn, spawn_idx = [], []
         fns = {}
         shared = {}  # (code, stdout bytes) -> one read-only DetectResult
+        cur = None  # builtin_detect.Dir of the current target (jobs come grouped by target)
         for k, job in enumerate(todo):
             d, script, target = job
             fn = fns.get((d, script), False)
@@ -83,7 +84,9 @@ def _run_detect_jobs(jobs):
                 spawn.append(job)
                 spawn_idx.append(k)
                 continue
-            key = fn(target)
+            if cur is None or cur.src != target:
+                cur = builtin_detect.Dir(target)
+            key = fn(cur)
             r = shared.get(key)
             if r is None:
                 r = shared[key] = DetectResult(key[0], key[1].decode("utf-8", "replace"))
