@@ -8,13 +8,14 @@ import sys
 from . import assets, move2kube, qaengine
 from .containerizer import cnb
 from .models import plan as plantypes
-from .utils import sshkeys, yamlio
+from .utils import fsindex, sshkeys, yamlio
 from .utils.constants import QA_CACHE_FILE, settings
 
 
 def reset_state():
     """Forget engines, caches and provider probes from a previous run."""
     qaengine.reset()
+    fsindex.drop_kept()
     cnb.reset_cache()
     providers = sys.modules.get("move2kube_amd.containerizer.cnb.providers")
     if providers is not None:
@@ -67,7 +68,9 @@ class Session:
 
     def _translate(self, src, outdir, name, plan, curate):
         if plan is None:
-            p = move2kube.create_plan(os.path.abspath(src), name)
+            src = os.path.abspath(src)
+            p = move2kube.create_plan(src, name, keep_index=fsindex.handoff_allowed(
+                src, os.path.join(os.path.abspath(outdir), name)))
         else:
             p = plan if isinstance(plan, plantypes.Plan) else plantypes.read_plan(plan)
         out = os.path.join(os.path.abspath(outdir), p.name)

@@ -11,7 +11,7 @@ import sys
 
 from .. import assets, move2kube, qaengine
 from ..models import plan as plantypes
-from ..utils import log, yamlio
+from ..utils import fsindex, log, yamlio
 from ..utils.constants import (APP_NAME_SHORT, DEFAULT_DIRECTORY_PERMISSION, DEFAULT_PLAN_FILE, DEFAULT_PROJECT_NAME,
                                QA_CACHE_FILE, settings)
 
@@ -75,7 +75,8 @@ def translate_handler(a):
                       "stat %s: no such file or directory" % planfile)
         check_source_path(srcpath)
         log.debug("Creating a new plan.")
-        p = move2kube.create_plan(srcpath, a.name)
+        p = move2kube.create_plan(srcpath, a.name,
+                                  keep_index=fsindex.handoff_allowed(srcpath, os.path.join(outpath, a.name)))
         outpath = os.path.join(outpath, p.name)
         check_output_path(outpath)
         create_output_directory_and_cache_file(outpath)

@@ -18,14 +18,15 @@ def collect(input_path, output_path, annotations=()):
     collector.collect(input_path, output_path, list(annotations))
 
 
-def create_plan(input_path, project_name):
+def create_plan(input_path, project_name, keep_index=False):
     """``CreatePlan`` (planner.go:30-64): every source translator proposes
     service options, then metadata loaders annotate the plan.  All planners
-    share one cached directory index of ``input_path``."""
+    share one cached directory index of ``input_path``; ``keep_index`` hands
+    it (and the detector results) to the translate of the same command."""
     p = plantypes.new_plan()
     p.name = project_name
     p.root_dir = input_path
-    with fsindex.scope(), trace.span("plan", "command"):
+    with fsindex.scope(keep_for=input_path if keep_index else None), trace.span("plan", "command"):
         log.info("Planning Translation")
         for t in source_translator.get_source_loaders():
             log.info("[%r] Planning translation", t)
@@ -151,8 +152,9 @@ def translate(p, outpath, qadisablecli=False):
 
 def _translate(p, outpath, qadisablecli):
     # source -> IR and metadata loading only read the source tree: one shared
-    # directory index for all translators/containerizers of this stage
-    with fsindex.scope():
+    # directory index for all translators/containerizers of this stage (the
+    # plan's, when the same command just planned this tree)
+    with fsindex.scope(adopt=p.root_dir):
         ir = _to_ir(p)
     ir = optimizer.optimize(ir)
     log.debug("Total services optimized : %d", len(ir.services))

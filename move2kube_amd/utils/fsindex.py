@@ -39,17 +39,44 @@ def _cache():
 
 
 @contextlib.contextmanager
-def scope():
-    """Reuse file indexes for the duration of the block (nestable)."""
+def scope(keep_for=None, adopt=None):
+    """Reuse file indexes for the duration of the block (nestable).
+
+    ``keep_for=root``: when this (outermost) scope ends, its listings and
+    scoped caches are kept for one later ``scope(adopt=root)`` on this thread
+    - the plan and the translate of one ``translate`` command, which walk the
+    same unchanged tree (see :func:`handoff_allowed`).  Anything kept and not
+    adopted is dropped by the next keeping scope or :func:`drop_kept`."""
     prev = _cache()
     if prev is None:
-        _local.cache = {}
+        kept = getattr(_local, "kept", None)
+        _local.kept = None
+        if adopt is not None and kept is not None and kept[0] == adopt:
+            _local.cache, _local.aux = kept[1], kept[2]
+        else:
+            _local.cache = {}
     try:
         yield
     finally:
         if prev is None:
+            if keep_for is not None:
+                _local.kept = (keep_for, _local.cache, getattr(_local, "aux", None))
             _local.cache = None
             _local.aux = None
+
+
+def drop_kept():
+    _local.kept = None
+
+
+def handoff_allowed(src_root, out_path):
+    """The plan's listings may serve the translate of the same command only
+    when nothing the command writes in between lands inside the source tree:
+    the output directory (created with its QA cache before translating) must
+    lie outside it."""
+    src = os.path.abspath(src_root)
+    out = os.path.abspath(out_path)
+    return not (out == src or out.startswith(src.rstrip(os.sep) + os.sep))
 
 
 def invalidate():
