@@ -2,10 +2,11 @@
 value parsers the Go compose libraries provide (durations, byte sizes, port
 specs, volume specs, Kubernetes quantity formatting)."""
 
+import functools
 import os
 import re
 
-from ...utils import common, log
+from ...utils import common, fsindex, log
 from ...utils.constants import settings
 from ...utils.lazyre import lazy as _lazy_re
 
@@ -231,3 +232,31 @@ def resolve_bind_source(src, working_dir):
     if not os.path.isabs(src):
         src = os.path.normpath(os.path.join(working_dir, src))
     return src
+
+
+def command_memo(name, error_type):
+    """Memoise a compose-file parser for the enclosing ``fsindex.scope()``
+    (one command): the planner tries every YAML file as compose and the
+    translator parses the same files again for each of their services.  The
+    result depends only on the file, the ``.env``/OS environment and
+    ``--ignoreenv``, none of which change within a command.  A parse error
+    (``error_type``) is remembered and raised again."""
+    def deco(fn):
+        @functools.wraps(fn)
+        def parse(path):
+            cache = fsindex.scoped_cache(name)
+            if cache is None:
+                return fn(path)
+            key = (path, settings.ignore_environment)
+            hit = cache.get(key)
+            if hit is None:
+                try:
+                    hit = (True, fn(path))
+                except error_type as e:
+                    hit = (False, e)
+                cache[key] = hit
+            if hit[0]:
+                return hit[1]
+            raise hit[1]
+        return parse
+    return deco

@@ -265,6 +265,7 @@ def _parse_service(svc, in_file, datas, lookup, compose_path, depth=0):
     return merged
 
 
+@cu.command_memo("compose-v1v2", ComposeError)
 def parse_v2(path):
     """Parse a v1/v2 compose file the way the reference's libcompose
     ``project.Parse()`` does (``v1v2.go:93-129``): interpolation (``.env`` then

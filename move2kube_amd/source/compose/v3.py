@@ -177,6 +177,7 @@ def _check_string_keys(v, prefix):
             _check_string_keys(x, "%s[%d]" % (prefix, i))
 
 
+@cu.command_memo("compose-v3", ComposeError)
 def parse_v3(path):
     """Parse and load a v3 compose file -> normalized config dict."""
     try:

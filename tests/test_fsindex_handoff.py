@@ -77,3 +77,22 @@ def test_output_inside_source_walks_again(tmp_path, monkeypatch):
     with api.Session(qaskip=True) as s:
         s.translate(str(src), str(src))
     assert len([w for w in walks if w == str(src)]) == 2
+
+
+def test_compose_files_parsed_once_per_command(tmp_path, monkeypatch):
+    """The planner and the translator of one command share each compose
+    file's parse (``source/compose/utils.py:command_memo``)."""
+    from move2kube_amd.source.compose import v3
+    src = tmp_path / "dc"
+    shutil.copytree(ref_path("samples", "docker-compose"), str(src))
+    calls = []
+    real = v3.parse_v3.__wrapped__
+
+    def counting(path):
+        calls.append(path)
+        return real(path)
+    monkeypatch.setattr(v3, "parse_v3", v3.cu.command_memo("compose-v3", v3.ComposeError)(counting))
+    with api.Session(qaskip=True) as s:
+        s.translate(str(src), str(tmp_path / "out"))
+    compose_files = [c for c in calls if c.endswith("docker-compose.yaml") or c.endswith("docker-compose.yml")]
+    assert compose_files and len(compose_files) == len(set(compose_files))
