@@ -221,6 +221,11 @@ class DockerAPIProvider:
 # podman CLI
 # ---------------------------------------------------------------------------
 
+def _chain_errors():
+    """Errors that send a probe on to the next provider of the chain."""
+    return (ProviderError, OSError, subprocess.SubprocessError, ValueError, KeyError)
+
+
 def parallel_map(fn, items, workers=None):
     """[fn(x) for x in items] on up to ``workers`` threads (child processes
     run concurrently; the GIL is free while they are waited for).  An
@@ -322,7 +327,11 @@ class ContainerRuntimeProvider:
         results = parallel_map(lambda i: _run(self._detect_cmd(*pairs[i])).returncode == 0, runnable,
                                min(settings.workers, CONTAINER_PARALLEL))
         for i, r in zip(runnable, results):
-            out[i] = None if isinstance(r, (OSError, subprocess.SubprocessError)) else r
+            if isinstance(r, Exception):
+                if not isinstance(r, _chain_errors()):
+                    raise r
+                r = None  # this pair goes on down the chain, as in is_builder_supported
+            out[i] = r
         return out
 
     def get_all_buildpacks(self, builders):
@@ -512,7 +521,7 @@ def is_builder_supported(path, builder):
     for p in providers():
         try:
             return p.is_builder_supported(path, builder)
-        except (ProviderError, OSError, subprocess.SubprocessError, ValueError, KeyError) as e:
+        except _chain_errors() as e:
             log.debug("CNB provider %s: %s", type(p).__name__, e)
             continue
     _log_not_supported()
@@ -533,7 +542,7 @@ def is_builder_supported_batch(pairs):
         if batch is not None:
             try:
                 got = batch([pairs[i] for i in todo])
-            except (ProviderError, OSError, subprocess.SubprocessError, ValueError, KeyError) as e:
+            except _chain_errors() as e:
                 log.debug("CNB provider %s: %s", type(p).__name__, e)
                 continue
             rest = []
@@ -548,7 +557,7 @@ def is_builder_supported_batch(pairs):
         for i in todo:
             try:
                 results[i] = p.is_builder_supported(*pairs[i])
-            except (ProviderError, OSError, subprocess.SubprocessError, ValueError, KeyError) as e:
+            except _chain_errors() as e:
                 log.debug("CNB provider %s: %s", type(p).__name__, e)
                 rest.append(i)
         todo = rest
@@ -561,7 +570,7 @@ def get_all_buildpacks(builders):
     for p in providers():
         try:
             bps = p.get_all_buildpacks(builders)
-        except (ProviderError, OSError, subprocess.SubprocessError, ValueError, KeyError) as e:
+        except _chain_errors() as e:
             log.debug("CNB provider %s: %s", type(p).__name__, e)
             continue
         if bps:
