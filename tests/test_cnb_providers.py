@@ -176,3 +176,24 @@ def test_batched_probes_run_concurrently_and_match_sequential(monkeypatch, tmp_p
     seen = [int((logdir / f).read_text()) for f in os.listdir(str(logdir)) if f.startswith("seen.")]
     assert len(seen) == 6 and max(seen) >= 2
     assert [providers.is_builder_supported(a, b) for a, b in pairs] == got
+
+
+def test_batched_probe_errors(monkeypatch):
+    """A probe that fails with a chain error (here ValueError) is not taken as
+    'supported': it goes on down the chain, ending unsupported; any other
+    exception propagates, as from the sequential chain."""
+    p = providers.ContainerRuntimeProvider()
+    p.runtime = "podman"
+    monkeypatch.setattr(providers.ContainerRuntimeProvider, "is_builder_available", lambda self, b: True)
+    monkeypatch.setattr(providers, "providers", lambda: [p])
+
+    def bad(cmd, timeout=600):
+        raise ValueError("bad mount")
+    monkeypatch.setattr(providers, "_run", bad)
+    assert providers.is_builder_supported_batch([("/a", "b1"), ("/b", "b2")]) == [False, False]
+
+    def worse(cmd, timeout=600):
+        raise RuntimeError("bug")
+    monkeypatch.setattr(providers, "_run", worse)
+    with pytest.raises(RuntimeError):
+        providers.is_builder_supported_batch([("/a", "b1")])
