@@ -9,11 +9,17 @@ import argparse
 import os
 import sys
 
-from .. import assets, move2kube, qaengine
+from .. import assets
 from ..models import plan as plantypes
 from ..utils import fsindex, log, yamlio
 from ..utils.constants import (APP_NAME_SHORT, DEFAULT_DIRECTORY_PERMISSION, DEFAULT_PLAN_FILE, DEFAULT_PROJECT_NAME,
                                QA_CACHE_FILE, settings)
+from ..utils.lazyre import LazyModule
+
+# the orchestration layer (translators, QA engine, transformers) loads on
+# first use: `collect` and `version` never need it
+move2kube = LazyModule("move2kube_amd.move2kube")
+qaengine = LazyModule("move2kube_amd.qaengine")
 
 
 class _StringSlice(argparse.Action):
@@ -142,12 +148,14 @@ def collect_handler(a):
             log.fatal("Source path is a file, expected directory: %s.", srcpath)
     outpath = os.path.join(os.path.normpath(outpath), APP_NAME_SHORT + "_collect")
     annotations = a.annotations.split(",") if a.annotations else []
-    move2kube.collect(srcpath, outpath, annotations)
+    from .. import collector  # move2kube.collect without loading the orchestration layer
+    collector.collect(srcpath, outpath, annotations)
     log.info("Collect Output in [%s]. Copy this directory into the source directory to be used for planning.", outpath)
 
 
 def version_handler(a):
-    print(move2kube.get_version(a.long))
+    from ..models import info
+    print(info.get_version() if not a.long else yamlio.dump(info.get_version_info().to_yaml()))
 
 
 _VERBS = ("collect", "plan", "translate", "version")
