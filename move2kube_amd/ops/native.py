@@ -81,9 +81,19 @@ def remove_tree(path):
         raise OSError(err, os.strerror(err), where)
 
 
-def write_files(items, nthreads=8):
+_write_threads = None
+
+
+def write_files(items, nthreads=None):
     """Write ``[(path, text_or_bytes, mode)]``; returns ``[OSError or None]`` per
-    item.  Native: parallel, GIL released; a repeated path keeps its last content."""
+    item.  Native: parallel (up to 8 threads, within this rank's CPU share), GIL
+    released; a repeated path keeps its last content."""
+    global _write_threads
+    if nthreads is None:
+        if _write_threads is None:
+            from ..utils.constants import host_threads
+            _write_threads = host_threads(8)
+        nthreads = _write_threads
     datas = [d.encode("utf-8", errors="surrogateescape") if isinstance(d, str) else bytes(d) for _, d, _ in items]
     m = _load()
     if m is not None:

@@ -34,15 +34,43 @@ DEFAULT_SERVICE_PORT = 8080
 DEFAULT_PVC_SIZE = "100Mi"
 
 
+def _cgroup_cpu_limit(root="/sys/fs/cgroup"):
+    """CPUs granted by the cgroup CPU quota (v2 ``cpu.max``, v1
+    ``cpu.cfs_quota_us``/``cpu.cfs_period_us``), or None when unlimited.  A
+    container or pod limited to N CPUs usually still sees every host CPU in
+    its affinity mask; sizing pools from the mask oversubscribes the quota and
+    gets the whole process throttled."""
+    try:
+        with open(os.path.join(root, "cpu.max")) as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) / int(period)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open(os.path.join(root, "cpu", "cpu.cfs_quota_us")) as f:
+            quota = int(f.read())
+        with open(os.path.join(root, "cpu", "cpu.cfs_period_us")) as f:
+            period = int(f.read())
+        if quota > 0 and period > 0:
+            return max(1, quota // period)
+    except (OSError, ValueError):
+        pass
+    return None
+
 
 def host_threads(cap):
     """Threads this process should use: the CPUs it may run on (affinity, not
-    the whole machine), shared among the ranks torchrun placed on this node
-    (LOCAL_WORLD_SIZE), capped."""
+    the whole machine, and no more than the cgroup CPU quota), shared among
+    the ranks torchrun placed on this node (LOCAL_WORLD_SIZE), capped."""
     try:
         n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         n = os.cpu_count() or 4
+    limit = _cgroup_cpu_limit()
+    if limit is not None:
+        n = min(n, limit)
     try:
         local = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
     except ValueError:

@@ -172,3 +172,22 @@ def test_copy_file_like_go_copyfile(tmp_path):
     src.write_bytes(b"x")
     common.copy_file(str(dst), str(src))
     assert dst.read_bytes() == b"x" and dst.stat().st_mode & 0o777 == 0o600
+
+
+def test_cgroup_cpu_limit(tmp_path):
+    """Thread pools are sized within the cgroup CPU quota (v2 and v1)."""
+    from move2kube_amd.utils.constants import _cgroup_cpu_limit
+    v2 = tmp_path / "v2"
+    v2.mkdir()
+    (v2 / "cpu.max").write_text("1600000 100000\n")
+    assert _cgroup_cpu_limit(str(v2)) == 16
+    (v2 / "cpu.max").write_text("max 100000\n")
+    assert _cgroup_cpu_limit(str(v2)) is None
+    v1 = tmp_path / "v1"
+    (v1 / "cpu").mkdir(parents=True)
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("250000\n")
+    (v1 / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert _cgroup_cpu_limit(str(v1)) == 2
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
+    assert _cgroup_cpu_limit(str(v1)) is None
+    assert _cgroup_cpu_limit(str(tmp_path / "none")) is None
