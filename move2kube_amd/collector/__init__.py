@@ -61,16 +61,44 @@ def collect(input_path, output_path, annotations=()):
     except OSError as e:
         log.fatal("Unable to create output directory at path %r Error: %r", output_path, str(e))
     log.info("Begin collection")
-    for c in get_collectors():
-        if annotations and not has_overlap(annotations, c.get_annotations()):
+    selected = [c for c in get_collectors()
+                if not annotations or has_overlap(annotations, c.get_annotations())]
+    # The collectors are independent (their own CLIs and output sub-directories)
+    # and wait on external tools - cluster discovery, `docker`, `cf curl`, a
+    # container runtime - so they run at the same time; the reference runs them
+    # one after another.  Each one's log lines are held and written in
+    # collector order, as a sequential run prints them.
+    results = [None] * len(selected)
+
+    def run_one(i):
+        c = selected[i]
+        with log.hold() as held:
+            fatal = None
+            log.info("[%r] Begin collection", c)
+            try:
+                c.collect(input_path, output_path)
+            except log.FatalError as e:
+                fatal = e
+            except Exception as e:  # noqa: BLE001
+                log.warning("[%r] failed. Error: %r", c, str(e))
+            else:
+                log.info("[%r] Done", c)
+        results[i] = (held.lines, fatal)
+
+    if len(selected) == 1:
+        run_one(0)
+    else:
+        import threading
+        threads = [threading.Thread(target=run_one, args=(i,), name="m2k-collect-%d" % i) for i in range(len(selected))]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    for r in results:
+        if r is None:  # the thread died outside Exception (interrupted)
             continue
-        log.info("[%r] Begin collection", c)
-        try:
-            c.collect(input_path, output_path)
-        except Exception as e:  # noqa: BLE001
-            if isinstance(e, log.FatalError):
-                raise
-            log.warning("[%r] failed. Error: %r", c, str(e))
-            continue
-        log.info("[%r] Done", c)
+        lines, fatal = r
+        log.emit(lines)
+        if fatal is not None:
+            raise fatal
     log.info("Collection done")

@@ -43,6 +43,10 @@ class _Logger:
         except (TypeError, ValueError):
             text = "%s %r" % (msg, args)
         line = "%s[%04d] %s\n" % (_LEVEL_NAMES.get(level, "INFO"), int(time.time() - _START), text)
+        held = getattr(_held, "lines", None)
+        if held is not None:
+            held.append(line)
+            return
         stream = self.stream or sys.stderr
         with self._lock:
             stream.write(line)
@@ -69,6 +73,32 @@ class _Logger:
 
 
 logger = _Logger()
+_held = threading.local()
+
+
+class hold:
+    """Context manager: this thread's log lines are kept (``.lines``) instead
+    of written, so work run on several threads can be logged in a fixed order
+    afterwards with :func:`emit`."""
+
+    def __enter__(self):
+        self.lines = []
+        self._prev = getattr(_held, "lines", None)
+        _held.lines = self.lines
+        return self
+
+    def __exit__(self, *exc):
+        _held.lines = self._prev
+        return False
+
+
+def emit(lines):
+    """Write lines kept by :class:`hold`."""
+    stream = logger.stream or sys.stderr
+    with logger._lock:
+        for line in lines:
+            stream.write(line)
+        stream.flush()
 
 
 def set_verbose(verbose=True):

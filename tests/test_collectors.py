@@ -224,3 +224,48 @@ def test_discovery_failed_group_falls_back_to_cli_in_reference_mode(stub_path, m
         assert "Route" not in m and m["Ingress"][0] == "networking.k8s.io/v1"
     finally:
         api.stop()
+
+
+def test_collectors_run_concurrently_with_ordered_logs(monkeypatch, tmp_path):
+    """Selected collectors run at the same time; their log lines come out in
+    collector order; a failing one is a warning; a fatal one is raised after
+    the lines of the collectors before it."""
+    import io
+    import time
+    import move2kube_amd.collector as coll
+    from move2kube_amd.utils import log
+
+    class Slow(coll.Collector):
+        annotations = ("x",)
+
+        def __init__(self, name, delay, fail=None):
+            self.name, self.delay, self.fail = name, delay, fail
+
+        def __repr__(self):
+            return self.name
+
+        def collect(self, input_path, output_path):
+            time.sleep(self.delay)
+            log.info("%s working", self.name)
+            if self.fail == "error":
+                raise ValueError("boom")
+            if self.fail == "fatal":
+                log.fatal("%s cannot go on", self.name)
+
+    buf = io.StringIO()
+    monkeypatch.setattr(log.logger, "stream", buf)
+    monkeypatch.setattr(coll, "get_collectors", lambda: [Slow("a", 0.3), Slow("b", 0.1, "error"), Slow("c", 0.2)])
+    t0 = time.perf_counter()
+    coll.collect("", str(tmp_path / "out"), ["x"])
+    assert time.perf_counter() - t0 < 0.55
+    msgs = [line.split("] ", 1)[1] for line in buf.getvalue().splitlines()]
+    assert msgs == ["Begin collection", "[a] Begin collection", "a working", "[a] Done", "[b] Begin collection",
+                    "b working", "[b] failed. Error: 'boom'", "[c] Begin collection", "c working", "[c] Done",
+                    "Collection done"]
+    buf.truncate(0)
+    buf.seek(0)
+    monkeypatch.setattr(coll, "get_collectors", lambda: [Slow("a", 0.1), Slow("f", 0.0, "fatal"), Slow("c", 0.0)])
+    with pytest.raises(log.FatalError):
+        coll.collect("", str(tmp_path / "out"), ["x"])
+    msgs = [line.split("] ", 1)[1] for line in buf.getvalue().splitlines()]
+    assert msgs[-1] == "f cannot go on" and "[a] Done" in msgs and "[c] Done" not in msgs
