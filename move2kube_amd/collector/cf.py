@@ -112,22 +112,53 @@ def get_all_used_buildpacks(directory):
     return bps
 
 
+def concurrently(*fns):
+    """Run the callables on threads (they wait on external CLIs); returns
+    their results in order, a raised exception in its slot.  Log lines of
+    each are held and written in call order, as a sequential run prints them."""
+    import threading
+    out = [None] * len(fns)
+    held = [None] * len(fns)
+
+    def one(i):
+        with log.hold() as h:
+            try:
+                out[i] = fns[i]()
+            except Exception as e:  # noqa: BLE001
+                out[i] = e
+        held[i] = h.lines
+    threads = [threading.Thread(target=one, args=(i,), name="m2k-cf-%d" % i) for i in range(len(fns))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    for lines in held:
+        log.emit(lines or [])
+    return out
+
+
 def get_cf_buildpack_names(input_path):
     names = []
 
-    def add(src, what):
-        try:
-            for b in src():
-                if not common.is_string_present(names, b):
-                    names.append(b)
-        except Exception as e:  # noqa: BLE001
-            log.warning(what, e)
+    def add(found, what):
+        if isinstance(found, Exception):
+            log.warning(what, found)
+            return
+        for b in found:
+            if not common.is_string_present(names, b):
+                names.append(b)
 
     if input_path:
-        add(lambda: get_all_used_buildpacks(input_path), "Unable to find used buildpacks : %s")
+        try:
+            found = get_all_used_buildpacks(input_path)
+        except Exception as e:  # noqa: BLE001
+            found = e
+        add(found, "Unable to find used buildpacks : %s")
     else:
-        add(get_all_cf_instance_buildpacks, "Unable to collect buildpacks from cf instance : %s")
-        add(get_all_cf_app_buildpacks, "Unable to find used buildpacks : %s")
+        # `cf buildpacks` and `cf curl /v2/apps` at the same time
+        inst, apps = concurrently(get_all_cf_instance_buildpacks, get_all_cf_app_buildpacks)
+        add(inst, "Unable to collect buildpacks from cf instance : %s")
+        add(apps, "Unable to find used buildpacks : %s")
     return names
 
 
@@ -165,11 +196,15 @@ class CFContainerTypesCollector(Collector):
         output_path = os.path.join(output_path, "cf")
         os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
         cz = collection.CfContainerizers()
-        names = get_cf_buildpack_names(input_path)
-        log.debug("buildpackNames : %s", names)
         cnb = CNBContainerizer()
         cnb.init("")
-        buildpacks = cnb.get_all_buildpacks()
+        # the buildpack names (manifests or the foundation) and the builders'
+        # buildpack lists (a container runtime) are gathered at the same time
+        names, buildpacks = concurrently(lambda: get_cf_buildpack_names(input_path), cnb.get_all_buildpacks)
+        for r in (names, buildpacks):
+            if isinstance(r, Exception):
+                raise r
+        log.debug("buildpackNames : %s", names)
         log.debug("buildpacks : %s", buildpacks)
         cz.buildpack_containerizers = get_buildpack_containerizers(names, buildpacks)
         file_name = "cfcontainertypes_" + "".join(names)

@@ -93,7 +93,12 @@ class hold:
 
 
 def emit(lines):
-    """Write lines kept by :class:`hold`."""
+    """Write lines kept by :class:`hold` (into this thread's own held lines
+    when it is holding too)."""
+    held = getattr(_held, "lines", None)
+    if held is not None:
+        held.extend(lines)
+        return
     stream = logger.stream or sys.stderr
     with logger._lock:
         for line in lines:

@@ -269,3 +269,27 @@ def test_collectors_run_concurrently_with_ordered_logs(monkeypatch, tmp_path):
         coll.collect("", str(tmp_path / "out"), ["x"])
     msgs = [line.split("] ", 1)[1] for line in buf.getvalue().splitlines()]
     assert msgs[-1] == "f cannot go on" and "[a] Done" in msgs and "[c] Done" not in msgs
+
+
+def test_held_log_lines_nest(monkeypatch):
+    import io
+    import threading
+    from move2kube_amd.utils import log
+    buf = io.StringIO()
+    monkeypatch.setattr(log.logger, "stream", buf)
+    with log.hold() as outer:
+        log.info("one")
+        inner_lines = []
+
+        def work():
+            with log.hold() as h:
+                log.info("two")
+            inner_lines.extend(h.lines)
+        t = threading.Thread(target=work)
+        t.start()
+        t.join()
+        log.emit(inner_lines)
+        log.info("three")
+    assert buf.getvalue() == ""
+    log.emit(outer.lines)
+    assert [l.split("] ", 1)[1] for l in buf.getvalue().splitlines()] == ["one", "two", "three"]
