@@ -42,6 +42,41 @@ def run(argv, combined=False, timeout=300):
     return p.stdout
 
 
+def concurrently(*fns, workers=8):
+    """Run the callables on up to ``workers`` threads (they wait on external
+    CLIs); returns their results in order, a raised ``Exception`` in its slot.
+    The log lines of each are held and written in call order, as a sequential
+    run prints them."""
+    import threading
+    n = len(fns)
+    out = [None] * n
+    held = [None] * n
+    nxt = [0]
+    lock = threading.Lock()
+
+    def worker():
+        while True:
+            with lock:
+                i = nxt[0]
+                nxt[0] += 1
+            if i >= n:
+                return
+            with log.hold() as h:
+                try:
+                    out[i] = fns[i]()
+                except Exception as e:  # noqa: BLE001
+                    out[i] = e
+            held[i] = h.lines
+    threads = [threading.Thread(target=worker, name="m2k-collect-worker") for _ in range(max(1, min(workers, n)))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    for lines in held:
+        log.emit(lines or [])
+    return out
+
+
 def get_collectors():
     from .cf import CfAppsCollector, CFContainerTypesCollector
     from .cluster import ClusterCollector

@@ -16,7 +16,7 @@ from ..models import collection
 from ..models import plan as plantypes
 from ..utils import common, log
 from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
-from . import Collector, run
+from . import Collector, concurrently, run
 
 
 def _cf_apps():
@@ -110,31 +110,6 @@ def get_all_used_buildpacks(directory):
                 bps.append(a.buildpack.value)
             bps.extend(a.buildpacks)
     return bps
-
-
-def concurrently(*fns):
-    """Run the callables on threads (they wait on external CLIs); returns
-    their results in order, a raised exception in its slot.  Log lines of
-    each are held and written in call order, as a sequential run prints them."""
-    import threading
-    out = [None] * len(fns)
-    held = [None] * len(fns)
-
-    def one(i):
-        with log.hold() as h:
-            try:
-                out[i] = fns[i]()
-            except Exception as e:  # noqa: BLE001
-                out[i] = e
-        held[i] = h.lines
-    threads = [threading.Thread(target=one, args=(i,), name="m2k-cf-%d" % i) for i in range(len(fns))]
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join()
-    for lines in held:
-        log.emit(lines or [])
-    return out
 
 
 def get_cf_buildpack_names(input_path):

@@ -6,7 +6,7 @@ import os
 from ..models.collection import ImageInfo
 from ..utils import common, log
 from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
-from . import Collector, CommandError, run
+from . import Collector, CommandError, concurrently, run
 from ..utils.lazyre import lazy as _lazy_re
 
 _NUM = _lazy_re(r"[0-9]+")
@@ -113,11 +113,14 @@ class ImagesCollector(Collector):
         os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
         names = get_all_image_names() if input_path == "" else get_dc_image_names(input_path)
         log.debug("Images : %s", names)
-        for name in names:
-            try:
-                data = get_docker_inspect_result(name)
-            except (OSError, CommandError):
+        # one `docker inspect` per image, up to 8 at a time (the reference runs
+        # them one after another); results are handled in list order
+        inspected = concurrently(*[(lambda n=name: get_docker_inspect_result(n)) for name in names])
+        for name, data in zip(names, inspected):
+            if isinstance(data, (OSError, CommandError)):
                 continue
+            if isinstance(data, Exception):
+                raise data
             if data is None:
                 continue
             info = get_image_info(data)
