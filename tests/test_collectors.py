@@ -293,3 +293,27 @@ def test_held_log_lines_nest(monkeypatch):
     assert buf.getvalue() == ""
     log.emit(outer.lines)
     assert [l.split("] ", 1)[1] for l in buf.getvalue().splitlines()] == ["one", "two", "three"]
+
+
+def test_images_collector_inspects_concurrently(tmp_path, monkeypatch):
+    """`docker inspect` runs for several images at once; every image still
+    gets its metadata file."""
+    import time
+    from move2kube_amd.collector.images import ImagesCollector
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    (bindir / "docker").write_text(
+        '#!/bin/sh\n[ "$1" = inspect ] || exit 1\nsleep 0.3\n'
+        'printf \'[{"RepoTags": ["%s"], "ContainerConfig": {"User": "1001", "WorkingDir": "/app", '
+        '"ExposedPorts": {"8080/tcp": {}}}}]\' "$2"\n')
+    os.chmod(str(bindir / "docker"), 0o755)
+    monkeypatch.setenv("PATH", str(bindir) + os.pathsep + os.environ["PATH"])
+    src = tmp_path / "src"
+    src.mkdir()
+    (src / "docker-compose.yml").write_text(
+        "version: '3'\nservices:\n" + "".join("  s%d:\n    image: img%d:1\n" % (i, i) for i in range(4)))
+    t0 = time.perf_counter()
+    ImagesCollector().collect(str(src), str(tmp_path / "out"))
+    assert time.perf_counter() - t0 < 1.0   # 4 x 0.3 s one after another would be 1.2 s
+    files = sorted(os.listdir(str(tmp_path / "out" / "images")))
+    assert [f.split("-")[0] for f in files] == ["img%d" % i for i in range(4)]
