@@ -6,7 +6,9 @@ under ``<out>/m2k_collect/<area>/``.  Collectors are selected by annotation
 (``-a k8s,cf``); a failing collector is logged and skipped.
 """
 
+import os
 import subprocess
+import threading
 
 from ..utils import log
 
@@ -32,11 +34,23 @@ class CommandError(RuntimeError):
         self.output = output
 
 
+_SERIAL_CLIS = {"cf": threading.Lock()}
+
+
 def run(argv, combined=False, timeout=300):
     """Run a command; stdout bytes (stdout+stderr with ``combined``). Raises
-    :class:`CommandError` on a non-zero exit and FileNotFoundError if missing."""
-    p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT if combined else subprocess.PIPE,
-                       stdin=subprocess.DEVNULL, timeout=timeout)
+    :class:`CommandError` on a non-zero exit and FileNotFoundError if missing.
+
+    Collectors run concurrently, but two ``cf`` commands never do: the cf
+    CLI rewrites ``~/.cf/config.json`` when it refreshes its token."""
+    lock = _SERIAL_CLIS.get(os.path.basename(argv[0])) if argv else None
+    if lock is not None:
+        with lock:
+            p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT if combined else subprocess.PIPE,
+                               stdin=subprocess.DEVNULL, timeout=timeout)
+    else:
+        p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT if combined else subprocess.PIPE,
+                           stdin=subprocess.DEVNULL, timeout=timeout)
     if p.returncode != 0:
         raise CommandError(argv, p.returncode, p.stdout)
     return p.stdout
@@ -89,7 +103,6 @@ def has_overlap(a, b):
 
 
 def collect(input_path, output_path, annotations=()):
-    import os
     from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION
     try:
         os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)

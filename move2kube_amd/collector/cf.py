@@ -130,10 +130,13 @@ def get_cf_buildpack_names(input_path):
             found = e
         add(found, "Unable to find used buildpacks : %s")
     else:
-        # `cf buildpacks` and `cf curl /v2/apps` at the same time
-        inst, apps = concurrently(get_all_cf_instance_buildpacks, get_all_cf_app_buildpacks)
-        add(inst, "Unable to collect buildpacks from cf instance : %s")
-        add(apps, "Unable to find used buildpacks : %s")
+        for src, what in ((get_all_cf_instance_buildpacks, "Unable to collect buildpacks from cf instance : %s"),
+                          (get_all_cf_app_buildpacks, "Unable to find used buildpacks : %s")):
+            try:
+                found = src()
+            except Exception as e:  # noqa: BLE001
+                found = e
+            add(found, what)
     return names
 
 
