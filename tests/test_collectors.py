@@ -317,3 +317,22 @@ def test_images_collector_inspects_concurrently(tmp_path, monkeypatch):
     assert time.perf_counter() - t0 < 1.0   # 4 x 0.3 s one after another would be 1.2 s
     files = sorted(os.listdir(str(tmp_path / "out" / "images")))
     assert [f.split("-")[0] for f in files] == ["img%d" % i for i in range(4)]
+
+
+def test_cf_commands_never_overlap(tmp_path, monkeypatch):
+    """Concurrent collectors still run one `cf` command at a time."""
+    import threading
+    import move2kube_amd.collector as coll
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    (bindir / "cf").write_text('#!/bin/sh\nif [ -e "$LOG/busy" ]; then echo overlap >> "$LOG/overlaps"; fi\n'
+                               'touch "$LOG/busy"\nsleep 0.1\nrm -f "$LOG/busy"\necho ok\n')
+    os.chmod(str(bindir / "cf"), 0o755)
+    monkeypatch.setenv("PATH", str(bindir) + os.pathsep + os.environ["PATH"])
+    monkeypatch.setenv("LOG", str(tmp_path))
+    threads = [threading.Thread(target=coll.run, args=(["cf", "curl", "/v2/apps"],)) for _ in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not (tmp_path / "overlaps").exists()
