@@ -202,6 +202,32 @@ class DockerAPIProvider:
             log.debug("Detect failed %s : %s", builder, e)
             return False
 
+    def is_builder_supported_batch(self, pairs):
+        """[(path, builder)] -> [True/False, or None where this provider cannot
+        answer]: builder images are settled once each, then the detector
+        containers run up to ``CONTAINER_PARALLEL`` at a time on the daemon
+        (the reference creates, runs and removes one container per probe, in
+        sequence)."""
+        out = [None] * len(pairs)
+        runnable = [i for i, (_, builder) in enumerate(pairs) if self.is_builder_available(builder)]
+
+        def probe(i):
+            path, builder = pairs[i]
+            try:
+                log.debug(self.run_container(builder, "/cnb/lifecycle/detector", os.path.abspath(path), "/workspace"))
+                return True
+            except ProviderError as e:
+                log.debug("Detect failed %s : %s", builder, e)
+                return False
+        results = parallel_map(probe, runnable, min(settings.workers, CONTAINER_PARALLEL))
+        for i, r in zip(runnable, results):
+            if isinstance(r, Exception):
+                if not isinstance(r, _chain_errors()):
+                    raise r
+                r = None
+            out[i] = r
+        return out
+
     def get_all_buildpacks(self, builders):
         if not self.is_sock_accessible():
             raise ProviderError("Container runtime not supported in this instance")

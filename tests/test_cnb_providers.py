@@ -1,6 +1,7 @@
 """CNB provider chain against fakes: a Docker Engine API served on a unix
 socket, and stub podman / pack executables."""
 
+import itertools
 import json
 import os
 import socketserver
@@ -13,6 +14,10 @@ from move2kube_amd.containerizer.cnb import providers
 
 STUBS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "stubbin")
 LABEL = json.dumps([{"group": [{"id": "google.nodejs.runtime"}, {"id": "google.go.runtime"}]}])
+
+
+_FAKE_LOCK = threading.Lock()
+_FAKE_IDS = itertools.count()
 
 
 class _FakeDockerd(BaseHTTPRequestHandler):
@@ -36,7 +41,8 @@ class _FakeDockerd(BaseHTTPRequestHandler):
             return self._json(200, {"status": "pulled"})
         if self.path == "/containers/create":
             cfg = json.loads(body or b"{}")
-            cid = "c%d" % len(self.state)
+            with _FAKE_LOCK:
+                cid = "c%d" % next(_FAKE_IDS)
             mounts = (cfg.get("HostConfig") or {}).get("Mounts") or []
             src = mounts[0]["Source"] if mounts else ""
             self.state[cid] = 0 if (cfg.get("Image") == "hello-world" or os.path.exists(os.path.join(src, "package.json"))) else 1
@@ -197,3 +203,19 @@ def test_batched_probe_errors(monkeypatch):
     monkeypatch.setattr(providers, "_run", worse)
     with pytest.raises(RuntimeError):
         providers.is_builder_supported_batch([("/a", "b1")])
+
+
+def test_docker_api_batched_probes_match_sequential(fake_dockerd, tmp_path):
+    """The Docker API provider's batch answers equal its one-at-a-time
+    answers (the fake daemon's detector passes where a package.json is)."""
+    dirs = []
+    for i in range(6):
+        d = tmp_path / ("app%d" % i)
+        d.mkdir()
+        if i % 2 == 0:
+            (d / "package.json").write_text("{}")
+        dirs.append(str(d))
+    pairs = [(d, b) for d in dirs for b in ("gcr.io/buildpacks/builder", "cloudfoundry/cnb:cflinuxfs3")]
+    p = providers.DockerAPIProvider()
+    assert p.is_builder_supported_batch(pairs) == [p.is_builder_supported(d, b) for d, b in pairs]
+    assert p.is_builder_supported_batch(pairs) == [i // 2 % 2 == 0 for i in range(len(pairs))]
