@@ -58,6 +58,20 @@ def test_two_ranks_gloo():
     assert d["scaling"] == "weak"
 
 
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only contract test")
+def test_one_rank_under_torchrun_joins_the_group():
+    """Launched by torchrun with one rank, bench.py still initialises the
+    process group (the collective path of the multi-GPU runs) and reports
+    the work tree it used."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", "29534", "bench.py", "--steps", "1",
+           "--warmup", "1", "--check-runs", "0", "--workdir", "disk"]
+    p = subprocess.run(cmd, cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    d = _last_json(p.stdout.decode())
+    assert d["n_gpus"] == 1 and d["workdir_fs"] == "disk" and "on disk" in d["data"]
+
+
 def test_baseline_configs_bench_golang():
     """benchmarks/baseline_configs.py (BASELINE.md per-configuration wall clock):
     one warm, one fork-model emulation and one cold CLI run of the golang
