@@ -15,10 +15,16 @@ cache, defaults otherwise) + translate + write of every artifact, in process;
 nothing is cached between steps (fresh file index, detector runs, QA engines,
 output directory).  ``benchmarks/refconfigs.py`` defines the commands.
 
-Multi-GPU: one rank per GPU (torch.distributed), each rank translating its own
-copy of the corpus (weak scaling); the timed region is bracketed by a barrier
-and ``torch.cuda.synchronize()`` and the slowest rank's time is reported.
-``value`` = translated services per second summed over all ranks.
+Multi-GPU: one rank per GPU (torch.distributed over RCCL; joined whenever a
+launcher set RANK and MASTER_ADDR, one rank included), each rank translating
+its own copy of the corpus (weak scaling); the timed region is bracketed by a
+barrier and ``torch.cuda.synchronize()`` and the slowest rank's time is
+reported.  ``value`` = translated services per second summed over all ranks.
+
+Work tree: inputs and output trees live on a tmpfs (``/dev/shm``) when one is
+available (``--workdir``, reported as ``workdir_fs``): every step rewrites the
+output tree, and on the hosts' discard-mounted scratch disks that churn slows
+every later run (see README "Why tmpfs").
 
 Correctness (untimed, rank 0): ``manifest_diff_vs_ref`` is the number of
 files that differ from the reference-derived expected trees
