@@ -8,6 +8,10 @@ VERSION = "v0.1.0"
 BUILD_METADATA = ""
 GIT_COMMIT = ""
 GIT_TREE_STATE = ""
+try:  # stamped into release archives by scripts/builddist.py (the reference's -ldflags -X, Makefile:40-56)
+    from .._buildinfo import BUILD_METADATA, GIT_COMMIT, GIT_TREE_STATE, VERSION  # noqa: F401
+except ImportError:
+    pass
 
 
 def get_version():

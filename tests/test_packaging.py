@@ -10,7 +10,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_builddist_and_install(tmp_path):
     out = tmp_path / "dist"
-    subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "builddist.py"), "--version", "v0.1.0", "--out", str(out)],
+    subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "builddist.py"), "--version", "v0.3.1+unreleased",
+                    "--commit", "abc123", "--tree", "clean", "--out", str(out)],
                    check=True, stdout=subprocess.PIPE)
     archives = sorted(p for p in os.listdir(str(out)))
     tgz = [a for a in archives if a.endswith(".tar.gz")][0]
@@ -20,10 +21,18 @@ def test_builddist_and_install(tmp_path):
     assert any(n.endswith("/bin/move2kube") for n in names)
     assert any(n.endswith("move2kube_amd/cli/main.py") for n in names)
     prefix = tmp_path / "prefix"
+    elsewhere = tmp_path / "work"
+    elsewhere.mkdir()
+    env = {k: v for k, v in os.environ.items() if k != "PYTHONPATH"}
+    # run outside the repository: nothing may resolve through the working directory
     p = subprocess.run(["bash", os.path.join(ROOT, "scripts", "install.sh"), str(out / tgz), str(prefix)],
-                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, cwd=str(elsewhere), env=env)
     assert p.returncode == 0, p.stdout.decode()
-    assert b"v0.1.0" in p.stdout
+    assert p.stdout.decode().splitlines()[-1] == "v0.3.1+unreleased"   # install.sh ends with `move2kube version`
+    long = subprocess.run([str(prefix / "bin" / "move2kube"), "version", "-l"], stdout=subprocess.PIPE, check=True,
+                          cwd=str(elsewhere), env=env)
+    assert long.stdout.decode().splitlines()[:3] == ["version: v0.3.1+unreleased", "gitCommit: abc123",
+                                                      "gitTreeState: clean"]
 
 
 def test_cli_version_and_help():
