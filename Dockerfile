@@ -15,13 +15,22 @@ RUN PYTORCH_ROCM_ARCH=gfx950 python3 -m move2kube_amd.ops.build \
 
 FROM ${ROCM_IMAGE}
 ARG VERSION=latest
+ARG GIT_COMMIT=""
+ARG GIT_TREE_STATE=""
 LABEL org.opencontainers.image.title="move2kube-amd" org.opencontainers.image.version="${VERSION}"
 RUN apt-get update && apt-get install -y --no-install-recommends python3 python3-yaml python3-numpy git openssh-client \
  && rm -rf /var/lib/apt/lists/*
 COPY --from=builder /src/move2kube_amd /opt/move2kube-amd/move2kube_amd
 COPY --from=builder /src/samples /opt/move2kube-amd/samples
-RUN printf '#!/bin/sh\nPYTHONPATH=/opt/move2kube-amd exec python3 -m move2kube_amd "$@"\n' > /usr/local/bin/move2kube \
- && chmod +x /usr/local/bin/move2kube
+# version stamp (the reference's -ldflags -X) and a launcher that runs the
+# package by file, so a move2kube_amd directory in /wksps cannot shadow it
+RUN printf 'VERSION = "%s"\nBUILD_METADATA = ""\nGIT_COMMIT = "%s"\nGIT_TREE_STATE = "%s"\n' \
+      "${VERSION}" "${GIT_COMMIT}" "${GIT_TREE_STATE}" > /opt/move2kube-amd/move2kube_amd/_buildinfo.py \
+ && printf 'import sys\nsys.path.insert(0, "/opt/move2kube-amd")\nfrom move2kube_amd.cli.main import main\nsys.exit(main())\n' \
+      > /opt/move2kube-amd/m2k_main.py \
+ && printf '#!/bin/sh\nexec python3 /opt/move2kube-amd/m2k_main.py "$@"\n' > /usr/local/bin/move2kube \
+ && chmod +x /usr/local/bin/move2kube \
+ && python3 -m compileall -q /opt/move2kube-amd/move2kube_amd
 VOLUME /wksps
 WORKDIR /wksps
 ENTRYPOINT ["move2kube"]

@@ -68,7 +68,8 @@ info: ## Version info
 
 .PHONY: cbuild
 cbuild: ## Build the container image
-	docker build -t $(IMAGE):$(VERSION) --build-arg VERSION=$(VERSION) .
+	docker build -t $(IMAGE):$(VERSION) --build-arg VERSION=$(VERSION) --build-arg GIT_COMMIT=$(GIT_COMMIT) \
+		--build-arg GIT_TREE_STATE=$(GIT_DIRTY) .
 
 .PHONY: cpush
 cpush: ## Push the container image
