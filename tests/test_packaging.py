@@ -44,3 +44,32 @@ def test_cli_version_and_help():
     for flag in (b"--plan", b"--curate", b"--source", b"--outpath", b"--name", b"--qacache", b"--ignoreenv"):
         assert flag in p.stdout
     assert b"--qaskip" not in p.stdout  # hidden like the reference
+
+
+def test_wheel_with_the_images_setuptools(tmp_path):
+    """`pip wheel .` with the installed setuptools (no build isolation, no
+    index) builds a complete, platform-tagged wheel: package, console script,
+    the in-tree native libraries and every asset including dot-files."""
+    import shutil
+    import zipfile
+    leftovers = [os.path.join(ROOT, d) for d in ("build", "move2kube_amd.egg-info")]
+    existed = [os.path.exists(d) for d in leftovers]
+    try:
+        p = subprocess.run([sys.executable, "-m", "pip", "wheel", "--no-deps", "--no-build-isolation", "--no-index",
+                            "-w", str(tmp_path), ROOT], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    finally:
+        for d, was in zip(leftovers, existed):
+            if not was:
+                shutil.rmtree(d, ignore_errors=True)
+    assert p.returncode == 0, p.stdout.decode()[-2000:]
+    wheels = [f for f in os.listdir(str(tmp_path)) if f.endswith(".whl")]
+    assert len(wheels) == 1 and wheels[0].startswith("move2kube_amd-") and "none-any" not in wheels[0]
+    with zipfile.ZipFile(str(tmp_path / wheels[0])) as z:
+        names = z.namelist()
+        entry = [n for n in names if n.endswith("entry_points.txt")]
+        assert entry and "move2kube = move2kube_amd.cli.main:main" in z.read(entry[0]).decode()
+    assert "move2kube_amd/cli/main.py" in names
+    assert "move2kube_amd/assets/m2kassets/s2i/python/.s2i/environment" in names
+    assert "move2kube_amd/assets/templates/k8sreadme.md.tpl" in names
+    if os.path.exists(os.path.join(ROOT, "move2kube_amd", "ops", "libm2k_ed_hip.so")):
+        assert "move2kube_amd/ops/libm2k_ed_hip.so" in names
