@@ -155,8 +155,8 @@ def decode(data, scheme="k8s"):
 
 
 def decode_file(path, scheme="k8s"):
-    with open(path, "rb") as f:
-        return decode(f.read(), scheme)
+    from ..utils.common import read_bytes  # a FIFO in the tree is an error, not a hang
+    return decode(read_bytes(path), scheme)
 
 
 def gvk(obj):

@@ -159,7 +159,7 @@ bool trim_continuation(std::string &line, char esc) {
 
 std::string sniff_one(const std::string &path) {
   const size_t kMaxLine = 64 * 1024;  // bufio.Scanner default token limit
-  int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  int fd = open(path.c_str(), O_RDONLY | O_NONBLOCK | O_CLOEXEC);  // a FIFO must not block: rejected by the S_ISREG check below
   if (fd < 0) return "";
   struct stat st;
   if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {

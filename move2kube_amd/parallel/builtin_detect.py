@@ -20,7 +20,7 @@ in readdir order (file-system dependent in the reference too).
 
 import os
 
-from ..utils import fsindex
+from ..utils import common, fsindex
 from ..utils.constants import settings
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -82,9 +82,8 @@ def _find_main(d):
         if len(shown) < 3 or not shown.endswith("py"):  # awk '/.py$/': any character, then "py"
             continue
         try:
-            with open(p, "rb") as f:
-                if b"__main__" not in f.read():
-                    continue
+            if b"__main__" not in common.read_bytes(p):
+                continue
         except OSError:
             continue
         try:

@@ -25,9 +25,9 @@ def _trim_continuation(line, esc):
 
 def sniff_first_from(path):
     """Original line of the first non-ARG instruction if it is FROM, else ''."""
+    from ..utils.common import read_bytes
     try:
-        with open(path, "rb") as f:
-            data = f.read()
+        data = read_bytes(path)
     except OSError:
         return ""
     text = data.decode("utf-8", errors="surrogateescape")

@@ -94,9 +94,25 @@ def get_files_by_name(input_path, names):
 # YAML / JSON IO
 # ---------------------------------------------------------------------------
 
+def read_bytes(path):
+    """Contents of a regular file found in a source tree.  Opened without
+    blocking and checked with fstat, so a FIFO, socket or device that happens
+    to carry a .yaml/.py/Dockerfile name is an error, not a hang (ReadFile
+    in the reference blocks forever on a FIFO with no writer)."""
+    import errno
+    import stat
+    fd = os.open(path, os.O_RDONLY | os.O_NONBLOCK | os.O_CLOEXEC)
+    try:
+        if not stat.S_ISREG(os.fstat(fd).st_mode):
+            raise OSError(errno.EINVAL, "not a regular file", path)
+        with open(fd, "rb", closefd=False) as f:
+            return f.read()
+    finally:
+        os.close(fd)
+
+
 def read_text(path):
-    with open(path, "rb") as f:
-        return f.read().decode("utf-8", errors="surrogateescape")
+    return read_bytes(path).decode("utf-8", errors="surrogateescape")
 
 
 def write_text(path, text, mode=DEFAULT_FILE_PERMISSION):

@@ -819,14 +819,23 @@ def _native_loader():
 def _parse(text, mode, multi):
     nl = _native_loader()
     if nl and isinstance(text, str):
-        r = nl(text, mode, multi, go_resolve_number, _UNSUPPORTED)
+        try:
+            r = nl(text, mode, multi, go_resolve_number, _UNSUPPORTED)
+        except UnicodeError:
+            r = _UNSUPPORTED
         if r is not _UNSUPPORTED:
             return r
     lz = _lz()
     loader = (lz.typed, lz.v2, lz.raw)[mode]
-    if multi:
-        return list(lz.yaml.load_all(text, Loader=loader))
-    return lz.yaml.load(text, Loader=loader)
+    try:
+        if multi:
+            return list(lz.yaml.load_all(text, Loader=loader))
+        return lz.yaml.load(text, Loader=loader)
+    except UnicodeError as e:
+        # bytes that are not UTF-8 (kept as surrogates by read_text): a parse
+        # error of this document, as go-yaml reports "invalid leading UTF-8
+        # octet" - callers skip the file instead of losing the whole planner
+        raise lz.yaml.YAMLError("invalid UTF-8 in document: %s" % e) from None
 
 
 def load(text):

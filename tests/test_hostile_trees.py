@@ -1,0 +1,65 @@
+"""Source trees with special files and undecodable YAML: the planner and the
+translator skip what they cannot read instead of hanging or dropping a whole
+translator (crashes and hangs are fixed)."""
+
+import os
+import shutil
+import threading
+
+import pytest
+
+from move2kube_amd import api
+from move2kube_amd.utils import common
+
+from conftest import ref_path
+
+
+def _bounded(fn, seconds=20):
+    out = {}
+
+    def run():
+        try:
+            out["value"] = fn()
+        except BaseException as e:  # noqa: BLE001
+            out["error"] = e
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    t.join(seconds)
+    assert not t.is_alive(), "hung"
+    if "error" in out:
+        raise out["error"]
+    return out.get("value")
+
+
+def test_read_bytes_rejects_a_fifo_without_blocking(tmp_path):
+    fifo = tmp_path / "x.yaml"
+    os.mkfifo(str(fifo))
+    with pytest.raises(OSError):
+        _bounded(lambda: common.read_bytes(str(fifo)), 5)
+    (tmp_path / "ok.yaml").write_bytes(b"a: 1\n")
+    assert common.read_bytes(str(tmp_path / "ok.yaml")) == b"a: 1\n"
+
+
+def _tree(tmp_path, name):
+    src = tmp_path / name
+    shutil.copytree(ref_path("samples", "nodejs"), str(src / "app"))
+    shutil.copytree(ref_path("samples", "docker-compose"), str(src / "dc"))
+    (src / "app" / "requirements.txt").write_text("flask\n")  # the python detectors then read *.py files
+    return src
+
+
+def test_translate_a_tree_with_fifos_and_bad_utf8(tmp_path):
+    """Same services as the clean tree; FIFOs named like YAML, Dockerfiles and
+    Python files, a Latin-1 compose file and binary junk are skipped."""
+    clean = _tree(tmp_path / "a", "src")   # same root name: it names a service
+    src = _tree(tmp_path / "b", "src")
+    for name in ("app/pipe.yaml", "app/Dockerfile.fifo", "app/main.py", "dc/fifo.yml"):
+        os.mkfifo(str(src / name))
+    (src / "latin1.yml").write_bytes(b'version: "3"\nservices:\n  web:\n    image: "caf\xe9:1"\n')
+    (src / "junk.yaml").write_bytes(bytes(range(256)) * 4)
+    with api.Session(qaskip=True) as s:
+        want = s.translate(str(clean), str(tmp_path / "out-clean"))
+        got = _bounded(lambda: s.translate(str(src), str(tmp_path / "out")), 60)
+    assert sorted(os.listdir(os.path.join(got, "myproject"))) == sorted(os.listdir(os.path.join(want, "myproject")))
+    with open(os.path.join(got, "docker-compose.yaml")) as a, open(os.path.join(want, "docker-compose.yaml")) as b:
+        assert a.read() == b.read()
