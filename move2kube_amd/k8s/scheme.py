@@ -126,7 +126,15 @@ def versions_for_kind(kind, scheme="all"):
 def decode(data, scheme="k8s"):
     """UniversalDeserializer().Decode: first YAML document -> object dict.
 
-    Raises DecodeError when the document has no registered apiVersion/kind."""
+    Raises DecodeError when the document has no registered apiVersion/kind,
+    or is nested too deeply for the recursive checks (this file only)."""
+    try:
+        return _decode(data, scheme)
+    except RecursionError:
+        raise DecodeError("document nested too deeply") from None
+
+
+def _decode(data, scheme):
     try:
         text = data.decode("utf-8", "surrogateescape") if isinstance(data, bytes) else data
         # sigs.k8s.io/yaml converts YAML to JSON with go-yaml v2 scalars

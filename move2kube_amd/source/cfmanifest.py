@@ -198,7 +198,16 @@ def _decode_manifest(doc):
 
 
 def read_application_manifest(path, service_name="", artifact_type=plantypes.YAMLS):
-    """(applications, variables) of a CF manifest (cfmanifest2kube.go:422-470)."""
+    """(applications, variables) of a CF manifest (cfmanifest2kube.go:422-470).
+    A document nested too deeply for the recursive walks is a ManifestError
+    of this file (Go's growable stacks never hit that limit)."""
+    try:
+        return _read_application_manifest(path, service_name, artifact_type)
+    except RecursionError:
+        raise ManifestError("%s: document nested too deeply" % path) from None
+
+
+def _read_application_manifest(path, service_name, artifact_type):
     variables = get_missing_variables(path)
     doc = _load(path)
     values = {}

@@ -242,16 +242,23 @@ def command_memo(name, error_type):
     ``--ignoreenv``, none of which change within a command.  A parse error
     (``error_type``) is remembered and raised again."""
     def deco(fn):
+        def checked(path):
+            try:
+                return fn(path)
+            except RecursionError:  # nested too deeply for the recursive walks: this file only
+                raise error_type("Unable to load Compose file at path %s Error: document nested too deeply"
+                                 % path) from None
+
         @functools.wraps(fn)
         def parse(path):
             cache = fsindex.scoped_cache(name)
             if cache is None:
-                return fn(path)
+                return checked(path)
             key = (path, settings.ignore_environment)
             hit = cache.get(key)
             if hit is None:
                 try:
-                    hit = (True, fn(path))
+                    hit = (True, checked(path))
                 except error_type as e:
                     hit = (False, e)
                 cache[key] = hit

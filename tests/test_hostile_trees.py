@@ -63,3 +63,20 @@ def test_translate_a_tree_with_fifos_and_bad_utf8(tmp_path):
     assert sorted(os.listdir(os.path.join(got, "myproject"))) == sorted(os.listdir(os.path.join(want, "myproject")))
     with open(os.path.join(got, "docker-compose.yaml")) as a, open(os.path.join(want, "docker-compose.yaml")) as b:
         assert a.read() == b.read()
+
+
+def test_a_deeply_nested_yaml_only_loses_itself(tmp_path):
+    """A document nested deeper than the recursive walks allow is skipped as a
+    file; the other manifests of every translator are still planned."""
+    src = tmp_path / "src"
+    src.mkdir()
+    deep = "".join("  " * (i + 1) + "k%d:\n" % i for i in range(1500)) + "  " * 1501 + "v\n"
+    (src / "crd.yaml").write_text("apiVersion: example.com/v1\nkind: Widget\nmetadata:\n  name: w\nspec:\n" + deep)
+    (src / "compose.yml").write_text("version: '3'\nservices:\n  deep:\n    image: x\n    labels:\n" + deep)
+    (src / "dep.yaml").write_text(
+        "apiVersion: apps/v1\nkind: Deployment\nmetadata:\n  name: web\nspec:\n  selector:\n    matchLabels:\n"
+        "      app: web\n  template:\n    metadata:\n      labels:\n        app: web\n    spec:\n      containers:\n"
+        "      - name: web\n        image: nginx:1.19\n")
+    with api.Session(qaskip=True) as s:
+        out = _bounded(lambda: s.translate(str(src), str(tmp_path / "out")), 120)
+    assert "web-deployment.yaml" in os.listdir(os.path.join(out, "myproject"))
