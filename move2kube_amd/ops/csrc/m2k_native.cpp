@@ -120,7 +120,19 @@ py::tuple walk(const std::string &root) {
       r.kinds.push_back(S_ISLNK(st.st_mode) ? K_SYMLINK : K_FILE);
     }
   }
-  return py::make_tuple(r.paths, r.kinds, r.errors);
+  // File names are bytes: decode them like os.fsdecode (surrogateescape), so a
+  // name that is not UTF-8 round-trips instead of failing the whole walk.
+  auto fsdecode = [](const std::string &s) {
+    PyObject *o = PyUnicode_DecodeFSDefaultAndSize(s.data(), static_cast<Py_ssize_t>(s.size()));
+    if (!o) throw py::error_already_set();
+    return py::reinterpret_steal<py::str>(o);
+  };
+  py::list paths(r.paths.size());
+  for (size_t i = 0; i < r.paths.size(); i++) paths[i] = fsdecode(r.paths[i]);
+  py::list errors(r.errors.size());
+  for (size_t i = 0; i < r.errors.size(); i++)
+    errors[i] = py::make_tuple(fsdecode(r.errors[i].first), fsdecode(r.errors[i].second));
+  return py::make_tuple(paths, r.kinds, errors);
 }
 
 // ----------------------------------------------------------------------------
@@ -824,7 +836,7 @@ static int remove_dir_contents(int dfd, const std::string &path, std::string &er
   return err;
 }
 
-std::pair<int, std::string> remove_tree(const std::string &path) {
+std::pair<int, py::bytes> remove_tree(const std::string &path) {
   std::string errpath;
   int err = 0;
   {
@@ -846,7 +858,7 @@ std::pair<int, std::string> remove_tree(const std::string &path) {
       }
     }
   }
-  return {err, errpath};
+  return {err, py::bytes(errpath)};  // raw bytes: the caller decodes with os.fsdecode
 }
 
 // yaml_emit.cpp

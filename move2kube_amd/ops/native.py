@@ -37,8 +37,14 @@ def module():
     return _load()
 
 
+# Paths cross into C++ as bytes (os.fsencode: a file name that is not UTF-8
+# arrives in Python with surrogates and goes back out as the same bytes);
+# paths coming back are decoded the same way (m2k_native.cpp:walk).
+_fsencode = os.fsencode
+
+
 def walk(root):
-    return _load().walk(root)
+    return _load().walk(_fsencode(root))
 
 
 def crc64_ecma(data):
@@ -60,7 +66,7 @@ def fnv64a(data):
 def sniff_dockerfiles(paths, nthreads=8):
     m = _load()
     if m is not None:
-        return m.sniff_dockerfiles(paths, nthreads)
+        return m.sniff_dockerfiles([_fsencode(p) for p in paths], nthreads)
     from ..source.dockerfile_parser import sniff_first_from
     return [sniff_first_from(p) for p in paths]
 
@@ -76,9 +82,9 @@ def remove_tree(path):
         else:
             os.remove(path)
         return
-    err, where = m.remove_tree(path)
+    err, where = m.remove_tree(_fsencode(path))
     if err:
-        raise OSError(err, os.strerror(err), where)
+        raise OSError(err, os.strerror(err), os.fsdecode(where))
 
 
 _write_threads = None
@@ -98,7 +104,7 @@ def write_files(items, nthreads=None):
     m = _load()
     if m is not None:
         paths = [p for p, _, _ in items]
-        errs = m.write_files(paths, datas, [int(md) for _, _, md in items], nthreads)
+        errs = m.write_files([_fsencode(p) for p in paths], datas, [int(md) for _, _, md in items], nthreads)
         return [OSError(e, os.strerror(e), p) if e else None for p, e in zip(paths, errs)]
     out = []
     for (p, _, md), data in zip(items, datas):
@@ -114,5 +120,6 @@ def write_files(items, nthreads=None):
 def run_commands(argvs, cwds, parallel=8, timeout_s=0.0):
     m = _load()
     if m is not None:
-        return m.run_commands(argvs, cwds, parallel, timeout_s)
+        return m.run_commands([[_fsencode(a) for a in argv] for argv in argvs], [_fsencode(c) for c in cwds],
+                              parallel, timeout_s)
     return None

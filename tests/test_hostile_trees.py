@@ -80,3 +80,18 @@ def test_a_deeply_nested_yaml_only_loses_itself(tmp_path):
     with api.Session(qaskip=True) as s:
         out = _bounded(lambda: s.translate(str(src), str(tmp_path / "out")), 120)
     assert "web-deployment.yaml" in os.listdir(os.path.join(out, "myproject"))
+
+
+def test_translate_a_tree_with_non_utf8_file_names(tmp_path):
+    """A file or directory name that is not UTF-8 does not fail the walk: the
+    services of the tree are still planned and translated."""
+    clean = _tree(tmp_path / "a", "src")
+    src = _tree(tmp_path / "b", "src")
+    bsrc = os.fsencode(str(src))
+    os.makedirs(os.path.join(bsrc, b"caf\xe9"))
+    with open(os.path.join(bsrc, b"caf\xe9", b"notes\xff.txt"), "wb") as f:
+        f.write(b"x\n")
+    with api.Session(qaskip=True) as s:
+        want = s.translate(str(clean), str(tmp_path / "out-clean"))
+        got = _bounded(lambda: s.translate(str(src), str(tmp_path / "out")), 60)
+    assert sorted(os.listdir(os.path.join(got, "myproject"))) == sorted(os.listdir(os.path.join(want, "myproject")))

@@ -120,3 +120,23 @@ def test_remove_tree(tmp_path):
     assert not f.exists()
     with pytest.raises(OSError):
         nat.remove_tree(str(tmp_path / "nope"))
+
+
+@needs_native
+def test_non_utf8_file_names_round_trip(tmp_path):
+    """File names are bytes on Linux: a Latin-1 name walks, is written and is
+    removed through the native runtime like os.fsencode/os.fsdecode would."""
+    root = os.fsencode(str(tmp_path))
+    os.makedirs(os.path.join(root, b"d\xe9"))
+    with open(os.path.join(root, b"d\xe9", b"caf\xe9.yaml"), "wb") as f:
+        f.write(b"a: 1\n")
+    paths, kinds, errors = native.walk(str(tmp_path))
+    ppaths, pkinds, perrors = fsindex._walk_py(str(tmp_path))
+    assert list(paths) == list(ppaths) and list(kinds) == list(pkinds) and not errors
+    assert any(os.fsencode(p).endswith(b"caf\xe9.yaml") for p in paths)
+    out = os.path.join(os.fsdecode(root), os.fsdecode(b"out\xff.txt"))
+    assert native.write_files([(out, b"x", 0o644)]) == [None]
+    with open(os.fsencode(out), "rb") as f:
+        assert f.read() == b"x"
+    native.remove_tree(os.fsdecode(os.path.join(root, b"d\xe9")))
+    assert not os.path.exists(os.path.join(root, b"d\xe9"))
