@@ -281,7 +281,7 @@ std::string sniff_one(const std::string &path) {
   return result;
 }
 
-std::vector<std::string> sniff_dockerfiles(const std::vector<std::string> &paths, int nthreads) {
+static std::vector<std::string> sniff_all(const std::vector<std::string> &paths, int nthreads) {
   std::vector<std::string> out(paths.size());
   py::gil_scoped_release nogil;
   if (nthreads <= 1 || paths.size() < 64) {
@@ -301,6 +301,20 @@ std::vector<std::string> sniff_dockerfiles(const std::vector<std::string> &paths
     });
   }
   for (auto &th : pool) th.join();
+  return out;
+}
+
+// FROM lines are file bytes: decoded as UTF-8 with surrogateescape, like the
+// Python sniffer (dockerfile_parser.py:sniff_first_from), so a Latin-1 byte in
+// one Dockerfile does not fail the whole batch.
+py::list sniff_dockerfiles(const std::vector<std::string> &paths, int nthreads) {
+  std::vector<std::string> raw = sniff_all(paths, nthreads);
+  py::list out(raw.size());
+  for (size_t i = 0; i < raw.size(); i++) {
+    PyObject *o = PyUnicode_DecodeUTF8(raw[i].data(), static_cast<Py_ssize_t>(raw[i].size()), "surrogateescape");
+    if (!o) throw py::error_already_set();
+    out[i] = py::reinterpret_steal<py::str>(o);
+  }
   return out;
 }
 

@@ -140,3 +140,14 @@ def test_non_utf8_file_names_round_trip(tmp_path):
         assert f.read() == b"x"
     native.remove_tree(os.fsdecode(os.path.join(root, b"d\xe9")))
     assert not os.path.exists(os.path.join(root, b"d\xe9"))
+
+
+@needs_native
+def test_sniff_dockerfiles_undecodable_from_line(tmp_path):
+    """A Latin-1 byte in a FROM line is kept as a surrogate, as the Python
+    sniffer does, instead of failing the batch (threaded and serial paths)."""
+    p = tmp_path / "Dockerfile"
+    p.write_bytes(b"FROM caf\xe9:1\nRUN x\n")
+    want = dockerfile_parser.sniff_first_from(str(p))
+    assert native.sniff_dockerfiles([str(p)]) == [want]
+    assert native.sniff_dockerfiles([str(p)] * 100) == [want] * 100
