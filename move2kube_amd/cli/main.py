@@ -6,7 +6,9 @@ Verbs and flags match the reference: ``collect [-a] [-o] [-s]``,
 """
 
 import argparse
+import errno
 import os
+import stat
 import sys
 
 from .. import assets
@@ -35,19 +37,37 @@ def _abs(p):
     return os.path.abspath(p) if p else p
 
 
+def _go_stat(path):
+    """``os.Stat``: (stat result, None) or (None, (errno, Go error string))."""
+    try:
+        return os.stat(path), None
+    except OSError as e:
+        msg = os.strerror(e.errno) if e.errno else str(e)
+        return None, (e.errno, "stat %s: %s" % (path, msg[:1].lower() + msg[1:]))
+
+
 def check_source_path(src):
-    if not os.path.exists(src):
-        log.fatal("The given source directory %s does not exist. Error: %r", src,
-                  "stat %s: no such file or directory" % src)
-    if not os.path.isdir(src):
+    """translate.go:54-65: only ENOENT is "does not exist"; any other stat
+    error (ENOTDIR, EACCES, ELOOP...) is an access error."""
+    st, err = _go_stat(src)
+    if err and err[0] == errno.ENOENT:
+        log.fatal("The given source directory %s does not exist. Error: %r", src, err[1])
+    if err:
+        log.fatal("Error while accessing the given source directory %s Error: %r", src, err[1])
+    if not stat.S_ISDIR(st.st_mode):
         log.fatal("The given source path %s is a file. Expected a directory. Exiting.", src)
 
 
 def check_output_path(out):
-    if not os.path.exists(out):
+    """translate.go:67-80 (an output path under a regular file is an access
+    error here, before any planning, not a failed MkdirAll afterwards)."""
+    st, err = _go_stat(out)
+    if err and err[0] == errno.ENOENT:
         log.debug("Translated artifacts will be written to %s", out)
         return
-    if not os.path.isdir(out):
+    if err:
+        log.fatal("Error while accessing output directory at path %s Error: %r . Exiting", out, err[1])
+    if not stat.S_ISDIR(st.st_mode):
         log.fatal("Output path %s is a file. Expected a directory. Exiting", out)
     log.info("Output directory %s exists. The contents might get overwritten.", out)
 
@@ -113,16 +133,20 @@ def translate_handler(a):
 def plan_handler(a):
     planfile = _abs(a.plan)
     srcpath = _abs(a.source)
-    if not os.path.exists(srcpath):
-        log.fatal("Unable to access source directory : stat %s: no such file or directory", srcpath)
-    if not os.path.isdir(srcpath):
+    st, err = _go_stat(srcpath)
+    if err:
+        log.fatal("Unable to access source directory : %s", err[1])
+    if not stat.S_ISDIR(st.st_mode):
         log.fatal("Input is a file, expected directory: %s", srcpath)
-    if not os.path.exists(planfile):
+    pst, err = _go_stat(planfile)
+    if err and err[0] != errno.ENOENT:
+        log.fatal("Error while accessing plan file path %s : %s ", planfile, err[1])
+    if err:
         # (the reference tests the trailing separator on the already-cleaned
         # absolute path, so only an extension-less base name selects a directory)
         if planfile.endswith(os.sep) or "." not in os.path.basename(planfile):
             planfile = os.path.join(planfile, DEFAULT_PLAN_FILE)
-    elif os.path.isdir(planfile):
+    elif stat.S_ISDIR(pst.st_mode):
         planfile = os.path.join(planfile, DEFAULT_PLAN_FILE)
     p = move2kube.create_plan(srcpath, a.name)
     try:
@@ -142,9 +166,12 @@ def collect_handler(a):
     srcpath = ""
     if a.source:
         srcpath = _abs(a.source)
-        if not os.path.exists(srcpath):
-            log.fatal("Source directory does not exist: stat %s: no such file or directory.", srcpath)
-        if not os.path.isdir(srcpath):
+        st, err = _go_stat(srcpath)
+        if err and err[0] == errno.ENOENT:
+            log.fatal("Source directory does not exist: %s.", err[1])
+        if err:
+            log.fatal("Error while accessing directory: %s. ", srcpath)
+        if not stat.S_ISDIR(st.st_mode):
             log.fatal("Source path is a file, expected directory: %s.", srcpath)
     outpath = os.path.join(os.path.normpath(outpath), APP_NAME_SHORT + "_collect")
     annotations = a.annotations.split(",") if a.annotations else []

@@ -15,6 +15,50 @@ DEBUG, INFO, WARNING, ERROR, CRITICAL = 10, 20, 30, 40, 50
 _LEVEL_NAMES = {DEBUG: "DEBU", INFO: "INFO", WARNING: "WARN", ERROR: "ERRO", CRITICAL: "FATA"}
 
 
+_GO_ESC = {"\a": "\\a", "\b": "\\b", "\f": "\\f", "\n": "\\n", "\r": "\\r", "\t": "\\t",
+           "\v": "\\v", "\\": "\\\\", '"': '\\"'}
+
+
+def go_quote(s):
+    """``strconv.Quote``: what the reference's ``%q`` prints for a string.
+    Bytes that were not UTF-8 (surrogateescape) come out as ``\\xNN``."""
+    out = ['"']
+    for ch in s:
+        e = _GO_ESC.get(ch)
+        if e is not None:
+            out.append(e)
+            continue
+        o = ord(ch)
+        if 0xDC80 <= o <= 0xDCFF:
+            out.append("\\x%02x" % (o - 0xDC00))
+        elif o < 0x20 or o == 0x7F:
+            out.append("\\x%02x" % o)
+        elif ch.isprintable() or ch == " ":
+            out.append(ch)
+        elif o < 0x10000:
+            out.append("\\u%04x" % o)
+        else:
+            out.append("\\U%08x" % o)
+    out.append('"')
+    return "".join(out)
+
+
+class _GoQ(str):
+    """A string argument of a ``%r`` in a log format: printed as Go's ``%q``
+    (double quotes) rather than Python's repr; ``%s`` is unchanged."""
+
+    __slots__ = ()
+
+    def __repr__(self):
+        return go_quote(self)
+
+
+def _format(msg, args):
+    if "%r" in msg:
+        args = tuple(_GoQ(a) if type(a) is str else a for a in args)
+    return msg % args
+
+
 class FatalError(RuntimeError):
     """Raised where the reference calls ``log.Fatalf``."""
 
@@ -39,7 +83,7 @@ class _Logger:
         if level < self.level:
             return
         try:
-            text = msg % args if args else msg
+            text = _format(msg, args) if args else msg
         except (TypeError, ValueError):
             text = "%s %r" % (msg, args)
         line = "%s[%04d] %s\n" % (_LEVEL_NAMES.get(level, "INFO"), int(time.time() - _START), text)
@@ -135,4 +179,4 @@ def error(msg, *args):
 
 def fatal(msg, *args):
     logger.critical(msg, *args)
-    raise FatalError(msg % args if args else msg)
+    raise FatalError(_format(msg, args) if args else msg)

@@ -124,6 +124,35 @@ def test_translate_output_path_is_a_file(work):
     assert cli.main(["translate", "-s", str(work / "src"), "-o", str(work / "out"), "--qaskip"]) == 1
 
 
+@pytest.mark.parametrize("argv,want", [
+    (["plan", "-s", "{w}/file/x"], "FATA[0000] Unable to access source directory : stat {w}/file/x: not a directory"),
+    (["plan", "-s", "{w}/src", "-p", "{w}/file/p.yaml"],
+     "FATA[0000] Error while accessing plan file path {w}/file/p.yaml : stat {w}/file/p.yaml: not a directory "),
+    (["translate", "-s", "{w}/file/x", "--qaskip"],
+     'FATA[0000] Error while accessing the given source directory {w}/file/x Error: "stat {w}/file/x: not a directory"'),
+    (["translate", "-s", "{w}/nope", "--qaskip"],
+     'FATA[0000] The given source directory {w}/nope does not exist. Error: "stat {w}/nope: no such file or directory"'),
+    (["translate", "-s", "{w}/src", "-o", "{w}/file", "--qaskip"],
+     'FATA[0000] Error while accessing output directory at path {w}/file/myproject Error: '
+     '"stat {w}/file/myproject: not a directory" . Exiting'),
+    (["collect", "-s", "{w}/file/x"], "FATA[0000] Error while accessing directory: {w}/file/x. "),
+])
+def test_stat_errors_are_reported_like_os_stat(work, capsys, argv, want):
+    """cmd/move2kube/{plan,translate,collect}.go: only ENOENT is "does not
+    exist"; ENOTDIR and the like are access errors, with Go's %q quoting."""
+    (work / "file").write_text("x")
+    w = str(work)
+    assert cli.main([a.format(w=w) for a in argv]) == 1
+    lines = [ln[:4] + ln[10:] for ln in capsys.readouterr().err.splitlines()]  # without the [ssss] clock
+    assert want.format(w=w).replace("[0000]", "", 1) in lines
+
+
+def test_log_quotes_like_go():
+    from move2kube_amd.utils import log
+    assert log.go_quote('a"b\\c\n\x01\xe9\udce9\u200b') == '"a\\"b\\\\c\\n\\x01\xe9\\xe9\\u200b"'
+    assert log._format("%r and %s and %r", ("it's", "x", 3)) == '"it\'s" and x and 3'
+
+
 def test_version(capsys):
     assert cli.main(["version"]) == 0
     short = capsys.readouterr().out.strip()

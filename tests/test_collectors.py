@@ -260,7 +260,7 @@ def test_collectors_run_concurrently_with_ordered_logs(monkeypatch, tmp_path):
     assert time.perf_counter() - t0 < 0.55
     msgs = [line.split("] ", 1)[1] for line in buf.getvalue().splitlines()]
     assert msgs == ["Begin collection", "[a] Begin collection", "a working", "[a] Done", "[b] Begin collection",
-                    "b working", "[b] failed. Error: 'boom'", "[c] Begin collection", "c working", "[c] Done",
+                    "b working", '[b] failed. Error: "boom"', "[c] Begin collection", "c working", "[c] Done",
                     "Collection done"]
     buf.truncate(0)
     buf.seek(0)
