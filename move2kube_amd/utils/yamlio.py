@@ -804,6 +804,68 @@ _UNSUPPORTED = object()
 _native_load = None
 
 
+def _allowed_alias_ratio(decoded):
+    """go-yaml v3 decode.go allowedAliasRatio: 99% of the nodes may come
+    through aliases up to 400k decoded nodes, falling to 10% at 4M."""
+    if decoded <= 400000:
+        return 0.99
+    if decoded >= 4000000:
+        return 0.10
+    return 0.99 - 0.89 * (decoded - 400000) / 3600000.0
+
+
+def _check_aliasing(doc, error):
+    """Reject a document the way go-yaml v3 does before it is walked: an
+    anchor that contains itself, or aliases that expand it far beyond its text
+    ("billion laughs").  PyYAML shares one object per anchor, so the load is
+    cheap, but every later walk (copies, conversions, emission) would expand
+    it.  Counted on the loaded tree: every container object is one node
+    however often it is referenced; ``decoded`` counts each reference's
+    subtree again, as go-yaml's decoder does.  (The reference checks the
+    ratio while decoding; checked here once over the whole document.)"""
+    if not isinstance(doc, (dict, list)):
+        return
+    expanded = {}          # id -> nodes decoded for one reference to it
+    unique = 0
+    on_path = set()
+    stack = [(doc, False)]
+    while stack:
+        o, done = stack.pop()
+        i = id(o)
+        if done:
+            on_path.discard(i)
+            n = 1
+            if isinstance(o, dict):
+                for k, v in o.items():
+                    n += 1 + (expanded[id(v)] if isinstance(v, (dict, list)) else 1)
+            else:
+                for v in o:
+                    n += expanded[id(v)] if isinstance(v, (dict, list)) else 1
+            expanded[i] = n
+            if n > 4000000 * 4:
+                break
+            continue
+        if i in expanded:
+            continue
+        if i in on_path:
+            raise error("anchor value contains itself")
+        on_path.add(i)
+        vals = o.values() if isinstance(o, dict) else o
+        unique += 1 + (len(o) if isinstance(o, dict) else 0) + sum(1 for v in vals if not isinstance(v, (dict, list)))
+        stack.append((o, True))
+        for v in vals:
+            if isinstance(v, (dict, list)) and id(v) not in expanded:
+                if id(v) in on_path:
+                    raise error("anchor value contains itself")
+                stack.append((v, False))
+    decoded = expanded.get(id(doc))
+    if decoded is None:  # stopped early: far past any allowed expansion
+        raise error("document contains excessive aliasing")
+    aliased = decoded - unique
+    if aliased > 100 and decoded > 1000 and aliased / decoded > _allowed_alias_ratio(decoded):
+        raise error("document contains excessive aliasing")
+
+
 def _native_loader():
     global _native_load
     if _native_load is None:
@@ -829,8 +891,13 @@ def _parse(text, mode, multi):
     loader = (lz.typed, lz.v2, lz.raw)[mode]
     try:
         if multi:
-            return list(lz.yaml.load_all(text, Loader=loader))
-        return lz.yaml.load(text, Loader=loader)
+            docs = list(lz.yaml.load_all(text, Loader=loader))
+        else:
+            docs = lz.yaml.load(text, Loader=loader)
+        if "*" in text:
+            for d in (docs if multi else (docs,)):
+                _check_aliasing(d, lz.yaml.YAMLError)
+        return docs
     except UnicodeError as e:
         # bytes that are not UTF-8 (kept as surrogates by read_text): a parse
         # error of this document, as go-yaml reports "invalid leading UTF-8

@@ -95,3 +95,38 @@ def test_translate_a_tree_with_non_utf8_file_names(tmp_path):
         want = s.translate(str(clean), str(tmp_path / "out-clean"))
         got = _bounded(lambda: s.translate(str(src), str(tmp_path / "out")), 60)
     assert sorted(os.listdir(os.path.join(got, "myproject"))) == sorted(os.listdir(os.path.join(want, "myproject")))
+
+
+def _laughs(levels=10, width=9):
+    lines = ['a0: &a0 [%s]' % ",".join(['"x"'] * width)]
+    for i in range(1, levels):
+        lines.append("a%d: &a%d [%s]" % (i, i, ",".join(["*a%d" % (i - 1)] * width)))
+    return "\n".join("  " + ln for ln in lines) + "\n"
+
+
+def test_yaml_alias_expansion_is_refused_like_go_yaml():
+    """go-yaml v3 fails "document contains excessive aliasing" and "anchor
+    value contains itself"; the loaded tree would otherwise be expanded by
+    every later walk (9**10 nodes here)."""
+    from move2kube_amd.utils import yamlio
+    with pytest.raises(yamlio._lz().yaml.YAMLError, match="excessive aliasing"):
+        _bounded(lambda: yamlio.load("data:\n" + _laughs()), 10)
+    with pytest.raises(yamlio._lz().yaml.YAMLError, match="contains itself"):
+        yamlio.load("a: &a [1, *a]\n")
+    legit = "a: &a {" + ", ".join("k%d: v" % i for i in range(30)) + "}\nl:\n" + "- *a\n" * 50
+    assert len(yamlio.load(legit)["l"]) == 50 and yamlio.load("b: &b {x: 1}\nm:\n  <<: *b\n  y: 2\n")["m"] == {
+        "x": 1, "y": 2}
+
+
+def test_a_yaml_bomb_only_loses_itself(tmp_path):
+    src = tmp_path / "src"
+    src.mkdir()
+    (src / "bomb.yaml").write_text("apiVersion: v1\nkind: ConfigMap\nmetadata:\n  name: b\ndata:\n" + _laughs())
+    (src / "compose.yml").write_text("version: '3'\nx-b:\n" + _laughs() + "services:\n  web:\n    image: nginx\n")
+    (src / "dep.yaml").write_text(
+        "apiVersion: apps/v1\nkind: Deployment\nmetadata:\n  name: web\nspec:\n  selector:\n    matchLabels:\n"
+        "      app: web\n  template:\n    metadata:\n      labels:\n        app: web\n    spec:\n      containers:\n"
+        "      - name: web\n        image: nginx:1.19\n")
+    with api.Session(qaskip=True) as s:
+        out = _bounded(lambda: s.translate(str(src), str(tmp_path / "out")), 60)
+    assert "web-deployment.yaml" in os.listdir(os.path.join(out, "myproject"))
