@@ -785,10 +785,9 @@ def _memoized(kind, text, parse):
     ok, val = hit
     if not ok:
         raise val.with_traceback(None)
-    try:
-        return _tree_copy(val)
-    except RecursionError:  # self-referencing aliases
-        return copy.deepcopy(val)
+    # (self-containing anchors were refused by _check_aliasing; a document too
+    # deep to copy raises RecursionError and its caller skips the file)
+    return _tree_copy(val)
 
 
 _MISS = object()
