@@ -66,6 +66,67 @@ EXTRA_CONFIGS = {
     "samples-yamls": ("samples", "samples", [], False, None),
 }
 
+# The capability surface beyond the five BASELINE configurations, pinned by
+# expected trees in ``tests/golden/reference/coverage/<name>``
+# (``tests/test_coverage_trees.py``).  QA answers are given as a dict
+# {question: answer} and written to a cache file when the run is prepared.
+PROFILES = ("AWS-EKS", "Azure-AKS", "GCP-GKE", "IBM-IKS", "IBM-Openshift", "Kubernetes", "Openshift")
+GOLDEN_COVERAGE = os.path.join(GOLDEN_REF, "coverage")
+CARRIED_OVER = os.path.join(FIXTURES, "carried_over")
+GIT_REPOS = os.path.join(FIXTURES, "git_repos")
+Q_ARTIFACT = "Choose the artifact type:"
+Q_CLUSTER = "Choose the cluster type:"
+
+
+def _coverage_configs():
+    out = {}
+    for p in PROFILES:
+        # samples/ in Yamls mode on every built-in cluster profile
+        out["profiles/" + p] = ("samples", "samples", {Q_CLUSTER: p}, False, None)
+    out["artifacts/knative-kubernetes"] = ("samples", "samples", {Q_ARTIFACT: "Knative"}, False, None)
+    out["artifacts/knative-openshift"] = ("samples", "samples", {Q_ARTIFACT: "Knative", Q_CLUSTER: "Openshift"},
+                                          False, None)
+    out["artifacts/helm-kubernetes"] = ("samples", "samples", {Q_ARTIFACT: "Helm"}, False, None)
+    for p in ("Kubernetes", "Openshift", "AWS-EKS", "IBM-Openshift"):
+        # old-version Kubernetes/OpenShift YAMLs carried over to each profile
+        out["carried-over/" + p] = ("carried", "carried", {Q_CLUSTER: p}, False, None)
+    # source trees that are git repos with an origin remote
+    out["git-repos"] = ("git", "git", {}, False, None)
+    return out
+
+
+COVERAGE_CONFIGS = _coverage_configs()
+
+
+def _lookup(name):
+    for table in (CONFIGS, EXTRA_CONFIGS, COVERAGE_CONFIGS):
+        if name in table:
+            return table[name]
+    raise KeyError(name)
+
+
+def golden_dir(name):
+    return os.path.join(GOLDEN_COVERAGE if name in COVERAGE_CONFIGS else GOLDEN_REF, name)
+
+
+def qacache_text(answers):
+    """A ``QACache`` file answering Select questions (``types/qaengine/cache.go``)."""
+    lines = ["apiVersion: move2kube.konveyor.io/v1alpha1", "kind: QACache", "spec:", "  solutions:"]
+    for desc, ans in answers.items():
+        lines += ["    - description: '%s'" % desc, "      solution:", "        type: Select",
+                  "        answer:", "          - %s" % ans, "      resolved: true"]
+    return "\n".join(lines) + "\n"
+
+
+def _copy_git_repos(dst):
+    """``tests/fixtures/git_repos``: every ``dot-git`` directory becomes ``.git``
+    (a nested ``.git`` cannot be committed)."""
+    shutil.copytree(GIT_REPOS, dst, symlinks=True)
+    for dp, dns, _fns in os.walk(dst):
+        if "dot-git" in dns:
+            os.rename(os.path.join(dp, "dot-git"), os.path.join(dp, ".git"))
+            dns.remove("dot-git")
+
 
 class Run:
     """One prepared configuration: inputs copied under ``work``."""
@@ -73,10 +134,14 @@ class Run:
     def __init__(self, name, work):
         self.name = name
         self.work = os.path.abspath(work)
-        layout, src, caches, cnb, collect = CONFIGS[name] if name in CONFIGS else EXTRA_CONFIGS[name]
+        layout, src, caches, cnb, collect = _lookup(name)
         self.layout = layout
         self.src = os.path.join(self.work, src)
-        self.caches = [os.path.join(CONFIG_FIXTURES, c) for c in caches]
+        self.answers = caches if isinstance(caches, dict) else None
+        if self.answers is not None:
+            self.caches = [os.path.join(self.work, "qacache.yaml")] if self.answers else []
+        else:
+            self.caches = [os.path.join(CONFIG_FIXTURES, c) for c in caches]
         self.cnb = cnb
         self.collect_annotations = collect
         self.outdir = os.path.join(self.work, "out")
@@ -99,6 +164,13 @@ class Run:
                 shutil.copytree(os.path.join(SAMPLES, d), os.path.join(root, d), symlinks=True)
         elif self.layout == "cf":
             shutil.copytree(CF_APP, os.path.join(self.work, "cf"), symlinks=True)
+        elif self.layout == "carried":
+            shutil.copytree(CARRIED_OVER, self.src, symlinks=True)
+        elif self.layout == "git":
+            _copy_git_repos(self.src)
+        if self.answers:
+            with open(self.caches[0], "w") as f:
+                f.write(qacache_text(self.answers))
         return self
 
     def env(self, base=None):
@@ -207,20 +279,75 @@ def tree_files(root):
     return out
 
 
-def diff_files(actual_root, expected_root):
-    """Relative paths that differ, are missing or are extra (sorted)."""
+WORK_PLACEHOLDER = b"$WORK"
+
+
+def diff_files(actual_root, expected_root, work=None):
+    """Relative paths that differ, are missing or are extra (sorted).  With
+    ``work``, that directory's path in the actual files reads as ``$WORK``
+    (the QA cache records absolute ``~/.ssh`` paths under the run's HOME)."""
     a, g = tree_files(actual_root), tree_files(expected_root)
     bad = sorted(set(a) ^ set(g))
     for rel in sorted(set(a) & set(g)):
         with open(a[rel], "rb") as fa, open(g[rel], "rb") as fg:
-            if fa.read() != fg.read():
+            data = fa.read()
+            if work:
+                data = data.replace(os.fsencode(work), WORK_PLACEHOLDER)
+            if data != fg.read():
                 bad.append(rel)
     return sorted(bad)
 
 
+def write_expected_tree(name, actual_root, work):
+    """Copy a run's output to ``golden_dir(name)`` with the work directory
+    replaced by ``$WORK``.  Only ``python benchmarks/refconfigs.py --write``
+    calls this: expected trees change by reviewed commits, never from tests."""
+    dst = golden_dir(name)
+    shutil.rmtree(dst, ignore_errors=True)
+    for rel, src in tree_files(actual_root).items():
+        out = os.path.join(dst, rel)
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        with open(src, "rb") as f:
+            data = f.read().replace(os.fsencode(work), WORK_PLACEHOLDER)
+        with open(out, "wb") as f:
+            f.write(data)
+        shutil.copymode(src, out)
+    return dst
+
+
+def _main(argv):
+    import argparse
+    import tempfile
+    ap = argparse.ArgumentParser(description="write expected trees of coverage configurations")
+    ap.add_argument("--write", nargs="+", required=True, metavar="NAME",
+                    help="coverage configurations (or 'all') whose expected tree is (re)written")
+    args = ap.parse_args(argv)
+    names = sorted(COVERAGE_CONFIGS) if args.write == ["all"] else args.write
+    sys.path.insert(0, ROOT)
+    for name in names:
+        if name not in COVERAGE_CONFIGS:
+            raise SystemExit("not a coverage configuration: %s" % name)
+        work = tempfile.mkdtemp(prefix="m2k-cov-")
+        try:
+            run = Run(name, work).prepare()
+            undo = run.apply_env()
+            try:
+                with run.session() as s:
+                    out = run.step(s)
+            finally:
+                undo()
+            print(write_expected_tree(name, out, run.work))
+        finally:
+            shutil.rmtree(work, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    _main(sys.argv[1:])
+
+
 def manifest_diff_vs_ref(name, actual_root):
     """Number of files differing from the reference-derived expected tree."""
-    golden = os.path.join(GOLDEN_REF, name)
+    golden = golden_dir(name)
     if not os.path.isdir(golden):
         return None
     return len(diff_files(actual_root, golden))

@@ -99,19 +99,67 @@ _META = "inline:TypeMeta metadata:ObjectMeta,o "
 _def("Pod", _META + "spec:PodSpec,o status:PodStatus,o")
 _def("Deployment", _META + "spec:DeploymentSpec,o status:DeploymentStatus,o")
 _def("DeploymentSpec", "replicas:*int,o selector:*LabelSelector template:PodTemplateSpec strategy:DeploymentStrategy,o "
-     "minReadySeconds:int,o revisionHistoryLimit:*int,o paused:bool,o rollbackTo:*any,o progressDeadlineSeconds:*int,o")
+     "minReadySeconds:int,o revisionHistoryLimit:*int,o paused:bool,o progressDeadlineSeconds:*int,o")
+# extensions/v1beta1 and apps/v1beta1: selector is omitempty and rollbackTo exists
+_def("DeploymentV1beta1", _META + "spec:DeploymentSpecV1beta1,o status:DeploymentStatus,o")
+_def("DeploymentSpecV1beta1", "replicas:*int,o selector:*LabelSelector,o template:PodTemplateSpec "
+     "strategy:DeploymentStrategy,o minReadySeconds:int,o revisionHistoryLimit:*int,o paused:bool,o "
+     "rollbackTo:*any,o progressDeadlineSeconds:*int,o")
 _def("DeploymentStrategy", "type:string,o rollingUpdate:*any,o")
 _def("DeploymentStatus", "observedGeneration:int,o replicas:int,o updatedReplicas:int,o readyReplicas:int,o "
      "availableReplicas:int,o unavailableReplicas:int,o conditions:[]any,o collisionCount:*int,o")
 _def("DaemonSet", _META + "spec:DaemonSetSpec,o status:DaemonSetStatus,o")
 _def("DaemonSetSpec", "selector:*LabelSelector template:PodTemplateSpec updateStrategy:DaemonSetUpdateStrategy,o "
-     "minReadySeconds:int,o templateGeneration:int,o revisionHistoryLimit:*int,o")
+     "minReadySeconds:int,o revisionHistoryLimit:*int,o")
+# extensions/v1beta1: selector is omitempty and templateGeneration exists
+_def("DaemonSetV1beta1", _META + "spec:DaemonSetSpecV1beta1,o status:DaemonSetStatus,o")
+_def("DaemonSetSpecV1beta1", "selector:*LabelSelector,o template:PodTemplateSpec "
+     "updateStrategy:DaemonSetUpdateStrategy,o minReadySeconds:int,o templateGeneration:int,o "
+     "revisionHistoryLimit:*int,o")
 _def("DaemonSetUpdateStrategy", "type:string,o rollingUpdate:*any,o")
 _def("DaemonSetStatus", "currentNumberScheduled:int numberMisscheduled:int desiredNumberScheduled:int numberReady:int "
      "observedGeneration:int,o updatedNumberScheduled:int,o numberAvailable:int,o numberUnavailable:int,o "
      "collisionCount:*int,o conditions:[]any,o")
-_def("StatefulSet", _META + "spec:any,o status:any,o")
-_def("ReplicaSet", _META + "spec:any,o status:any,o")
+_def("StatefulSet", _META + "spec:StatefulSetSpec,o status:StatefulSetStatus,o")
+_def("StatefulSetSpec", "replicas:*int,o selector:*LabelSelector template:PodTemplateSpec "
+     "volumeClaimTemplates:[]PersistentVolumeClaim,o serviceName:string podManagementPolicy:string,o "
+     "updateStrategy:StatefulSetUpdateStrategy,o revisionHistoryLimit:*int,o")
+_def("StatefulSetUpdateStrategy", "type:string,o rollingUpdate:*any,o")
+_def("StatefulSetStatus", "observedGeneration:int,o replicas:int readyReplicas:int,o currentReplicas:int,o "
+     "updatedReplicas:int,o currentRevision:string,o updateRevision:string,o collisionCount:*int,o "
+     "conditions:[]any,o")
+# apps/v1beta1: selector is omitempty, status.observedGeneration is a pointer
+_def("StatefulSetV1beta1", _META + "spec:StatefulSetSpecV1beta1,o status:StatefulSetStatusV1beta1,o")
+_def("StatefulSetSpecV1beta1", "replicas:*int,o selector:*LabelSelector,o template:PodTemplateSpec "
+     "volumeClaimTemplates:[]PersistentVolumeClaim,o serviceName:string podManagementPolicy:string,o "
+     "updateStrategy:StatefulSetUpdateStrategy,o revisionHistoryLimit:*int,o")
+_def("StatefulSetStatusV1beta1", "observedGeneration:*int,o replicas:int readyReplicas:int,o currentReplicas:int,o "
+     "updatedReplicas:int,o currentRevision:string,o updateRevision:string,o collisionCount:*int,o "
+     "conditions:[]any,o")
+_def("ReplicaSet", _META + "spec:ReplicaSetSpec,o status:ReplicaSetStatus,o")
+_def("ReplicaSetSpec", "replicas:*int,o minReadySeconds:int,o selector:*LabelSelector template:PodTemplateSpec,o")
+_def("ReplicaSetV1beta1", _META + "spec:ReplicaSetSpecV1beta1,o status:ReplicaSetStatus,o")
+_def("ReplicaSetSpecV1beta1", "replicas:*int,o minReadySeconds:int,o selector:*LabelSelector,o "
+     "template:PodTemplateSpec,o")
+_def("ReplicaSetStatus", "replicas:int fullyLabeledReplicas:int,o readyReplicas:int,o availableReplicas:int,o "
+     "observedGeneration:int,o conditions:[]any,o")
+_def("CronJob", _META + "spec:CronJobSpec,o status:CronJobStatus,o")
+_def("CronJobSpec", "schedule:string startingDeadlineSeconds:*int,o concurrencyPolicy:string,o suspend:*bool,o "
+     "jobTemplate:JobTemplateSpec successfulJobsHistoryLimit:*int,o failedJobsHistoryLimit:*int,o")
+_def("JobTemplateSpec", "metadata:ObjectMeta,o spec:JobSpec,o")
+_def("CronJobStatus", "active:[]ObjectReference,o lastScheduleTime:*Time,o")
+_def("HorizontalPodAutoscaler", _META + "spec:HPASpec,o status:HPAStatus,o")
+_def("HPASpec", "scaleTargetRef:CrossVersionObjectReference minReplicas:*int,o maxReplicas:int "
+     "targetCPUUtilizationPercentage:*int,o")
+_def("HPAStatus", "observedGeneration:*int,o lastScaleTime:*Time,o currentReplicas:int desiredReplicas:int "
+     "currentCPUUtilizationPercentage:*int,o")
+_def("CrossVersionObjectReference", "kind:string name:string apiVersion:string,o")
+# autoscaling/v2beta1 and v2beta2 share the object shape down to the metric sources
+_def("HorizontalPodAutoscalerV2", _META + "spec:HPASpecV2,o status:HPAStatusV2,o")
+_def("HPASpecV2", "scaleTargetRef:CrossVersionObjectReference minReplicas:*int,o maxReplicas:int "
+     "metrics:[]any,o behavior:*any,o")
+_def("HPAStatusV2", "observedGeneration:*int,o lastScaleTime:*Time,o currentReplicas:int desiredReplicas:int "
+     "currentMetrics:[]any conditions:[]any")
 _def("Job", _META + "spec:JobSpec,o status:JobStatus,o")
 _def("JobSpec", "parallelism:*int,o completions:*int,o activeDeadlineSeconds:*int,o backoffLimit:*int,o "
      "selector:*LabelSelector,o manualSelector:*bool,o template:PodTemplateSpec ttlSecondsAfterFinished:*int,o")
@@ -194,6 +242,14 @@ _def("PolicyRule", "verbs:[]string apiGroups:[]string,o resources:[]string,o res
 _def("RoleBinding", _META + "subjects:[]Subject,o roleRef:RoleRef")
 _def("Subject", "kind:string apiGroup:string,o name:string namespace:string,o")
 _def("RoleRef", "apiGroup:string kind:string name:string")
+_def("RoleBindingV1alpha1", _META + "subjects:[]SubjectV1alpha1,o roleRef:RoleRef")
+_def("SubjectV1alpha1", "kind:string apiVersion:string,o name:string namespace:string,o")
+# authorization.openshift.io/v1 (github.com/openshift/api/authorization/v1)
+_def("RoleOpenShift", _META + "rules:[]PolicyRuleOpenShift")
+_def("PolicyRuleOpenShift", "verbs:[]string attributeRestrictions:RawExtension apiGroups:[]string "
+     "resources:[]string resourceNames:[]string,o nonResourceURLs:[]string,o")
+_def("RoleBindingOpenShift", _META + "userNames:[]string groupNames:[]string subjects:[]ObjectReference "
+     "roleRef:ObjectReference")
 _def("ServiceAccount", _META + "secrets:[]ObjectReference,o imagePullSecrets:[]LocalObjectReference,o "
      "automountServiceAccountToken:*bool,o")
 
@@ -255,7 +311,8 @@ KIND_TYPES = {
     "ImageStream": "ImageStream", "Role": "Role", "RoleBinding": "RoleBinding", "ServiceAccount": "ServiceAccount",
     "Pipeline": "Pipeline", "PipelineRun": "PipelineRun", "EventListener": "EventListener",
     "TriggerBinding": "TriggerBinding", "TriggerTemplate": "TriggerTemplate",
-    "StatefulSet": "StatefulSet", "ReplicaSet": "ReplicaSet",
+    "StatefulSet": "StatefulSet", "ReplicaSet": "ReplicaSet", "CronJob": "CronJob",
+    "HorizontalPodAutoscaler": "HorizontalPodAutoscaler",
 }
 
 
@@ -267,7 +324,23 @@ def type_for(obj):
         return "KnativeService"
     if kind == "Ingress" and gv in ("networking.k8s.io/v1beta1", "extensions/v1beta1"):
         return "IngressV1beta1"
-    return KIND_TYPES.get(kind)
+    v = _VERSIONED.get((gv, kind))
+    return v if v is not None else KIND_TYPES.get(kind)
+
+
+# types whose fields differ between the versions a kind is registered under
+_VERSIONED = {
+    ("extensions/v1beta1", "Deployment"): "DeploymentV1beta1",
+    ("apps/v1beta1", "Deployment"): "DeploymentV1beta1",
+    ("extensions/v1beta1", "DaemonSet"): "DaemonSetV1beta1",
+    ("extensions/v1beta1", "ReplicaSet"): "ReplicaSetV1beta1",
+    ("apps/v1beta1", "StatefulSet"): "StatefulSetV1beta1",
+    ("autoscaling/v2beta1", "HorizontalPodAutoscaler"): "HorizontalPodAutoscalerV2",
+    ("autoscaling/v2beta2", "HorizontalPodAutoscaler"): "HorizontalPodAutoscalerV2",
+    ("rbac.authorization.k8s.io/v1alpha1", "RoleBinding"): "RoleBindingV1alpha1",
+    ("authorization.openshift.io/v1", "Role"): "RoleOpenShift",
+    ("authorization.openshift.io/v1", "RoleBinding"): "RoleBindingOpenShift",
+}
 
 
 # -- typed-decode checks -------------------------------------------------------

@@ -206,7 +206,7 @@ class K8sTransformer(Transformer):
             else:
                 version = versions[0]
             try:
-                obj = convert.convert_to_version(obj, version)
+                obj = (convert.convert_fixed if settings.fixed else convert.convert_to_version)(obj, version)
             except convert.ConversionError as e:
                 log.error("Error while transforming version : %s. Writing in original version.", e)
             objs.append(obj)

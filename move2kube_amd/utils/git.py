@@ -94,25 +94,124 @@ def remote_names(path):
     return list(_read_config(git_dir).keys())
 
 
-def repo_details(path, remote_name):
-    """(remote_urls, branch, repo_dir) like ``GetGitRepoDetails``."""
-    root, git_dir = find_repo(path)
-    branch = ""
+def _common_dir(git_dir):
+    common_file = os.path.join(git_dir, "commondir")
+    try:
+        with open(common_file) as f:
+            return os.path.normpath(os.path.join(git_dir, f.read().strip()))
+    except OSError:
+        return git_dir
+
+
+def _ref_exists(git_dir, ref):
+    """A loose ``refs/...`` file or a ``packed-refs`` line names ``ref``."""
+    for d in (git_dir, _common_dir(git_dir)):
+        if os.path.isfile(os.path.join(d, ref)):
+            return True
+        try:
+            with open(os.path.join(d, "packed-refs")) as f:
+                for line in f:
+                    parts = line.split()
+                    if len(parts) == 2 and parts[1] == ref and not line.startswith(("#", "^")):
+                        return True
+        except OSError:
+            pass
+    return False
+
+
+def head_branch(git_dir):
+    """``filepath.Base(repo.Head().Name())``: go-git resolves HEAD, so a branch
+    without any commit (no ref yet) is an error and gives ''; a detached HEAD
+    is named ``HEAD``."""
     try:
         with open(os.path.join(git_dir, "HEAD")) as f:
             head = f.read().strip()
-        if head.startswith("ref:"):
-            branch = os.path.basename(head[4:].strip())
-        else:
-            branch = "HEAD"
     except OSError:
-        pass
+        return ""
+    if not head.startswith("ref:"):
+        return "HEAD" if head else ""
+    ref = head[4:].strip()
+    if not _ref_exists(git_dir, ref):
+        return ""
+    return go_base(ref)
+
+
+def repo_details(path, remote_name):
+    """(remote_urls, branch, repo_dir) like ``GetGitRepoDetails``."""
+    root, git_dir = find_repo(path)
+    branch = head_branch(git_dir)
     urls = _read_config(git_dir).get(remote_name, [])
     return list(urls), branch, root
 
 
+def go_base(p):
+    """Go ``filepath.Base``: '' -> '.', only slashes -> '/', trailing slashes dropped."""
+    if p == "":
+        return "."
+    p = p.rstrip("/")
+    if p == "":
+        return "/"
+    return p.rsplit("/", 1)[-1]
+
+
+def go_ext(p):
+    """Go ``filepath.Ext``: the suffix from the last dot of the last element
+    (``.cfg`` for ``.cfg``; Python's splitext treats that as no extension)."""
+    i = len(p) - 1
+    while i >= 0 and p[i] != "/":
+        if p[i] == ".":
+            return p[i:]
+        i -= 1
+    return ""
+
+
+_SCHEME_RE = _lazy_re(r"^([A-Za-z][A-Za-z0-9+.\-]*):")
+_HEX = "0123456789abcdefABCDEF"
+
+
+def go_url_path(raw):
+    """``url.Parse(raw).Path`` for the subset of ``net/url`` rules that a git
+    remote can hit; raises ValueError where Go returns an error."""
+    if any(ord(c) < 0x20 or ord(c) == 0x7f for c in raw):
+        raise ValueError("net/url: invalid control character in URL")
+    rest = raw.split("#", 1)[0]
+    if rest.count("?") == 1 and rest.endswith("?"):
+        rest = rest[:-1]
+    else:
+        rest = rest.split("?", 1)[0]
+    if rest.startswith(":"):
+        raise ValueError("missing protocol scheme")
+    m = _SCHEME_RE.match(rest)
+    scheme = ""
+    if m:
+        scheme = m.group(1)
+        rest = rest[m.end():]
+    if scheme and not rest.startswith("/"):
+        return ""  # opaque URL: Path stays empty
+    if not scheme:
+        seg = rest.split("/", 1)[0]
+        if ":" in seg:
+            raise ValueError("first path segment in URL cannot contain colon")
+    if rest.startswith("//"):
+        auth, slash, rest = rest[2:].partition("/")
+        rest = slash + rest
+        host = auth.rsplit("@", 1)[-1]
+        if not host.startswith("["):
+            _h, colon, port = host.rpartition(":")
+            if colon and port and not port.isdigit():
+                raise ValueError('invalid port ":%s" after host' % port)
+    i = rest.find("%")
+    while i >= 0:
+        if i + 2 >= len(rest) or rest[i + 1] not in _HEX or rest[i + 2] not in _HEX:
+            raise ValueError("invalid URL escape %r" % rest[i:i + 3])
+        i = rest.find("%", i + 3)
+    import urllib.parse
+    return urllib.parse.unquote(rest)
+
+
 def repo_name(path):
-    """(name, root) of the repo's ``origin`` remote, or ('', '') (``GetGitRepoName``)."""
+    """(name, root) of the repo's ``origin`` remote, or ('', '') (``GetGitRepoName``,
+    ``internal/common/utils.go:682-718``)."""
     try:
         root, git_dir = find_repo(path)
     except GitError:
@@ -127,14 +226,13 @@ def repo_name(path):
             return "", ""
         u = parts[1]
     try:
-        import urllib.parse
-        parsed = urllib.parse.urlparse(u)
+        upath = go_url_path(u)
     except ValueError:
         return "", ""
-    name = os.path.basename(parsed.path.rstrip("/")) if parsed.path else "."
-    base, ext = os.path.splitext(name)
-    if ext:
-        name = base
+    name = go_base(upath)
+    ext = go_ext(name)
+    if ext and name.endswith(ext):
+        name = name[:-len(ext)]
     return name, root
 
 

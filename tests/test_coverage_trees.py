@@ -1,0 +1,170 @@
+"""Expected trees for the capability surface beyond the five BASELINE
+configurations (``benchmarks/refconfigs.py:COVERAGE_CONFIGS``):
+
+* ``profiles/<P>``: ``samples/`` in Yamls mode on each of the seven built-in
+  cluster profiles (``internal/metadata/clusters/*.yaml``);
+* ``artifacts/*``: Knative on the Kubernetes and Openshift profiles, Helm on
+  Kubernetes (``knativetransformer.go:46-101``, ``k8stransformer.go:44-293``);
+* ``carried-over/<P>``: old-version Kubernetes/OpenShift YAMLs
+  (``tests/fixtures/carried_over``) through the K8sFiles loader, the kind
+  handlers and the GroupVersion conversion of ``k8stransformer.go:106-141``;
+* ``git-repos``: source trees that are git repos with remotes
+  (``dockerfile2kube.go:146-263``, ``types/plan/plan.go:232-272``,
+  ``tektonapiresourceset.go:203-286``, ``pipeline.go:78-143``).
+
+The trees were written by ``python benchmarks/refconfigs.py --write`` and
+audited file class by file class (``tests/golden/reference/PROVENANCE.md``);
+a test run never rewrites them.
+"""
+
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+import refconfigs  # noqa: E402
+
+from move2kube_amd.utils import yamlio  # noqa: E402
+
+
+def _run(name, work):
+    run = refconfigs.Run(name, str(work)).prepare()
+    undo = run.apply_env()
+    try:
+        with run.session() as s:
+            out = run.step(s)
+    finally:
+        undo()
+    return run, out
+
+
+@pytest.mark.parametrize("name", sorted(refconfigs.COVERAGE_CONFIGS))
+def test_coverage_tree_matches_expected(name, tmp_path):
+    run, out = _run(name, tmp_path)
+    golden = refconfigs.golden_dir(name)
+    assert os.path.isdir(golden), golden
+    assert refconfigs.diff_files(out, golden, work=run.work) == []
+
+
+def _objects(name, sub="myproject"):
+    root = os.path.join(refconfigs.golden_dir(name), sub)
+    return {f: yamlio.load(open(os.path.join(root, f)).read()) for f in sorted(os.listdir(root))
+            if f.endswith(".yaml")}
+
+
+def test_every_profile_and_artifact_type_has_a_tree_or_a_reason():
+    """(artifact type x profile) combinations the curator can produce: each has
+    an expected tree here or in the BASELINE set, or a named reason in
+    DEVIATIONS.md §7."""
+    have = set(refconfigs.COVERAGE_CONFIGS) | set(refconfigs.CONFIGS)
+    for p in refconfigs.PROFILES:
+        assert "profiles/" + p in have
+    assert {"helm-openshift", "artifacts/helm-kubernetes", "artifacts/knative-kubernetes",
+            "artifacts/knative-openshift"} <= have
+    dev = open(os.path.join(refconfigs.GOLDEN_REF, "DEVIATIONS.md")).read()
+    assert "Helm or Knative on the other five profiles" in dev
+
+
+def test_no_tree_writes_an_invalid_selector():
+    """``selector: null`` would make an apps/v1 workload invalid; the reference
+    never relabels across groups, so no expected tree has one."""
+    for dp, _dn, fns in os.walk(refconfigs.GOLDEN_COVERAGE):
+        for fn in fns:
+            if fn.endswith(".yaml"):
+                assert b"selector: null" not in open(os.path.join(dp, fn), "rb").read(), os.path.join(dp, fn)
+
+
+@pytest.mark.parametrize("profile", ["AWS-EKS", "Azure-AKS", "GCP-GKE"])
+def test_generated_ingress_keeps_networking_v1_where_profile_prefers_v1beta1(profile):
+    """networking.k8s.io/v1 -> v1beta1 fails the converter's field walk
+    (``Spec.Backend`` has no source field), so the original v1 object is written."""
+    ing = _objects("profiles/" + profile)["myproject-ingress.yaml"]
+    assert ing["apiVersion"] == "networking.k8s.io/v1"
+    assert ing["spec"]["rules"][0]["http"]["paths"][0]["backend"]["service"]["name"]
+
+
+@pytest.mark.parametrize("profile", ["Kubernetes", "Openshift", "AWS-EKS", "IBM-Openshift"])
+def test_carried_over_versions(profile):
+    objs = _objects("carried-over/" + profile)
+    gv = {f: o["apiVersion"] for f, o in objs.items()}
+    # cross-group targets (extensions -> apps) are not-registered errors: original kept
+    assert gv["legacy-ext-deployment.yaml"] == "extensions/v1beta1"
+    assert "selector" not in objs["legacy-ext-deployment.yaml"]["spec"]
+    assert gv["old-agent-daemonset.yaml"] == "extensions/v1beta1"
+    assert objs["old-agent-daemonset.yaml"]["spec"]["templateGeneration"] == 3
+    # same group, every destination field present: converted, source-only fields dropped
+    assert gv["legacy-beta1-deployment.yaml"] == "apps/v1"
+    assert "rollbackTo" not in objs["legacy-beta1-deployment.yaml"]["spec"]
+    assert gv["node-agent-daemonset.yaml"] == "apps/v1"
+    assert gv["nightly-cronjob.yaml"] == "batch/v1beta1"
+    # same group, a destination field without a source: original kept
+    assert gv["db-statefulset.yaml"] == "apps/v1beta1"
+    assert gv["web-hpa-horizontalpodautoscaler.yaml"] == "autoscaling/v2beta2"
+    assert gv["old-ing-ingress.yaml"] == "extensions/v1beta1"
+    assert gv["beta-ing-ingress.yaml"] == "networking.k8s.io/v1beta1"
+    # RBAC never crosses into authorization.openshift.io (or back)
+    assert gv["reader-role.yaml"] == "rbac.authorization.k8s.io/v1"
+    assert gv["oc-reader-role.yaml"] == "authorization.openshift.io/v1"
+    openshift = profile.endswith("Openshift")
+    assert gv["reader-binding-rolebinding.yaml"] == (
+        "rbac.authorization.k8s.io/v1beta1" if openshift else "rbac.authorization.k8s.io/v1")
+    if openshift:
+        assert gv["new-ing-route.yaml"] == "route.openshift.io/v1"      # Ingress v1 -> Route
+        assert objs["web-deploymentconfig.yaml"]["kind"] == "DeploymentConfig"
+    else:
+        assert gv["new-ing-ingress.yaml"] == "networking.k8s.io/v1"
+        assert gv["web-deployment.yaml"] == "apps/v1"
+
+
+def test_git_repos_tree():
+    root = refconfigs.golden_dir("git-repos")
+    objs = _objects("git-repos")
+    # Dockerfile2Kube: one repo with two Dockerfiles -> <repo>-<bucket>; one with one -> <repo>
+    for svc in ("move2kube-demos-frontend", "move2kube-demos-backend", "internal-tools"):
+        assert "%s-deployment.yaml" % svc in objs
+    cicd = os.path.join(root, "cicd")
+    gh = yamlio.load(open(os.path.join(cicd, "myproject-git-repo-github-com-secret.yaml")).read())
+    assert gh["stringData"]["known_hosts"].startswith("github.com ssh-rsa ")
+    other = yamlio.load(open(os.path.join(cicd, "myproject-git-repo-git-corp-invalid-secret.yaml")).read())
+    assert other["metadata"]["annotations"] == {"tekton.dev/git-0": "git.corp.invalid"}
+    assert other["stringData"]["known_hosts"] == "<TODO: insert the known host keys for your git repo>"
+    pipe = yamlio.load(open(os.path.join(cicd, "myproject-clone-build-push-pipeline.yaml")).read())
+    params = {}
+    for t in pipe["spec"]["tasks"]:
+        params[t["name"]] = {p["name"]: p["value"] for p in t.get("params", [])}
+    clones = [v for k, v in sorted(params.items()) if k.startswith("clone-")]
+    builds = [v for k, v in sorted(params.items()) if k.startswith("build-push-")]
+    # the upstream remote wins over origin; the branch comes from packed-refs
+    assert {"url": "https://git.corp.invalid/tools/internal-tools.git", "revision": "develop",
+            "deleteExisting": "true"} in clones
+    assert {"url": "git@github.com:konveyor/move2kube-demos.git", "revision": "main",
+            "deleteExisting": "true"} in clones
+    dockerfiles = sorted(b["DOCKERFILE"] for b in builds)
+    assert dockerfiles == ["<TODO: insert path to the Dockerfile>", "Dockerfile",
+                           "backend/Dockerfile", "frontend/Dockerfile"]
+    cache = open(os.path.join(root, "m2kqacache.yaml")).read()
+    assert "Unable to find the public key for the domain git.corp.invalid" in cache
+    assert "$WORK/home/.ssh" in cache
+
+
+def test_plan_records_repo_info(tmp_path):
+    run = refconfigs.Run("git-repos", str(tmp_path)).prepare()
+    from move2kube_amd import api
+    undo = run.apply_env()
+    try:
+        with api.Session(qaskip=True) as s:
+            plan = s.plan(run.src, "myproject")
+    finally:
+        undo()
+    by_name = {name: svcs[0] for name, svcs in plan.services.items()}
+    fe = by_name["move2kube-demos-frontend"].repo_info
+    assert fe.git_repo_url == "git@github.com:konveyor/move2kube-demos.git"
+    assert fe.git_repo_branch == "main"
+    assert fe.git_repo_dir == os.path.join(run.src, "move2kube-demos")
+    tools = by_name["internal-tools"].repo_info
+    assert (tools.git_repo_url, tools.git_repo_branch) == ("https://git.corp.invalid/tools/internal-tools.git",
+                                                           "develop")
+    node = by_name["nodeapp"].repo_info
+    assert node.git_repo_dir == os.path.join(run.src, "move2kube-demos")

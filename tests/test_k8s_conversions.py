@@ -130,3 +130,83 @@ def test_emitted_objects_decode_back():
                     schema.check(d)
                     n += 1
     assert n > 200
+
+
+# -- GroupVersion conversion before writing (k8stransformer.go:128-141) --------
+
+def _dep(gv, selector=True):
+    d = {"apiVersion": gv, "kind": "Deployment", "metadata": {"name": "d"},
+         "spec": {"template": {"metadata": {"labels": {"app": "d"}}, "spec": {"containers": []}}}}
+    if selector:
+        d["spec"]["selector"] = {"matchLabels": {"app": "d"}}
+    return d
+
+
+@pytest.mark.parametrize("obj,target,ok", [
+    (_dep("apps/v1"), "apps/v1", True),                                  # no-op
+    (_dep("apps/v1beta1"), "apps/v1", True),                             # same group, fields present
+    (_dep("apps/v1beta2"), "apps/v1", True),
+    (_dep("apps/v1"), "apps/v1beta1", False),                            # rollbackTo has no source
+    (_dep("extensions/v1beta1", selector=False), "apps/v1", False),      # other group
+    ({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": "r"}, "rules": []},
+     "authorization.openshift.io/v1", False),
+    ({"apiVersion": "rbac.authorization.k8s.io/v1beta1", "kind": "RoleBinding", "metadata": {"name": "r"},
+      "subjects": [{"kind": "User", "name": "u"}], "roleRef": {"apiGroup": "", "kind": "Role", "name": "r"}},
+     "rbac.authorization.k8s.io/v1", True),
+    ({"apiVersion": "rbac.authorization.k8s.io/v1alpha1", "kind": "RoleBinding", "metadata": {"name": "r"},
+      "subjects": [{"kind": "User", "name": "u"}], "roleRef": {"apiGroup": "", "kind": "Role", "name": "r"}},
+     "rbac.authorization.k8s.io/v1", False),                             # Subject.apiGroup has no source
+    ({"apiVersion": "rbac.authorization.k8s.io/v1alpha1", "kind": "RoleBinding", "metadata": {"name": "r"},
+      "subjects": [], "roleRef": {"apiGroup": "", "kind": "Role", "name": "r"}},
+     "rbac.authorization.k8s.io/v1", True),                              # no element to walk
+    ({"apiVersion": "networking.k8s.io/v1", "kind": "Ingress", "metadata": {"name": "i"}, "spec": {}},
+     "networking.k8s.io/v1beta1", False),
+    ({"apiVersion": "networking.k8s.io/v1beta1", "kind": "Ingress", "metadata": {"name": "i"}, "spec": {}},
+     "networking.k8s.io/v1", False),
+    ({"apiVersion": "networking.k8s.io/v1", "kind": "Ingress", "metadata": {"name": "i"}, "spec": {}},
+     "extensions/v1beta1", False),
+])
+def test_convert_to_version_follows_scheme_rules(obj, target, ok):
+    from move2kube_amd.k8s import convert
+    if ok:
+        out = convert.convert_to_version(obj, target)
+        assert out["apiVersion"] == target and out["kind"] == obj["kind"]
+        assert obj["apiVersion"] != target or out is obj
+    else:
+        with pytest.raises(convert.ConversionError):
+            convert.convert_to_version(obj, target)
+
+
+def test_cross_group_error_text():
+    from move2kube_amd.k8s import convert
+    with pytest.raises(convert.ConversionError, match=r'^v1beta1\.Deployment is not suitable for converting '
+                                                      r'to "apps/v1" in scheme '):
+        convert.convert_to_version(_dep("extensions/v1beta1"), "apps/v1")
+
+
+def test_converted_object_marshals_as_target_version():
+    """apps/v1beta1 -> apps/v1 drops ``rollbackTo`` (no such field in the target
+    type); an unconverted extensions/v1beta1 object keeps an absent selector absent."""
+    from move2kube_amd.k8s import convert, schema
+    d = _dep("apps/v1beta1")
+    d["spec"]["rollbackTo"] = {"revision": 1}
+    out = schema.marshal(convert.convert_to_version(d, "apps/v1"))
+    assert "rollbackTo" not in out["spec"]
+    legacy = schema.marshal(_dep("extensions/v1beta1", selector=False))
+    assert "selector" not in legacy["spec"]
+    assert schema.marshal(_dep("apps/v1", selector=False))["spec"]["selector"] is None
+
+
+def test_fixed_mode_reshapes_and_fills_selector():
+    from move2kube_amd.k8s import convert
+    ing = {"apiVersion": "networking.k8s.io/v1", "kind": "Ingress", "metadata": {"name": "i"},
+           "spec": {"rules": [{"http": {"paths": [{"path": "/", "backend": {
+               "service": {"name": "s", "port": {"number": 80}}}}]}}]}}
+    beta = convert.convert_fixed(ing, "networking.k8s.io/v1beta1")
+    assert beta["spec"]["rules"][0]["http"]["paths"][0]["backend"] == {"serviceName": "s", "servicePort": 80}
+    dep = convert.convert_fixed(_dep("extensions/v1beta1", selector=False), "apps/v1")
+    assert dep["apiVersion"] == "apps/v1"
+    assert dep["spec"]["selector"] == {"matchLabels": {"app": "d"}}
+    role = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": "r"}, "rules": []}
+    with pytest.raises(convert.ConversionError):
+        convert.convert_fixed(role, "authorization.openshift.io/v1")
