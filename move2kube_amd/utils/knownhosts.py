@@ -74,18 +74,38 @@ def parse_known_hosts(path):
     return out
 
 
+# golang.org/x/crypto/ssh supportedHostKeyAlgos (plain keys): the client offers
+# these in this order and the server picks the first one it has, so this is
+# the key ``GetKey`` (knownhosts.go:137-155) ends up with.
+GO_HOST_KEY_ORDER = ("ecdsa-sha2-nistp256", "ecdsa-sha2-nistp384", "ecdsa-sha2-nistp521", "ssh-rsa", "ssh-dss",
+                     "ssh-ed25519")
+
+
+def pick_host_key_line(lines, host):
+    """From ``ssh-keyscan`` output, the line for the key a Go ssh client would
+    negotiate, as ``knownhosts.Line([host], key)`` writes it: ``host algo key``."""
+    best = None
+    for line in lines:
+        parts = line.split()
+        if len(parts) < 3 or line.startswith("#") or parts[1] not in GO_HOST_KEY_ORDER:
+            continue
+        rank = GO_HOST_KEY_ORDER.index(parts[1])
+        if best is None or rank < best[0]:
+            best = (rank, "%s %s %s" % (host, parts[1], parts[2]))
+    return best[1] if best else ""
+
+
 def get_known_hosts_line(host, timeout=5):
-    """``host algo base64key`` for the host, or '' when it cannot be fetched."""
+    """``host algo base64key`` for the host, or '' when it cannot be fetched.
+    Every key type the server offers is scanned and the one a Go client would
+    negotiate is kept (:data:`GO_HOST_KEY_ORDER`)."""
     if os.environ.get("M2K_NO_NETWORK") or shutil.which("ssh-keyscan") is None:
         log.debug("Cannot fetch the ssh host key of %s (no ssh-keyscan or network disabled)", host)
         return ""
     try:
-        p = subprocess.run(["ssh-keyscan", "-T", str(timeout), "-t", "rsa", host], stdout=subprocess.PIPE,
-                           stderr=subprocess.DEVNULL, timeout=timeout + 2)
-    except (OSError, subprocess.TimeoutExpired):
+        p = subprocess.run(["ssh-keyscan", "-T", str(timeout), "-t", "rsa,ecdsa,ed25519,dsa", host],
+                           stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, stdin=subprocess.DEVNULL,
+                           timeout=timeout + 2)
+    except (OSError, subprocess.SubprocessError):
         return ""
-    for line in p.stdout.decode("utf-8", "replace").splitlines():
-        line = line.strip()
-        if line and not line.startswith("#"):
-            return line
-    return ""
+    return pick_host_key_line(p.stdout.decode("utf-8", "replace").splitlines(), host)

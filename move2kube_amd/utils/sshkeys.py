@@ -90,21 +90,102 @@ def _load_ssh_keys_of_current_user():
     _state["keys"] = names
 
 
-def _to_pem(path, passphrase=""):
-    """Re-encode a private key file as PEM (PKCS#1 RSA / SEC1 EC) via ssh-keygen."""
-    if shutil.which("ssh-keygen") is None:
-        with open(path) as f:
-            return f.read()
-    with tempfile.TemporaryDirectory() as td:
+class KeyError_(ValueError):
+    pass
+
+
+_PEM_TYPES = ("-----BEGIN RSA PRIVATE KEY-----", "-----BEGIN EC PRIVATE KEY-----")
+
+# SSH_ASKPASS helper: prints what the parent writes into the FIFO named by
+# M2K_ASKPASS_FIFO.  Neither the passphrase nor anything derived from it is
+# on a command line or in an environment variable.
+_ASKPASS = '#!/bin/sh\nexec cat "$M2K_ASKPASS_FIFO"\n'
+
+
+def _feed_fifo(fifo, secret, done):
+    import threading
+
+    def run():
+        try:
+            with open(fifo, "w") as f:   # blocks until ssh-keygen's askpass opens it
+                f.write(secret + "\n")
+        except OSError:
+            pass
+        done.set()
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    return t
+
+
+def _to_pem(path, passphrase=None):
+    """Re-encode a private key file as PEM, like ``marshalRSAIntoPEM`` /
+    ``marshalECDSAIntoPEM`` (``sshkeys.go:170-232``): PKCS#1 RSA or SEC1 EC.
+    Other key types (ed25519, DSA) are an error, as in the reference.
+
+    ``ssh-keygen -p -m PEM -N ''`` does the re-encoding on a private copy.  The
+    old passphrase of an encrypted key reaches it through ``SSH_ASKPASS``
+    (``SSH_ASKPASS_REQUIRE=force``) and a FIFO in a private directory, never
+    through argv or the environment.  Without ``ssh-keygen`` this raises; the
+    caller warns and the secret keeps its placeholder."""
+    import threading
+    exe = shutil.which("ssh-keygen")
+    if exe is None:
+        raise KeyError_("ssh-keygen is not available to re-encode the private key as PEM")
+    with tempfile.TemporaryDirectory(prefix="m2k-key-") as td:
+        os.chmod(td, 0o700)
         tmp = os.path.join(td, "key")
         shutil.copyfile(path, tmp)
         os.chmod(tmp, 0o600)
-        p = subprocess.run(["ssh-keygen", "-p", "-m", "PEM", "-P", passphrase, "-N", "", "-f", tmp],
-                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, stdin=subprocess.DEVNULL, timeout=30)
+        env = {k: v for k, v in os.environ.items() if not k.startswith("SSH_")}
+        done = threading.Event()
+        feeder = None
+        argv = [exe, "-p", "-m", "PEM", "-N", "", "-f", tmp]
+        if passphrase is None:
+            argv[2:2] = ["-P", ""]       # not encrypted: an empty old passphrase is no secret
+        else:
+            helper = os.path.join(td, "askpass")
+            with open(helper, "w") as f:
+                f.write(_ASKPASS)
+            os.chmod(helper, 0o700)
+            fifo = os.path.join(td, "pass")
+            os.mkfifo(fifo, 0o600)
+            env.update({"SSH_ASKPASS": helper, "SSH_ASKPASS_REQUIRE": "force", "DISPLAY": ":0",
+                        "M2K_ASKPASS_FIFO": fifo})
+            feeder = _feed_fifo(fifo, passphrase, done)
+        try:
+            p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, stdin=subprocess.DEVNULL,
+                               env=env, timeout=30, start_new_session=True)
+        finally:
+            if feeder is not None and not done.is_set():
+                # askpass never ran: open the reading end so the writer returns
+                try:
+                    fd = os.open(fifo, os.O_RDONLY | os.O_NONBLOCK)
+                    feeder.join(1)
+                    os.close(fd)
+                except OSError:
+                    pass
         if p.returncode != 0:
-            raise ValueError(p.stderr.decode("utf-8", "replace").strip() or "ssh-keygen failed")
+            raise KeyError_(p.stderr.decode("utf-8", "replace").strip() or "ssh-keygen failed")
         with open(tmp) as f:
-            return f.read()
+            pem = f.read()
+        first = pem.lstrip().split("\n", 1)[0].strip()
+        if first not in _PEM_TYPES:
+            raise KeyError_("Unknown key type [%s]" % _go_key_type(exe, tmp, env))
+    return pem
+
+
+_GO_KEY_TYPES = {"ED25519": "*ed25519.PrivateKey", "DSA": "*dsa.PrivateKey"}
+
+
+def _go_key_type(exe, path, env):
+    """The Go type ``ssh.ParseRawPrivateKey`` would return (for the error text)."""
+    try:
+        p = subprocess.run([exe, "-l", "-f", path], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                           stdin=subprocess.DEVNULL, env=env, timeout=30)
+        kind = p.stdout.decode("ascii", "replace").strip().rsplit("(", 1)[-1].rstrip(")")
+    except (OSError, subprocess.SubprocessError):
+        kind = ""
+    return _GO_KEY_TYPES.get(kind, "*%s.PrivateKey" % (kind.lower() or "unknown"))
 
 
 def _is_encrypted(path):
@@ -126,7 +207,7 @@ def load_ssh_key(filename):
     from ..models import qa
     from ..qaengine import fetch_answer
     path = os.path.join(_state["key_dir"], filename)
-    passphrase = ""
+    passphrase = None
     if _is_encrypted(path):
         prob = qa.new_password_problem("Enter the password to decrypt the private key %r : " % filename, ["Password:"])
         passphrase = fetch_answer(prob).get_string_answer()
@@ -150,5 +231,9 @@ def get_ssh_key(domain):
     try:
         return load_ssh_key(name), True
     except (OSError, ValueError, subprocess.SubprocessError) as e:
-        log.warning("Failed to load the key %r Error %r", name, str(e))
+        log.warning("Failed to load the key %s Error %s", _q(name), _q(str(e)))
         return "", False
+
+
+def _q(s):
+    return log.go_quote(s)
