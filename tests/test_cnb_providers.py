@@ -219,3 +219,160 @@ def test_docker_api_batched_probes_match_sequential(fake_dockerd, tmp_path):
     p = providers.DockerAPIProvider()
     assert p.is_builder_supported_batch(pairs) == [p.is_builder_supported(d, b) for d, b in pairs]
     assert p.is_builder_supported_batch(pairs) == [i // 2 % 2 == 0 for i in range(len(pairs))]
+
+
+# -- runc + skopeo + umoci (runcprovider.go:45-208) ------------------------------
+
+RUNC_STUBS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "stubbin_runc")
+
+
+@pytest.fixture
+def runc_env(monkeypatch, tmp_path):
+    log = tmp_path / "stub.log"
+    log.write_text("")
+    monkeypatch.setenv("M2K_STUB_LOG", str(log))
+    monkeypatch.setenv("PATH", RUNC_STUBS + os.pathsep + "/usr/bin:/bin")
+    base = tmp_path / "cnb"
+    monkeypatch.setattr(providers.RuncProvider, "_paths",
+                        staticmethod(lambda: (str(base / "images"), str(base / "bundles"))))
+    return log, base
+
+
+def test_runc_provider_rewrites_bundle_and_parses_detection(runc_env, tmp_path):
+    log, base = runc_env
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "package.json").write_text("{}")
+    other = tmp_path / "other"
+    other.mkdir()
+    p = providers.RuncProvider()
+    assert p.is_available()
+    builder = "gcr.io/buildpacks/builder:v1"    # GetImageNameAndTag: image "builder", tag "v1"
+    assert p.is_builder_supported(str(app), builder) is True
+    assert p.is_builder_supported(str(other), builder) is False   # "No buildpack groups passed detection."
+    cfg = json.loads((base / "bundles" / "builder" / "config.json").read_text())
+    ws = [m for m in cfg["mounts"] if m["destination"] == "/workspace"]
+    assert ws == [{"destination": "/workspace", "type": "bind", "source": str(other), "options": ["rbind", "ro"]}]
+    assert [m["destination"] for m in cfg["mounts"]] == ["/proc", "/workspace"]   # replaced in place
+    assert cfg["process"]["args"] == ["/cnb/lifecycle/detector"] and cfg["process"]["terminal"] is False
+    calls = log.read_text().splitlines()
+    copies = [c for c in calls if c.startswith("skopeo copy")]
+    assert copies == ["skopeo copy docker://%s oci:builder:v1 @%s" % (builder, base / "images")]
+    unpacks = [c for c in calls if c.startswith("umoci")]
+    assert unpacks == ["umoci unpack --image builder:v1 %s @%s"
+                       % (base / "bundles" / "builder", base / "images")]
+    runs = [c for c in calls if c.startswith("runc")]
+    assert runs == ["runc run cnbbuilder @%s" % (base / "bundles" / "builder")] * 2
+
+
+def test_runc_provider_appends_workspace_mount_when_missing(runc_env, tmp_path):
+    _log, base = runc_env
+    p = providers.RuncProvider()
+    p._init(["b:latest"])
+    cfgp = base / "bundles" / "b" / "config.json"
+    cfg = json.loads(cfgp.read_text())
+    cfg["mounts"] = [m for m in cfg["mounts"] if m["destination"] != "/workspace"]
+    cfgp.write_text(json.dumps(cfg))
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "package.json").write_text("{}")
+    assert p.is_builder_supported(str(app), "b:latest") is True
+    cfg = json.loads(cfgp.read_text())
+    assert cfg["mounts"][-1] == {"destination": "/workspace", "type": "bind", "source": str(app),
+                                 "options": ["rbind", "ro"]}
+
+
+def test_runc_provider_errors_send_the_probe_on(runc_env, tmp_path):
+    p = providers.RuncProvider()
+    crash = tmp_path / "crash-app"
+    crash.mkdir()
+    (crash / "crash").write_text("")
+    with pytest.raises(providers.ProviderError):       # runc exits non-zero: error, not "unsupported"
+        p.is_builder_supported(str(crash), "b:latest")
+    with pytest.raises(providers.ProviderError, match="Runc Builder image not available"):
+        p.is_builder_supported(str(tmp_path), "missing/image:1")   # skopeo copy failed: no bundle
+
+
+def test_runc_provider_buildpacks_from_skopeo_label(runc_env):
+    p = providers.RuncProvider()
+    assert p.get_all_buildpacks(["b:latest", "missing/image:1"]) == {
+        "b:latest": ["paketo-buildpacks/nodejs", "paketo-buildpacks/go"]}
+
+
+def test_runc_provider_unavailable_without_all_three_tools(monkeypatch, tmp_path):
+    only = tmp_path / "bin"
+    only.mkdir()
+    os.symlink(os.path.join(RUNC_STUBS, "runc"), only / "runc")
+    monkeypatch.setenv("PATH", str(only))
+    p = providers.RuncProvider()
+    assert not p.is_available()
+    with pytest.raises(providers.ProviderError):
+        p.get_all_buildpacks(["b"])
+
+
+# -- docker API: create without the bind mount, then copy a tar in ------------------
+# (dockerapiprovider.go:176-194, 232-340)
+
+class _NoBindDockerd(_FakeDockerd):
+    """Refuses bind mounts (a remote daemon, or a rootless one without access to
+    the path); the source must arrive through PUT /containers/<id>/archive."""
+    archives = {}
+
+    def do_POST(self):  # noqa: N802
+        if self.path == "/containers/create":
+            n = int(self.headers.get("Content-Length") or 0)
+            cfg = json.loads(self.rfile.read(n) or b"{}")
+            if (cfg.get("HostConfig") or {}).get("Mounts"):
+                return self._json(500, {"message": "invalid mount config: bind source path does not exist"})
+            with _FAKE_LOCK:
+                cid = "n%d" % next(_FAKE_IDS)
+            self.state[cid] = 0 if cfg.get("Image") == "hello-world" else None
+            return self._json(201, {"Id": cid})
+        if "/wait" in self.path:
+            cid = self.path.split("/")[2]
+            code = self.state.get(cid)
+            if code is None:
+                names = self.archives.get(cid, [])
+                code = 0 if "workspace/package.json" in names else 1
+            return self._json(200, {"StatusCode": code})
+        return super().do_POST()
+
+    def do_PUT(self):  # noqa: N802
+        import io
+        import tarfile
+        cid = self.path.split("/")[2]
+        assert self.path.endswith("/archive?path=/"), self.path
+        assert self.headers.get("Content-Type") == "application/x-tar"
+        data = self.rfile.read(int(self.headers.get("Content-Length") or 0))
+        with tarfile.open(fileobj=io.BytesIO(data)) as tf:
+            self.archives[cid] = [m.name.lstrip("/") for m in tf.getmembers()]
+        return self._json(200, {})
+
+
+@pytest.fixture
+def nobind_dockerd(tmp_path, monkeypatch):
+    sock = str(tmp_path / "docker.sock")
+    srv = _UnixServer(sock, _NoBindDockerd)
+    t = threading.Thread(target=srv.serve_forever, daemon=True)
+    t.start()
+    monkeypatch.setenv("DOCKER_HOST", "unix://" + sock)
+    yield _NoBindDockerd.archives
+    srv.shutdown()
+    srv.server_close()
+
+
+def test_docker_api_copies_source_as_tar_when_bind_mount_fails(nobind_dockerd, tmp_path):
+    app = tmp_path / "app"
+    (app / "src" / "lib").mkdir(parents=True)
+    (app / "package.json").write_text("{}")
+    (app / "src" / "lib" / "index.js").write_text("x")
+    os.symlink("src/lib/index.js", app / "main.js")
+    other = tmp_path / "other"
+    other.mkdir()
+    (other / "README").write_text("")
+    p = providers.DockerAPIProvider()
+    assert p.is_builder_supported(str(app), "gcr.io/buildpacks/builder") is True
+    assert p.is_builder_supported(str(other), "gcr.io/buildpacks/builder") is False
+    copied = [names for names in nobind_dockerd.values() if "workspace/package.json" in names]
+    assert copied and set(copied[0]) == {"workspace/package.json", "workspace/src", "workspace/src/lib",
+                                         "workspace/src/lib/index.js", "workspace/main.js"}
