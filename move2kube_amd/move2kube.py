@@ -188,6 +188,33 @@ def _to_ir(p):
     return ir
 
 
+def _remove_stale_trash(parent, base):
+    """Delete ``.<base>.m2k-old-<pid>-<tid>`` trees left by a run that was
+    killed before its background delete finished (the next plan would walk
+    them as part of the source tree).  A tree whose pid is still alive belongs
+    to a concurrent run and is left alone."""
+    prefix = ".%s.m2k-old-" % base
+    try:
+        names = [n for n in os.listdir(parent) if n.startswith(prefix)]
+    except OSError:
+        return
+    for n in names:
+        pid = n[len(prefix):].split("-", 1)[0]
+        if not pid.isdigit():
+            continue
+        try:
+            os.kill(int(pid), 0)
+            continue                     # alive (or not ours to signal): keep
+        except ProcessLookupError:
+            pass
+        except (PermissionError, OverflowError, ValueError):
+            continue
+        try:
+            native.remove_tree(os.path.join(parent, n))
+        except OSError as e:
+            log.debug("Unable to remove the stale output %s : %s", n, e)
+
+
 def _remove_output(outpath):
     """``os.RemoveAll(out)`` (translator.go:64).  The old tree is renamed out of
     the way (one syscall) and deleted on a thread - the native delete releases
@@ -196,6 +223,7 @@ def _remove_output(outpath):
     delete when the rename is not possible."""
     import threading
     parent, base = os.path.split(os.path.abspath(outpath))
+    _remove_stale_trash(parent, base)
     trash = os.path.join(parent, ".%s.m2k-old-%d-%d" % (base, os.getpid(), threading.get_ident()))
     try:
         if os.path.lexists(trash):

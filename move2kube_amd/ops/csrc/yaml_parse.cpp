@@ -34,6 +34,14 @@ namespace m2kyamlp {
 
 struct Unsupported {};
 struct PyErrorSet {};
+// Nesting past go-yaml's limit (yaml.v3 scannerc.go max_flow_level /
+// max_indents = 10000): a parse error of this document, never handed to
+// PyYAML, whose C composer recurses once per level and overflows the stack.
+struct TooDeep {};
+constexpr int kMaxDepth = 10000;
+// libyaml / go-yaml refuse a simple (implicit) key longer than 1024 characters;
+// bytes >= characters, so a longer byte span is left to PyYAML to judge.
+constexpr int kMaxSimpleKey = 1024;
 
 enum Mode { TYPED = 0, V2 = 1, RAW = 2 };
 
@@ -78,6 +86,19 @@ struct Line {
 static inline bool is_flow_ind(char c) { return c == ',' || c == '[' || c == ']' || c == '{' || c == '}'; }
 
 class Parser {
+  // one level of node_at / flow recursion
+  struct DepthGuard {
+    int& d;
+    explicit DepthGuard(int& depth) : d(depth) {
+      if (++d > kMaxDepth) {
+        --d;
+        throw TooDeep();
+      }
+    }
+    ~DepthGuard() { --d; }
+  };
+  int depth_ = 0;
+
  public:
   Parser(const char* s, size_t n, int mode, PyObject* resolve_number)
       : mode_(mode), resolve_number_(resolve_number) {
@@ -377,6 +398,7 @@ class Parser {
       int p = end;
       while (p < ln.len && ln.s[p] == ' ') p++;
       if (p < ln.len && ln.s[p] == ':' && (p + 1 == ln.len || ln.s[p + 1] == ' ')) {
+        if (p - pos > kMaxSimpleKey) throw Unsupported();
         kend = end;
         colon = p;
         quoted_key = true;
@@ -391,6 +413,7 @@ class Parser {
         int e = p;
         while (e > pos && ln.s[e - 1] == ' ') e--;
         if (e == pos) throw Unsupported();  // empty key
+        if (p - pos > kMaxSimpleKey) throw Unsupported();
         kend = e;
         colon = p;
         quoted_key = false;
@@ -404,6 +427,7 @@ class Parser {
   // enclosing block collection (-1 at the root); `block_ok` is false for a
   // value on its key's line ("key: value"), where block collections cannot start.
   PyObject* node_at(int col, int parent, bool block_ok) {
+    DepthGuard guard(depth_);
     const Line& ln = L_[li_];
     const char c = ln.s[col];
     if (is_seq_entry(ln, col)) {
@@ -610,6 +634,7 @@ class Parser {
 
   // ---- flow collections (one line) ------------------------------------------
   PyObject* flow(const Line& ln, int pos, int& end) {
+    DepthGuard guard(depth_);
     const bool is_seq = ln.s[pos] == '[';
     const char close = is_seq ? ']' : '}';
     Ref coll(is_seq ? PyList_New(0) : PyDict_New());
@@ -624,7 +649,9 @@ class Parser {
       if (p >= ln.len) throw Unsupported();  // multi-line flow
       Ref key;
       if (!is_seq) {
+        const int kstart = p;
         key = Ref(flow_scalar(ln, p, p, true));
+        if (p - kstart > kMaxSimpleKey) throw Unsupported();
         if (PyObject_Hash(key.get()) == -1) throw PyErrorSet();
         while (p < ln.len && ln.s[p] == ' ') p++;
         if (!(p < ln.len && ln.s[p] == ':' && p + 1 < ln.len && ln.s[p + 1] == ' ')) throw Unsupported();
@@ -726,6 +753,9 @@ extern "C" PyObject* m2k_yaml_load(PyObject* text, int mode, int multi, PyObject
   } catch (const m2kyamlp::Unsupported&) {
     Py_INCREF(unsupported);
     return unsupported;
+  } catch (const m2kyamlp::TooDeep&) {
+    PyErr_Format(PyExc_ValueError, "yaml: exceeded max depth of %d", m2kyamlp::kMaxDepth);
+    return nullptr;
   } catch (const m2kyamlp::PyErrorSet&) {
     return nullptr;
   } catch (const std::bad_alloc&) {

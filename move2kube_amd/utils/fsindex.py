@@ -74,9 +74,24 @@ def handoff_allowed(src_root, out_path):
     when nothing the command writes in between lands inside the source tree:
     the output directory (created with its QA cache before translating) must
     lie outside it."""
-    src = os.path.abspath(src_root)
-    out = os.path.abspath(out_path)
+    src = os.path.realpath(src_root)
+    out = _realpath_of_nearest(out_path)
     return not (out == src or out.startswith(src.rstrip(os.sep) + os.sep))
+
+
+def _realpath_of_nearest(path):
+    """``realpath`` of ``path``, resolved through its nearest existing ancestor
+    when it does not exist yet (an output directory reached through a symlink
+    into the source tree must compare as inside it)."""
+    p = os.path.abspath(path)
+    tail = []
+    while not os.path.lexists(p):
+        parent, name = os.path.split(p)
+        if parent == p:
+            break
+        tail.append(name)
+        p = parent
+    return os.path.join(os.path.realpath(p), *reversed(tail))
 
 
 def invalidate():

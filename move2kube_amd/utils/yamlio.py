@@ -877,6 +877,66 @@ def _native_loader():
     return _native_load
 
 
+MAX_DEPTH = 10000  # go-yaml v2/v3: max_flow_level and max_indents
+
+
+def _too_deep(text, limit=MAX_DEPTH):
+    """Cheap upper-bound check of the nesting a parser would have to recurse
+    through: flow brackets (outside quotes) plus block levels (indentation
+    steps and compact ``- `` entries).  PyYAML's C composer recurses once per
+    level and overflows the C stack on deep documents (``'[' * 200000``), so
+    such a document is refused before it reaches PyYAML, with go-yaml's error.
+    The count only ever over-estimates the real depth by the quoted-bracket
+    approximation, and only documents of more than ``limit`` bytes are scanned."""
+    if len(text) <= limit:
+        return False
+    if text.count("[") + text.count("{") > limit:
+        flow = 0
+        quote = ""
+        prev = "\n"
+        escaped = False
+        for ch in text:
+            if quote:
+                if quote == "#":
+                    if ch == "\n":
+                        quote = ""
+                elif escaped:
+                    escaped = False
+                elif ch == "\\" and quote == '"':
+                    escaped = True
+                elif ch == quote:
+                    quote = ""
+                prev = ch
+                continue
+            if ch in "[{":
+                flow += 1
+                if flow > limit:
+                    return True
+            elif ch in "]}":
+                flow -= 1 if flow else 0
+            elif ch in "\"'" and prev in " \t\n:[{,-?":
+                quote = ch          # a quoted scalar starts only where a node can start
+            elif ch == "#" and prev in " \t\n":
+                quote = "#"
+            prev = ch
+    stack = []
+    for line in text.split("\n"):
+        body = line.lstrip(" ")
+        if not body or body[0] == "#":
+            continue
+        col = len(line) - len(body)
+        while stack and stack[-1] >= col:
+            stack.pop()
+        stack.append(col)
+        while body.startswith("- ") or body == "-":
+            col += 2
+            body = body[2:].lstrip(" ")
+            stack.append(col)
+        if len(stack) > limit:
+            return True
+    return False
+
+
 def _parse(text, mode, multi):
     nl = _native_loader()
     if nl and isinstance(text, str):
@@ -884,8 +944,12 @@ def _parse(text, mode, multi):
             r = nl(text, mode, multi, go_resolve_number, _UNSUPPORTED)
         except UnicodeError:
             r = _UNSUPPORTED
+        except ValueError as e:   # nesting past go-yaml's limit (yaml_parse.cpp TooDeep)
+            raise _lz().yaml.YAMLError(str(e)) from None
         if r is not _UNSUPPORTED:
             return r
+    if isinstance(text, str) and _too_deep(text):
+        raise _lz().yaml.YAMLError("yaml: exceeded max depth of %d" % MAX_DEPTH)
     lz = _lz()
     loader = (lz.typed, lz.v2, lz.raw)[mode]
     try:

@@ -132,6 +132,9 @@ EDGE_CASES = [
     "a: #c\n  b: 1\n", "a: # c\n- x\n", "#c\na: 1 # c\n# c\n", "a:\n  # c\n  b: 1\n",
     "image: nginx:1.19\nports:\n  - \"80:80\"\n  - 443:443\n", "command: [\"sh\", \"-c\", \"echo $$HOME\"]\n",
     "x: <<\n", "- <<\n", "a: <none>\n", "a: =\n", "a: ---\n", "a: ...\n", "---a\n", "--- \n", "----\n",
+    # implicit keys: libyaml and go-yaml refuse more than 1024 characters
+    "k" * 1024 + ": v\n", "k" * 1025 + ": v\n", "k" * 1100 + ": v\n", "'" + "k" * 1100 + "': v\n",
+    "a: {" + "k" * 1100 + ": v}\n", "- " + "k" * 1100 + ": v\n", "\u00e9" * 600 + ": v\n",
 ]
 
 
@@ -197,3 +200,25 @@ def test_generated_pyyaml_styles(data, flow, indent, explicit):
         return
     check(text)
     check(text + "---\n" + text)
+
+
+def test_nesting_past_go_yaml_limit_is_a_parse_error():
+    """go-yaml refuses nesting past 10000 levels ("exceeded max depth"); the
+    native parser raises that as YAMLError instead of recursing on, and the
+    document is never handed to PyYAML, whose C composer overflows the stack."""
+    import subprocess
+    import sys
+    code = ("from move2kube_amd.utils import yamlio\n"
+            "import sys\n"
+            "for t in [sys.argv[1] * 200000, '- ' * 200000 + 'x', 'a: x\\'\\n' + '[' * 200000]:\n"
+            "    try:\n"
+            "        yamlio.load(t)\n"
+            "        print('accepted')\n"
+            "    except yamlio.YAMLError as e:\n"
+            "        print(str(e).splitlines()[0])\n")
+    for native in ("1", "0"):
+        p = subprocess.run([sys.executable, "-c", code, "["], cwd=ROOT, capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, M2K_NATIVE_YAML=native))
+        assert p.returncode == 0, p.stderr[-2000:]
+        assert p.stdout.splitlines() == ["yaml: exceeded max depth of 10000"] * 3, (native, p.stdout)
+    assert yamlio.load("a: " + "[" * 9000 + "]" * 9000) is not None
