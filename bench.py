@@ -74,6 +74,26 @@ def per_config_checks(runs):
     return out
 
 
+def large_tree_check(sizes):
+    """Untimed: per-service ``translate`` cost on synthetic trees of growing
+    size (the scaling axis of this workload); a ratio near 1 means linear."""
+    saved = {k: os.environ.get(k) for k in ("M2K_NO_NETWORK", "M2K_DISABLE_CNB")}
+    os.environ.update({"M2K_NO_NETWORK": "1", "M2K_DISABLE_CNB": "1"})
+    try:
+        import translate_large_tree
+        rows = translate_large_tree.measure(sizes)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    per = {str(r["apps"]): r["ms_per_service"] for r in rows}
+    return {"large_tree_translate_ms_per_service": per,
+            "services": {str(r["apps"]): r["services"] for r in rows},
+            "ratio_largest_vs_smallest": round(rows[-1]["ms_per_service"] / rows[0]["ms_per_service"], 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -83,6 +103,9 @@ def main():
                     choices=sorted(refconfigs.CONFIGS) + sorted(refconfigs.EXTRA_CONFIGS))
     ap.add_argument("--check-runs", type=int, default=3,
                     help="warm/cold runs per configuration in the untimed per-config check (0 = skip)")
+    ap.add_argument("--large-tree", default="100,2000",
+                    help="untimed: translate synthetic trees of these app counts and report ms per service "
+                         "(benchmarks/translate_large_tree.py); empty = skip")
     ap.add_argument("--keep", action="store_true", help="keep the work directory")
     ap.add_argument("--workdir", default="auto",
                     help="root for the input copies and output trees: auto (tmpfs if available), disk, or a path")
@@ -150,6 +173,9 @@ def main():
     per_config = None
     if rank == 0 and args.check_runs > 0:
         per_config = per_config_checks(args.check_runs)
+    if rank == 0 and args.large_tree:
+        per_config = dict(per_config or {})
+        per_config["large-tree"] = large_tree_check([int(x) for x in args.large_tree.split(",")])
 
     if dist is not None:
         dev = torch.device("cuda", torch.cuda.current_device()) if have_cuda else torch.device("cpu")
@@ -161,7 +187,7 @@ def main():
     if rank == 0:
         total_diff = diff_headline
         if per_config is not None and total_diff is not None:
-            total_diff = sum(v["manifest_diff_vs_ref"] for v in per_config.values())
+            total_diff = sum(v["manifest_diff_vs_ref"] for v in per_config.values() if "manifest_diff_vs_ref" in v)
         print(json.dumps({
             "metric": "translate_throughput (BASELINE fallback: translate wall-clock + manifest diff vs ref on samples/)",
             "value": round(value, 3),

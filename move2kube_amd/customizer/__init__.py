@@ -39,9 +39,10 @@ class RegistryCustomizer:
         for c in ir.containers:
             if c.new:
                 newimages.extend(c.image_names)
+        new_folded = {x.casefold() for x in newimages}   # is_string_present, once per image
         for s in ir.sorted_services():
             for c in s.containers:
-                if not common.is_string_present(newimages, c.get("image", "")):
+                if c.get("image", "").casefold() not in new_folded:
                     parts = c.get("image", "").split("/")
                     if len(parts) == 3:
                         reg_list.append(parts[0])
@@ -147,7 +148,7 @@ class RegistryCustomizer:
         for s in ir.sorted_services():
             for c in s.containers:
                 image = c.get("image", "")
-                if common.is_string_present(newimages, image):
+                if image.casefold() in new_folded:
                     parts = image.split("/")
                     name, tag = common.get_image_name_and_tag(parts[-1])
                     if ir.kubernetes.registry_url and ir.kubernetes.registry_namespace:

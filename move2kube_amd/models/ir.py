@@ -334,17 +334,66 @@ class IR:
     def is_ingress_tls_enabled(self):
         return self.ingress_tls_secret_name != ""
 
+    # The reference offers every new container (storage) to each existing one
+    # in turn (ir.go:369-380, 387-395), which is quadratic in the number of
+    # services.  The first existing container that ``merge`` accepts is the
+    # first one of the same build type sharing an image name (case-folded), so
+    # an index from (build type, folded name) to list positions finds it
+    # directly; storages merge on equal names.  The indexes are rebuilt when
+    # the list object is replaced or its length changes behind their back.
+
+    def _container_index(self):
+        idx = self.__dict__.get("_cidx")
+        if idx is None or idx[0] is not self.containers or idx[1] != len(self.containers):
+            buckets = {}
+            for pos, c in enumerate(self.containers):
+                bt = c.container_build_type
+                for n in c.image_names:
+                    b = buckets.setdefault((bt, n.casefold()), [])
+                    if not b or b[-1] != pos:
+                        b.append(pos)
+            idx = self._cidx = [self.containers, len(self.containers), buckets]
+        return idx
+
     def add_container(self, container):
-        for c in self.containers:
+        idx = self._container_index()
+        buckets = idx[2]
+        bt = container.container_build_type
+        best = -1
+        for n in container.image_names:
+            b = buckets.get((bt, n.casefold()))
+            if b and (best < 0 or b[0] < best):
+                best = b[0]
+        if best >= 0:
+            c = self.containers[best]
             if c.merge(container):
+                for n in c.image_names:
+                    b = buckets.setdefault((bt, n.casefold()), [])
+                    if best not in b:
+                        b.append(best)
+                        b.sort()
                 return
+        pos = len(self.containers)
         self.containers.append(container)
+        for n in container.image_names:
+            b = buckets.setdefault((bt, n.casefold()), [])
+            if not b or b[-1] != pos:
+                b.append(pos)
+        idx[1] = len(self.containers)
 
     def add_storage(self, st):
-        for s in self.storages:
-            if s.merge(st):
-                return
+        idx = self.__dict__.get("_sidx")
+        if idx is None or idx[0] is not self.storages or idx[1] != len(self.storages):
+            first = {}
+            for pos, s in enumerate(self.storages):
+                first.setdefault(s.name, pos)
+            idx = self._sidx = [self.storages, len(self.storages), first]
+        pos = idx[2].get(st.name)
+        if pos is not None and self.storages[pos].merge(st):
+            return
+        idx[2].setdefault(st.name, len(self.storages))
         self.storages.append(st)
+        idx[1] = len(self.storages)
 
     def get_container(self, imagename):
         for c in self.containers:

@@ -71,8 +71,9 @@ class Problem:
         if self.type in (SELECT, MULTISELECT):
             ok = True
             self.answer = []
+            folded = {o.casefold() for o in self.options} if len(answer) > 1 else None
             for a in answer:
-                if not common.is_string_present(self.options, a):
+                if (a.casefold() not in folded) if folded is not None else not common.is_string_present(self.options, a):
                     log.warning("No matching value in options for %s. Ignoring.", a)
                     ok = False
                     continue
@@ -283,8 +284,9 @@ def _new_problem(t, desc, context, default, opts):
     if t == MULTISELECT:
         if len(opts) == 0:
             resolved = True
+        folded = {o.casefold() for o in opts}   # common.is_string_present for every default at once
         for d in default:
-            if not common.is_string_present(opts, d):
+            if d.casefold() not in folded:
                 raise ProblemError("Default value [%s] not present in options [%s]" % (d, opts))
     elif t == SELECT:
         if len(opts) == 0:
@@ -352,6 +354,94 @@ def new_multiline_input_problem(desc, context, default):
 
 def new_password_problem(desc, context):
     return _new_problem(PASSWORD, desc, context, [], [])
+
+
+class _DescIndex:
+    """Which problems of a list may ``match`` a new one (``_match_string``:
+    case-folded equality, or the listed description as a regex found in the
+    new description).  The reference scans the whole list for every lookup
+    (``types/qaengine/cache.go:84-111``), which makes a QA session over n
+    services quadratic; this index bounds a lookup by the new description's
+    length.
+
+    A listed description is filed under its case-folded text and under one
+    ``Q``-character piece of its required literals (:func:`required_literals`),
+    the piece whose bucket is smallest when it is filed.  Any string the regex
+    matches contains every required literal, hence that piece, so a lookup
+    only visits the buckets of the pieces of the new description, plus the
+    descriptions without a literal of ``Q`` characters.  Candidates are then
+    checked with the full ``matches``, in list order."""
+
+    Q = 6
+
+    def __init__(self, problems):
+        self.problems = problems
+        self.size = 0
+        self.fold = {}
+        self.grams = {}
+        self.always = set()
+        self.where = {}
+        for i, p in enumerate(problems):
+            self.add(i, p.desc)
+
+    def fresh(self, problems):
+        return problems is self.problems and len(problems) == self.size
+
+    def add(self, pos, desc):
+        fold = desc.casefold()
+        self.fold.setdefault(fold, set()).add(pos)
+        lits = _matcher(desc)[1]
+        gram = None
+        if lits:
+            best = None
+            q = self.Q
+            for lit in lits:
+                for j in range(len(lit) - q, -1, -1):
+                    g = lit[j:j + q]
+                    n = len(self.grams.get(g, ()))
+                    if best is None or n < best[0]:
+                        best = (n, g)
+                        if n == 0:
+                            break
+                if best is not None and best[0] == 0:
+                    break
+            if best is not None:
+                gram = best[1]
+        if gram is None:
+            self.always.add(pos)
+        else:
+            self.grams.setdefault(gram, set()).add(pos)
+        self.where[pos] = (fold, gram)
+        if pos >= self.size:
+            self.size = pos + 1
+
+    def remove(self, pos):
+        fold, gram = self.where.pop(pos)
+        self.fold[fold].discard(pos)
+        if gram is None:
+            self.always.discard(pos)
+        else:
+            self.grams[gram].discard(pos)
+
+    def candidates(self, desc):
+        out = set(self.fold.get(desc.casefold(), ()))
+        out |= self.always
+        grams, q = self.grams, self.Q
+        for i in range(len(desc) - q + 1):
+            b = grams.get(desc[i:i + q])
+            if b:
+                out |= b
+        return sorted(out)
+
+    def first_match(self, p, pred=None):
+        """Index of the first listed problem that ``matches(p)`` (and passes
+        ``pred``), or -1: the result of the reference's linear scan."""
+        problems = self.problems
+        for i in self.candidates(p.desc):
+            cp = problems[i]
+            if cp.matches(p) and (pred is None or pred(cp)):
+                return i
+        return -1
 
 
 class Cache:
@@ -439,12 +529,15 @@ class Cache:
             log.warning("Unresolved problem. Not going to be added to cache.")
             return False
         with self._lock:
-            for i, cp in enumerate(self.problems):
-                if cp.matches(p):
-                    log.warning("A solution already exists in cache for [%s], rewriting", p.desc)
-                    self.problems[i] = p.copy()
-                    break
+            idx = self._index()
+            i = idx.first_match(p)
+            if i >= 0:
+                log.warning("A solution already exists in cache for [%s], rewriting", p.desc)
+                self.problems[i] = p.copy()
+                idx.remove(i)
+                idx.add(i, p.desc)
             else:
+                idx.add(len(self.problems), p.desc)
                 self.problems.append(p.copy())
             if self.write_behind:
                 self.dirty = True
@@ -476,20 +569,28 @@ class Cache:
         if p.resolved:
             log.warning("Problem already solved.")
             return p
-        for cp in self.problems:
-            if cp.matches(p) and cp.resolved:
-                p.set_answer(cp.answer)
-                return p
+        with self._lock:
+            i = self._index().first_match(p, lambda cp: cp.resolved)
+        if i >= 0:
+            p.set_answer(self.problems[i].answer)
+            return p
         raise ProblemError("The problem %r was not found in the cache" % (p.desc,))
+
+    def _index(self):
+        idx = self.__dict__.get("_desc_index")
+        if idx is None or not idx.fresh(self.problems):
+            idx = self._desc_index = _DescIndex(self.problems)
+        return idx
 
     def _merge(self, other):
         # the reference's inner ``continue`` does not skip duplicates;
         # "fixed" compat drops later duplicates as the log message intends.
         from ..utils.constants import settings
+        idx = self._index()
         for p in other.problems:
-            dup = any(op.matches(p) for op in self.problems)
-            if dup:
+            if idx.first_match(p) >= 0:
                 log.warning("There are two answers for %s in cache. Ignoring latter ones.", p.desc)
                 if settings.fixed:
                     continue
+            idx.add(len(self.problems), p.desc)
             self.problems.append(p)

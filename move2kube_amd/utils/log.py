@@ -78,6 +78,7 @@ class _Logger:
 
     def setLevel(self, level):
         self.level = level
+        _rebind()
 
     def log(self, level, msg, *args):
         if level < self.level:
@@ -158,8 +159,22 @@ def set_quiet():
     logger.setLevel(ERROR)
 
 
-def debug(msg, *args):
+def _debug(msg, *args):
     logger.debug(msg, *args)
+
+
+def _off(msg, *args):
+    """``log.debug`` while debug logging is off: one call, no level test or
+    formatting (hot loops log per item)."""
+
+
+debug = _off
+
+
+def _rebind():
+    # ``log.debug`` is looked up on the module at every call site
+    global debug
+    debug = _debug if logger.level <= DEBUG else _off
 
 
 def info(msg, *args):
