@@ -30,7 +30,8 @@ def _last_json(stdout):
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only contract test")
 def test_single_rank():
-    p = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--check-runs", "1"], cwd=ROOT,
+    p = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--check-runs", "1",
+                        "--large-tree", "20,60"], cwd=ROOT,
                        env=_env(),
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
     assert p.returncode == 0, p.stderr.decode()
@@ -38,8 +39,10 @@ def test_single_rank():
     assert KEYS <= set(d)
     assert d["n_gpus"] == 1 and d["steps"] == 1 and d["value"] > 0
     assert d["manifest_diff_vs_ref"] == 0 and d["manifest_diff_vs_ref_headline"] == 0
-    assert sorted(d["per_config"]) == ["cf", "docker-compose", "golang", "helm-openshift", "java-cnb"]
-    assert all(v["manifest_diff_vs_ref"] == 0 for v in d["per_config"].values())
+    assert sorted(d["per_config"]) == ["cf", "docker-compose", "golang", "helm-openshift", "java-cnb", "large-tree"]
+    lt = d["per_config"]["large-tree"]
+    assert sorted(lt["large_tree_translate_ms_per_service"]) == ["20", "60"] and lt["ratio_largest_vs_smallest"] > 0
+    assert all(v["manifest_diff_vs_ref"] == 0 for k, v in d["per_config"].items() if k != "large-tree")
     # the headline names BASELINE.json configuration 5 verbatim
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         assert d["config"]["model"] in json.load(f)["configs"]
