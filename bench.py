@@ -70,7 +70,9 @@ def per_config_checks(runs):
         r = baseline_configs.warm_runs(name, runs)
         cold, cold_diff = baseline_configs.cold_runs(name, runs)
         out[name] = {"manifest_diff_vs_ref": r["manifest_diff_vs_ref"] + cold_diff,
-                     "warm_p50_ms": r["warm_p50_ms"], "cold_p50_ms": cold}
+                     "warm_p50_ms": r["warm_p50_ms"], "cold_p50_ms": cold["cold_p50_ms"],
+                     "cold_over_floor_p50_ms": cold["cold_over_floor_p50_ms"],
+                     "cold_launcher_p50_ms": cold["cold_launcher_p50_ms"]}
     return out
 
 

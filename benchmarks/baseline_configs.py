@@ -17,6 +17,10 @@ this reports:
   compares against; byte-compiled modules cached as in an installed package;
   ``cold_cpu_p50_ms`` is their CPU time and ``cold_over_floor_p50_ms`` the
   time above a bare ``python -c pass`` per process, paired run by run;
+* ``cold_launcher_p50_ms`` / ``cold_launcher_over_floor_p50_ms`` - the same
+  commands through the release archive's launcher (``python3 -S
+  bin/m2k_main.py``, ``scripts/builddist.py``), and its time above a bare
+  ``python -S -c pass``;
 * ``python_emulation_of_reference_fork_model_p50_ms`` - p50 of in-process runs
   with every detector forked as ``/bin/sh`` one at a time on one worker, the
   way ``dockerfilecontainerizer.go:76-83`` runs them.  This is a Python
@@ -123,7 +127,10 @@ def cold_stats(name, runs):
         extra = {"PYTHONPYCACHEPREFIX": os.path.join(work, "pycache")}
         env = run.env()
         env.update(extra)
+        launcher = refconfigs.release_launcher(work)
         walls, cpus, over, diff = [], [], [], 0
+        lwalls, lover = [], []
+        ncmd = len(run.cli_commands())
         for i in range(-1, runs):
             t0 = time.perf_counter()
             subprocess.run([sys.executable, "-c", "pass"], env=env)
@@ -135,18 +142,29 @@ def cold_stats(name, runs):
             if i >= 0:
                 walls.append(wall)
                 cpus.append(_children_cpu_ms() - c0)
-                over.append(wall - floor * len(run.cli_commands()))
+                over.append(wall - floor * ncmd)
+            diff += refconfigs.manifest_diff_vs_ref(name, out) or 0
+            t0 = time.perf_counter()
+            subprocess.run([sys.executable, "-S", "-c", "pass"], env=env)
+            floor = (time.perf_counter() - t0) * 1e3
+            t0 = time.perf_counter()
+            out = run.run_cli(extra_env=extra, launcher=launcher)
+            wall = (time.perf_counter() - t0) * 1e3
+            if i >= 0:
+                lwalls.append(wall)
+                lover.append(wall - floor * ncmd)
             diff += refconfigs.manifest_diff_vs_ref(name, out) or 0
         return {"cold_p50_ms": _p50(walls), "cold_cpu_p50_ms": _p50(cpus), "cold_over_floor_p50_ms": _p50(over),
+                "cold_launcher_p50_ms": _p50(lwalls), "cold_launcher_over_floor_p50_ms": _p50(lover),
                 "manifest_diff_vs_ref": diff}
     finally:
         shutil.rmtree(work, ignore_errors=True)
 
 
 def cold_runs(name, runs):
-    """(cold p50 ms, total manifest diff vs ref) - see :func:`cold_stats`."""
+    """(cold stats without the diff, total manifest diff vs ref) - see :func:`cold_stats`."""
     st = cold_stats(name, runs)
-    return st["cold_p50_ms"], st["manifest_diff_vs_ref"]
+    return st, st.pop("manifest_diff_vs_ref")
 
 
 def bench_config(name, runs, emulation_runs):
@@ -157,12 +175,12 @@ def bench_config(name, runs, emulation_runs):
     return res
 
 
-def interpreter_floor(runs):
+def interpreter_floor(runs, flags=()):
     """p50 of a bare ``python -c pass`` (the cold-run floor no Python CLI can beat)."""
     times = []
     for _ in range(runs):
         t0 = time.perf_counter()
-        subprocess.run([sys.executable, "-c", "pass"])
+        subprocess.run([sys.executable] + list(flags) + ["-c", "pass"])
         times.append((time.perf_counter() - t0) * 1e3)
     return _p50(times)
 
@@ -180,7 +198,8 @@ def main():
     root, workdir_fs = refconfigs.workdir_root(args.workdir)
     if root is not None:
         tempfile.tempdir = root
-    results = {"runs": args.runs, "workdir_fs": workdir_fs, "python_floor_ms": interpreter_floor(args.runs), "configs": []}
+    results = {"runs": args.runs, "workdir_fs": workdir_fs, "python_floor_ms": interpreter_floor(args.runs),
+               "python_floor_nosite_ms": interpreter_floor(args.runs, ["-S"]), "configs": []}
     # the headline corpus with default answers (Yamls, Kubernetes): what the
     # Helm + Openshift + operator output of the same 15 services costs on top
     yamls = warm_runs("samples-yamls", args.runs)

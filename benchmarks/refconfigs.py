@@ -229,14 +229,16 @@ class Run:
         cmds.append(t)
         return cmds
 
-    def run_cli(self, extra_env=None, cwd=None):
-        """Run the commands as separate ``python -m move2kube_amd`` processes."""
+    def run_cli(self, extra_env=None, cwd=None, launcher=None):
+        """Run the commands as separate ``python -m move2kube_amd`` processes
+        (or ``launcher + argv``, e.g. :func:`release_launcher`)."""
         env = self.env()
         env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
         if extra_env:
             env.update(extra_env)
+        prefix = launcher or [sys.executable, "-m", "move2kube_amd"]
         for argv in self.cli_commands():
-            p = subprocess.run([sys.executable, "-m", "move2kube_amd"] + argv, env=env, cwd=cwd or self.work,
+            p = subprocess.run(prefix + argv, env=env, cwd=cwd or self.work,
                                stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
             if p.returncode != 0:
                 raise RuntimeError("%s failed: %s" % (argv[0], p.stderr.decode(errors="replace")[-2000:]))
@@ -245,6 +247,18 @@ class Run:
                 shutil.rmtree(dst, ignore_errors=True)
                 shutil.copytree(os.path.join(self.work, "collect", "m2k_collect"), dst)
         return self.out
+
+
+def release_launcher(dirpath):
+    """argv prefix of what ``bin/move2kube`` of a release archive runs
+    (``scripts/builddist.py``: ``python3 -S bin/m2k_main.py``), with the entry
+    script written to ``dirpath`` and pointed at this tree."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import builddist
+    entry = os.path.join(dirpath, "m2k_main.py")
+    with open(entry, "w") as f:
+        f.write(builddist.ENTRY.replace("os.path.dirname(os.path.dirname(os.path.abspath(__file__)))", repr(ROOT)))
+    return [sys.executable, "-S", entry]
 
 
 def workdir_root(choice):

@@ -7,8 +7,6 @@ triggers).  Volume mounts without a volume are dropped and volumes are
 converted to kinds the cluster supports.
 """
 
-import copy
-
 from ..utils import common, log
 from ..utils.constants import settings
 from .base import (GOTYPE, IAPIResource, get_annotations, get_pod_labels, get_service_labels, is_type,
@@ -74,7 +72,7 @@ class Deployment(IAPIResource):
         return m
 
     def _podspec(self, service, restart="Always"):
-        ps = copy.deepcopy(service.pod_spec)
+        ps = common.deep_copy(service.pod_spec)
         ps = self.convert_volumes_kinds_by_policy(ps)
         ps["restartPolicy"] = restart
         return ps
@@ -131,7 +129,7 @@ class Deployment(IAPIResource):
                          "template": {"metadata": object_meta_copy(m), "spec": ps}}}
 
     def pod_to_job(self, pod):
-        ps = self.convert_volumes_kinds_by_policy(copy.deepcopy(pod.get("spec") or {}))
+        ps = self.convert_volumes_kinds_by_policy(common.deep_copy(pod.get("spec") or {}))
         ps["restartPolicy"] = "OnFailure"
         m = pod.get("metadata") or {}
         return {"kind": JOB, "apiVersion": "batch/v1", "metadata": m,
@@ -157,33 +155,33 @@ class Deployment(IAPIResource):
             return [obj], True
         if is_type(obj, "batch/v1", JOB) and not common.is_string_present(supported, JOB):
             if common.is_string_present(supported, POD):
-                return [self.to_pod(m, copy.deepcopy(tmpl_spec), "OnFailure")], True
+                return [self.to_pod(m, common.deep_copy(tmpl_spec), "OnFailure")], True
             log.warning("Both Job and Pod not supported. No other valid way to translate this object. : %s", m.get("name"))
             return [obj], True
         if common.is_string_present(supported, DEPLOYMENT_CONFIG):
             if is_type(obj, "apps/v1", DEPLOYMENT) or is_type(obj, "v1", REPLICATION_CONTROLLER):
-                return [self.to_deployment_config(m, copy.deepcopy(tmpl_spec), replicas or 0)], True
+                return [self.to_deployment_config(m, common.deep_copy(tmpl_spec), replicas or 0)], True
             if is_type(obj, "v1", POD):
-                return [self.to_deployment_config(m, copy.deepcopy(spec), 2)], True
+                return [self.to_deployment_config(m, common.deep_copy(spec), 2)], True
             return [obj], True
         if common.is_string_present(supported, DEPLOYMENT):
             if is_type(obj, "apps.openshift.io/v1", DEPLOYMENT_CONFIG):
-                return [self.to_deployment(m, copy.deepcopy(tmpl_spec), replicas or 0)], True
+                return [self.to_deployment(m, common.deep_copy(tmpl_spec), replicas or 0)], True
             if is_type(obj, "v1", REPLICATION_CONTROLLER):
-                return [self.to_deployment(m, copy.deepcopy(tmpl_spec), replicas or 0)], True
+                return [self.to_deployment(m, common.deep_copy(tmpl_spec), replicas or 0)], True
             if is_type(obj, "v1", POD):
-                return [self.to_deployment(m, copy.deepcopy(spec), 2)], True
+                return [self.to_deployment(m, common.deep_copy(spec), 2)], True
             return [obj], True
         if common.is_string_present(supported, REPLICATION_CONTROLLER):
             if is_type(obj, "apps.openshift.io/v1", DEPLOYMENT_CONFIG) or is_type(obj, "apps/v1", DEPLOYMENT):
-                return [self.to_replication_controller(m, copy.deepcopy(tmpl_spec), replicas or 0)], True
+                return [self.to_replication_controller(m, common.deep_copy(tmpl_spec), replicas or 0)], True
             if is_type(obj, "v1", POD):
-                return [self.to_replication_controller(m, copy.deepcopy(spec), 2)], True
+                return [self.to_replication_controller(m, common.deep_copy(spec), 2)], True
             return [obj], True
         if common.is_string_present(supported, POD):
             if (is_type(obj, "apps.openshift.io/v1", DEPLOYMENT_CONFIG) or is_type(obj, "apps/v1", DEPLOYMENT)
                     or is_type(obj, "v1", REPLICATION_CONTROLLER)):
-                return [self.to_pod(m, copy.deepcopy(tmpl_spec), "Always")], True
+                return [self.to_pod(m, common.deep_copy(tmpl_spec), "Always")], True
             return [obj], True
         return None, False
 
@@ -195,9 +193,9 @@ class Deployment(IAPIResource):
         for gv, kind in (("apps.openshift.io/v1", DEPLOYMENT_CONFIG), ("apps/v1", DEPLOYMENT),
                          ("v1", REPLICATION_CONTROLLER), ("batch/v1", JOB), ("apps/v1", DAEMONSET)):
             if is_type(obj, gv, kind):
-                return m.get("name", ""), copy.deepcopy((spec.get("template") or {}).get("spec") or {})
+                return m.get("name", ""), common.deep_copy((spec.get("template") or {}).get("spec") or {})
         if is_type(obj, "v1", POD):
-            return m.get("name", ""), copy.deepcopy(spec)
+            return m.get("name", ""), common.deep_copy(spec)
         raise ValueError("Incompatible object type")
 
     def convert_volumes_kinds_by_policy(self, ps):

@@ -2,8 +2,6 @@
 ``internal/apiresource/imagestream.go``, ``networkpolicy.go``,
 ``knativeservice.go``)."""
 
-import copy
-
 from ..utils import common, log
 from ..utils.constants import ANNOTATION_LABEL_VALUE, GROUP_NAME
 from .base import IAPIResource, get_annotations, get_service_labels, is_type
@@ -91,7 +89,7 @@ class KnativeService(IAPIResource):
     def create_new_resources(self, ir, supported):
         objs = []
         for service in ir.sorted_services():
-            ps = copy.deepcopy(service.pod_spec)
+            ps = common.deep_copy(service.pod_spec)
             ps["restartPolicy"] = "Always"
             m = {"name": service.name, "labels": get_service_labels(service.name)}
             ann = get_annotations(service)

@@ -7,8 +7,6 @@ ClusterIP Service (headless when it has no ports).  Existing Routes, Ingresses
 and NodePort/LoadBalancer Services are converted to what the cluster supports.
 """
 
-import copy
-
 from ..utils import common, log
 from ..utils.constants import EXPOSE_SELECTOR
 from .base import IAPIResource, get_annotations, get_service_labels, is_type, object_meta_copy
@@ -115,7 +113,7 @@ class Service(IAPIResource):
             tp = _int_or_string(sp.get("name", ""), sp.get("port", 0))
             objs.append(self._route(object_meta_copy(service.get("metadata")), ir.target_cluster_spec.host,
                                     path, name, tp))
-        svc = copy.deepcopy(service)
+        svc = common.deep_copy(service)
         svc.setdefault("spec", {})["type"] = "ClusterIP"
         objs.append(svc)
         return objs
@@ -151,7 +149,7 @@ class Service(IAPIResource):
                "metadata": object_meta_copy(service.get("metadata")), "spec": {"rules": rules}}
         if ir.is_ingress_tls_enabled():
             ing["spec"]["tls"] = [{"hosts": [ir.target_cluster_spec.host], "secretName": ir.ingress_tls_secret_name}]
-        svc = copy.deepcopy(service)
+        svc = common.deep_copy(service)
         svc.setdefault("spec", {})["type"] = "ClusterIP"
         return [ing, svc]
 

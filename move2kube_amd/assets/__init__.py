@@ -11,11 +11,10 @@
 * ``cfbuildpacks.json`` - built-in CF buildpack containerization map.
 """
 
-import json
 import os
 import shutil
 
-from ..utils import log
+from ..utils import fastjson, log
 from ..utils.constants import ASSETS_DIR, TEMP_DIR_PREFIX, settings
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -40,13 +39,13 @@ def builtin_clusters():
     global _clusters
     if _clusters is None:
         with open(os.path.join(HERE, "clusters.json")) as f:
-            _clusters = json.load(f)
+            _clusters = fastjson.load(f)
     return _clusters
 
 
 def builtin_cf_buildpacks():
     with open(os.path.join(HERE, "cfbuildpacks.json")) as f:
-        return json.load(f)["buildpackContainerizers"]
+        return fastjson.load(f)["buildpackContainerizers"]
 
 
 def _copy_tree(src, dst):

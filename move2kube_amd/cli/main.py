@@ -5,7 +5,6 @@ Verbs and flags match the reference: ``collect [-a] [-o] [-s]``,
 (+ hidden ``--qadisablecli --qaskip --qaport``), ``version [-l]``; global ``-v``.
 """
 
-import argparse
 import errno
 import os
 import stat
@@ -22,15 +21,6 @@ from ..utils.lazyre import LazyModule
 # first use: `collect` and `version` never need it
 move2kube = LazyModule("move2kube_amd.move2kube")
 qaengine = LazyModule("move2kube_amd.qaengine")
-
-
-class _StringSlice(argparse.Action):
-    """cobra StringSlice: repeatable, each value comma-separated."""
-
-    def __call__(self, parser, namespace, values, option_string=None):
-        cur = list(getattr(namespace, self.dest) or [])
-        cur.extend(v for v in values.split(",") if v != "")
-        setattr(namespace, self.dest, cur)
 
 
 def _abs(p):
@@ -185,82 +175,84 @@ def version_handler(a):
     print(info.get_version() if not a.long else yamlio.dump(info.get_version_info().to_yaml()))
 
 
-_VERBS = ("collect", "plan", "translate", "version")
+class _Args:
+    """The parsed flags of one command (cobra flag values by name)."""
+
+    def __init__(self, cmd):
+        for f in cmd.all_flags():
+            setattr(self, f.name, f.value)
+        self.command = cmd.name
+        self.cmd = cmd
 
 
-def _verb_of(argv):
-    """The sub-command named on the command line (after the root flags), or None."""
-    for arg in argv:
-        if arg in ("-v", "--verbose"):
-            continue
-        return arg if arg in _VERBS else None
-    return None
+def build_command_tree():
+    """The reference's cobra command tree (``cmd/move2kube/move2kube.go:37-51``,
+    ``collect.go:78-89``, ``plan.go:90-103``, ``translate.go:187-214``,
+    ``version.go:30-39``)."""
+    from .cobra import Command, add_help_command
+    root = Command("move2kube", "A tool to modernize to kubernetes/openshift",
+                   "move2kube is a tool to help optimally translate from platforms such as docker-swarm, CF to "
+                   "Kubernetes.")
+    root.flag("verbose", "v", "bool", False, "Enable verbose output", persistent=True)
 
+    c = Command("collect", "Collect and process metadata from multiple sources.",
+                "Collect metadata from multiple sources (cluster, image repo etc.), filter and summarize it into a "
+                "yaml.", run=collect_handler)
+    c.flag("annotations", "a", "string", "", "Specify annotations to select collector subset.")
+    c.flag("outpath", "o", "string", ".", "Specify output directory for collect.")
+    c.flag("source", "s", "string", "", "Specify source directory for the artifacts to be considered while "
+                                         "collecting.")
 
-def build_parser(only=None):
-    """The cobra command tree as argparse.  ``only`` = the verb being run: its
-    arguments are the only ones built (argparse translates every help string
-    through gettext as it is added, a measurable share of a cold run); the
-    other verbs stay registered, so choices and errors are unchanged."""
-    root = argparse.ArgumentParser(prog="move2kube", description="A tool to modernize to kubernetes/openshift")
-    root.add_argument("-v", "--verbose", action="store_true", help="Enable verbose output")
-    sub = root.add_subparsers(dest="command")
+    p = Command("plan", "Plan out a move", "Discover and create a plan file based on an input directory",
+                run=plan_handler)
+    p.flag("source", "s", "string", ".", "Specify source directory.")
+    p.flag("plan", "p", "string", DEFAULT_PLAN_FILE, "Specify a file path to save plan to.")
+    p.flag("name", "n", "string", DEFAULT_PROJECT_NAME, "Specify the project name.")
+    p.mark_required("source")
 
-    def wanted(verb):
-        return only is None or only == verb
+    t = Command("translate", "Translate using move2kube plan", "Translate artifacts using move2kube plan",
+                run=translate_handler)
+    t.flag("plan", "p", "string", DEFAULT_PLAN_FILE, "Specify a plan file to execute.")
+    t.flag("curate", "c", "bool", False, "Specify whether to curate the plan with a q/a.")
+    t.flag("source", "s", "string", "", "Specify source directory to translate. If you already have a m2k.plan "
+                                         "then this will override the rootdir value specified in that plan.")
+    t.flag("outpath", "o", "string", ".", "Path for output. Default will be directory with the project name.")
+    t.flag("name", "n", "string", DEFAULT_PROJECT_NAME, "Specify the project name.")
+    t.flag("qacache", "q", "stringSlice", [], "Specify qa cache file locations")
+    t.flag("ignoreenv", "", "bool", False, "Ignore data from local machine.")
+    t.flag("qadisablecli", "", "bool", False, "Enable/disable the QA Cli sub-system. Without this system, you will "
+           "have to use the REST API to interact.", hidden=True)
+    t.flag("qaskip", "", "bool", False, "Enable/disable the default answers to questions posed in QA Cli "
+           "sub-system. If disabled, you will have to answer the questions posed by QA during interaction.",
+           hidden=True)
+    t.flag("qaport", "", "int", 0, "Port for the QA service. By default it chooses a random free port.", hidden=True)
 
-    c = sub.add_parser("collect", help="Collect and process metadata from multiple sources.")
-    if wanted("collect"):
-        c.add_argument("-a", "--annotations", default="", help="Specify annotations to select collector subset.")
-        c.add_argument("-o", "--outpath", default=".", help="Specify output directory for collect.")
-        c.add_argument("-s", "--source", default="", help="Specify source directory for the artifacts to be considered while collecting.")
-        c.set_defaults(func=collect_handler)
+    v = Command("version", "Print the client version information", "Print the client version information",
+                run=version_handler)
+    v.flag("long", "l", "bool", False, "print the version details")
 
-    p = sub.add_parser("plan", help="Plan out a move")
-    if wanted("plan"):
-        p.add_argument("-s", "--source", required=True, help="Specify source directory.")
-        p.add_argument("-p", "--plan", default=DEFAULT_PLAN_FILE, help="Specify a file path to save plan to.")
-        p.add_argument("-n", "--name", default=DEFAULT_PROJECT_NAME, help="Specify the project name.")
-        p.set_defaults(func=plan_handler)
-
-    t = sub.add_parser("translate", help="Translate using move2kube plan")
-    if wanted("translate"):
-        t.add_argument("-p", "--plan", default=None, help="Specify a plan file to execute.")
-        t.add_argument("-c", "--curate", action="store_true", help="Specify whether to curate the plan with a q/a.")
-        t.add_argument("-s", "--source", default=None, help="Specify source directory to translate.")
-        t.add_argument("-o", "--outpath", default=".", help="Path for output. Default will be directory with the project name.")
-        t.add_argument("-n", "--name", default=None, help="Specify the project name.")
-        t.add_argument("-q", "--qacache", action=_StringSlice, default=[], help="Specify qa cache file locations")
-        t.add_argument("--ignoreenv", action="store_true", help="Ignore data from local machine.")
-        t.add_argument("--qadisablecli", action="store_true", help=argparse.SUPPRESS)
-        t.add_argument("--qaskip", action="store_true", help=argparse.SUPPRESS)
-        t.add_argument("--qaport", type=int, default=0, help=argparse.SUPPRESS)
-        t.set_defaults(func=translate_handler)
-
-    v = sub.add_parser("version", help="Print the client version information")
-    if wanted("version"):
-        v.add_argument("-l", "--long", action="store_true", help="print the version details")
-        v.set_defaults(func=version_handler)
+    root.add(c, p, t, v)
+    add_help_command(root)
     return root
 
 
 def main(argv=None):
+    from . import cobra
     if argv is None:
         argv = sys.argv[1:]
-    parser = build_parser(_verb_of(argv))
-    a = parser.parse_args(argv)
+    res = cobra.execute(build_command_tree(), argv)
+    if isinstance(res, int):
+        return res
+    cmd, positional = res
+    a = _Args(cmd)
     if a.verbose:
         log.set_verbose(True)
-    if not getattr(a, "func", None):
-        parser.print_help()
-        return 0
+    if cmd.name == "help":
+        return cmd.run(cmd, positional)
     if a.command == "translate":
-        a.plan_changed = a.plan is not None
-        a.source_changed = a.source is not None
-        a.name_changed = a.name is not None
-        a.plan = a.plan if a.plan is not None else DEFAULT_PLAN_FILE
-        a.source = a.source or ""
-        a.name = a.name if a.name is not None else DEFAULT_PROJECT_NAME
+        a.plan_changed = cmd.changed("plan")
+        a.source_changed = cmd.changed("source")
+        a.name_changed = cmd.changed("name")
     try:
         assets.setup()
     except OSError as e:
@@ -268,7 +260,7 @@ def main(argv=None):
         return 1
     try:
         with yamlio.parse_cache():  # one command = one parse of each YAML document
-            a.func(a)
+            cmd.run(a)
     except log.FatalError:
         return 1
     finally:

@@ -11,12 +11,11 @@ per process so that a missing runtime costs one probe, not one per directory.
 """
 
 import io
-import json
 import os
 import shutil
 import threading
 
-from ...utils import common, log
+from ...utils import common, fastjson, log
 from ...utils.constants import settings
 from ...utils.lazyre import LazyModule
 
@@ -39,7 +38,7 @@ _lock = threading.Lock()
 
 def get_builders_from_label(label):
     try:
-        order = json.loads(label)
+        order = fastjson.loads(label)
     except (ValueError, TypeError) as e:
         log.warning("Unable to read order : %s", e)
         return []
@@ -100,6 +99,7 @@ class DockerAPIProvider:
         try:
             hdrs = dict(headers or {})
             if body is not None and not isinstance(body, (bytes, bytearray)) and not hasattr(body, "read"):
+                import json
                 body = json.dumps(body).encode()
                 hdrs.setdefault("Content-Type", "application/json")
             conn.request(method, path, body=body, headers=hdrs)
@@ -113,7 +113,7 @@ class DockerAPIProvider:
             raise ProviderError("docker API %s %s: %d %s" % (method, path, resp.status, data[:200]))
         if raw:
             return data
-        return json.loads(data.decode() or "null") if data else None
+        return fastjson.loads(data.decode() or "null") if data else None
 
     def pull_image(self, image):
         name, tag = (image.rsplit(":", 1) + ["latest"])[:2] if ":" in image.rsplit("/", 1)[-1] else (image, "latest")
@@ -495,7 +495,7 @@ class RuncProvider:
             if p.returncode != 0:
                 continue
             try:
-                labels = json.loads(p.stdout.decode()).get("Labels") or {}
+                labels = fastjson.loads(p.stdout.decode()).get("Labels") or {}
             except ValueError:
                 continue
             if ORDER_LABEL in labels:

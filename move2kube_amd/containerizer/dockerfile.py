@@ -8,14 +8,13 @@ template.  All other files of the detector directory are copied next to the
 generated ``Dockerfile.<service>``.
 """
 
-import json
 import os
 
 from .. import assets
 from ..models import ir as irtypes
 from ..models import plan as plantypes
 from ..parallel.detect_pool import run_detect, run_detect_jobs
-from ..utils import common, log
+from ..utils import common, fastjson, log
 from ..utils.fsindex import get_index
 from ..utils.gotemplate import TemplateError
 from .base import CONTAINERIZER_JSON_PORT, Containerizer, ContainerizerError
@@ -25,7 +24,7 @@ DOCKERFILE_DETECT_SCRIPT = "m2kdfdetect.sh"
 
 def parse_detect_output(output):
     """JSON object from a detect script; numbers decode as float64 like Go's encoding/json."""
-    return json.loads(output, parse_int=float)
+    return fastjson.loads(output, parse_int=float)
 
 
 def _port_from(m):

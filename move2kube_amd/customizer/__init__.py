@@ -2,14 +2,12 @@
 registry (QA; image refs + ``~/.docker/config.json``) -> storage (QA; hostPath to
 PVC, storage classes) -> ingress host/TLS (QA)."""
 
-import base64
-import json
 import os
 
 from .. import qaengine
 from ..models import ir as irtypes
 from ..models import qa
-from ..utils import common, log, trace
+from ..utils import common, fastjson, log, trace
 from ..utils.constants import DEFAULT_PVC_SIZE, DEFAULT_REGISTRY_URL, IMAGE_PULL_SECRET_PREFIX, settings
 
 OTHER_REGISTRY = "Other"
@@ -25,7 +23,7 @@ def load_docker_auths():
     path = os.path.join(_docker_config_dir(), "config.json")
     try:
         with open(path) as f:
-            cfg = json.load(f)
+            cfg = fastjson.load(f)
     except (OSError, ValueError):
         return {}
     return {k: (v or {}).get("auth", "") for k, v in (cfg.get("auths") or {}).items()}
@@ -129,6 +127,7 @@ class RegistryCustomizer:
                 # the plain fields, so a config-file login alone serialises as an empty entry
                 entry = {}
                 if dauth["username"] or dauth["password"]:
+                    import base64
                     entry["auth"] = base64.b64encode(("%s:%s" % (dauth["username"], dauth["password"])).encode()).decode()
                 elif settings.fixed and dauth["auth"]:
                     entry["auth"] = dauth["auth"]
@@ -137,9 +136,11 @@ class RegistryCustomizer:
                     # to; only now is it referenced from imagePullSecrets
                     secret_name = IMAGE_PULL_SECRET_PREFIX + common.make_file_name_compliant(registry)
                     pull_secrets[registry] = secret_name
+                    import json
                     content = json.dumps({"auths": {registry: entry}}, indent="\t").encode()
                 else:
                     secret_name = pull_secrets.get(registry, "")
+                    import json
                     content = json.dumps({"auths": {ir.kubernetes.registry_url: entry}}, indent="\t").encode()
                 ir.add_storage(irtypes.Storage(name=secret_name, storage_type=irtypes.PULL_SECRET_KIND,
                                                content={".dockerconfigjson": content}))

@@ -31,8 +31,8 @@ instead reshapes an Ingress to the profile's preferred version and relabels
 template labels so the result stays a valid object (DEVIATIONS.md §4).
 """
 
-import copy
 
+from ..utils import common
 from . import scheme
 
 # What NewNotRegisteredErrForTarget prints as the scheme name: the call site of
@@ -175,7 +175,7 @@ def _backend_to_v1(b):
 
 def _reshape_ingress(obj, target):
     src = obj.get("apiVersion", "")
-    out = copy.deepcopy(obj)
+    out = common.deep_copy(obj)
     out["apiVersion"] = target
     spec = out.get("spec") or {}
     to_beta = target in _V1BETA1_INGRESS
@@ -201,7 +201,7 @@ def _reshape_ingress(obj, target):
 
 
 def _relabel_workload(obj, target):
-    out = copy.deepcopy(obj)
+    out = common.deep_copy(obj)
     out["apiVersion"] = target
     spec = out.get("spec")
     if isinstance(spec, dict) and not spec.get("selector"):

@@ -17,8 +17,6 @@ a struct name, ``*T`` (pointer), ``[]T`` (slice), ``map:T`` (map of T) or
 ``inline:T`` (embedded struct).
 """
 
-import base64
-
 _STRUCTS = {}
 
 
@@ -498,6 +496,7 @@ def _marshal_value(v, typ):
             return None
         if isinstance(v, str):
             return v
+        import base64
         return base64.b64encode(bytes(v)).decode()
     if typ == "Time":
         return v if v else None

@@ -11,7 +11,6 @@ here every consumer iterates services in sorted-name order (determinism fix,
 documented in SURVEY.md section 7.4 #5).
 """
 
-import copy as _copy
 
 from ..utils import common, log
 from ..utils.constants import ANNOTATION_LABEL_VALUE
@@ -118,8 +117,8 @@ class Service:
         return bool(self.annotations) and self.annotations.get(annotation) == ANNOTATION_LABEL_VALUE
 
     def copy(self):
-        s = _copy.copy(self)
-        s.pod_spec = _copy.deepcopy(self.pod_spec)
+        s = common.shallow_copy(self)
+        s.pod_spec = common.deep_copy(self.pod_spec)
         s.annotations = dict(self.annotations) if self.annotations is not None else None
         s.labels = dict(self.labels) if self.labels is not None else None
         s.port_forwardings = [PortForwarding(Port(f.service_port.number, f.service_port.name),
@@ -197,7 +196,7 @@ class Container:
             self.accessed_dirs.append(d)
 
     def copy(self):
-        c = _copy.copy(self)
+        c = common.shallow_copy(self)
         c.repo_info = self.repo_info.copy()
         c.image_names = list(self.image_names)
         c.new_files = dict(self.new_files)
@@ -242,14 +241,14 @@ class Storage:
             if self.content is not None and newst.content is not None:
                 self.content = newst.content
             self.storage_type = newst.storage_type
-            self.pvc_spec = _copy.deepcopy(newst.pvc_spec)
+            self.pvc_spec = common.deep_copy(newst.pvc_spec)
             return True
         log.debug("Mismatching storages [%s, %s]", self.name, newst.name)
         return False
 
     def copy(self):
-        s = _copy.copy(self)
-        s.pvc_spec = _copy.deepcopy(self.pvc_spec)
+        s = common.shallow_copy(self)
+        s.pvc_spec = common.deep_copy(self.pvc_spec)
         s.content = dict(self.content) if self.content is not None else None
         s.annotations = dict(self.annotations) if self.annotations is not None else None
         s.string_data = dict(self.string_data) if self.string_data is not None else None
@@ -406,7 +405,7 @@ class IR:
         return None, False
 
     def copy(self):
-        ir = _copy.copy(self)
+        ir = common.shallow_copy(self)
         ir.services = {k: v.copy() for k, v in self.services.items()}
         ir.storages = [s.copy() for s in self.storages]
         ir.containers = [c.copy() for c in self.containers]
@@ -415,7 +414,7 @@ class IR:
         ir.service_accounts = list(self.service_accounts)
         ir.kubernetes = self.kubernetes.copy()
         ir.target_cluster_spec = self.target_cluster_spec.copy()
-        ir.cached_objects = _copy.deepcopy(self.cached_objects)
+        ir.cached_objects = common.deep_copy(self.cached_objects)
         ir.values = self.values.copy()
         return ir
 

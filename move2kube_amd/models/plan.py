@@ -12,7 +12,6 @@ Schema and semantics follow the reference ``types/plan/plan.go:134-426`` and
   read -> write round-trips byte-for-byte.
 """
 
-import copy as _copy
 import os
 
 from ..utils import common, log, yamlio
@@ -170,7 +169,7 @@ class Service:
         return s
 
     def copy(self):
-        s = _copy.copy(self)
+        s = common.shallow_copy(self)
         s.source_types = list(self.source_types)
         s.target_options = list(self.target_options)
         s.source_artifacts = {k: list(v) for k, v in self.source_artifacts.items()}
@@ -315,7 +314,7 @@ class KubernetesOutput:
             self.target_cluster_path = new.target_cluster_path
 
     def copy(self):
-        return _copy.copy(self)
+        return common.shallow_copy(self)
 
 
 class Plan:

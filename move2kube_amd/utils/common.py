@@ -6,7 +6,6 @@ indexed walk shared by every planner instead of the reference's >=8 serial
 the reference (CRC-64/ECMA, FNV-64a, SHA-256 truncation).
 """
 
-import json
 import os
 import re
 import shutil
@@ -14,6 +13,38 @@ import shutil
 from . import log, yamlio
 from .constants import (DEFAULT_FILE_PERMISSION, GROUP_NAME, SCHEME_VERSION)
 from .lazyre import lazy as _lazy_re
+
+_ATOMS = (str, int, float, bool, type(None))
+
+
+def deep_copy(o):
+    """``copy.deepcopy`` of a JSON-shaped tree (plain dicts/lists of scalars)
+    without the copy module's memo and dispatch; anything else goes to
+    ``copy.deepcopy``."""
+    t = type(o)
+    if t is dict:
+        return {k: (v if type(v) in _ATOMS else deep_copy(v)) for k, v in o.items()}
+    if t is list:
+        return [v if type(v) in _ATOMS else deep_copy(v) for v in o]
+    if t in _ATOMS:
+        return o
+    import copy
+    return copy.deepcopy(o)
+
+
+def shallow_copy(obj):
+    """``copy.copy`` of a plain class instance (``__dict__`` and ``__slots__``)."""
+    cls = type(obj)
+    new = cls.__new__(cls)
+    d = getattr(obj, "__dict__", None)
+    if d is not None:
+        new.__dict__.update(d)
+    for klass in cls.__mro__:
+        for name in klass.__dict__.get("__slots__", ()):
+            if name not in ("__dict__", "__weakref__") and hasattr(obj, name):
+                setattr(new, name, getattr(obj, name))
+    return new
+
 
 # ---------------------------------------------------------------------------
 # hashing primitives (native when available; pure-python fallback is exact)
@@ -191,10 +222,12 @@ def read_move2kube_yaml(path, raw=True):
 
 
 def write_json(output_path, data):
+    import json
     write_text(output_path, json.dumps(data, separators=(",", ":")) + "\n")
 
 
 def read_json(path):
+    import json
     with open(path) as f:
         return json.load(f)
 

@@ -18,12 +18,12 @@ slice, print, printf, println, eq, ne, lt, le, gt, ge, html, js, urlquery,
 call).  Values print with Go ``fmt`` ``%v`` semantics.
 """
 
-import json
 import math
 import re
 
-from .yamlio import go_format_float
+from . import fastjson
 from .lazyre import lazy as _lazy_re
+from .yamlio import go_format_float
 
 
 class TemplateError(Exception):
@@ -182,6 +182,7 @@ def go_sprintf(fmt, args):
             elif isinstance(a, int):
                 s = "'%s'" % chr(a)
             else:
+                import json
                 s = json.dumps(go_sprint(a))
         elif verb == "d":
             s = str(a) if isinstance(a, int) and not isinstance(a, bool) else _bad_verb(verb, a)
@@ -455,9 +456,9 @@ def _parse_string(tok):
     if kind == "raw":
         return text[1:-1]
     if kind == "char":
-        return ord(json.loads('"' + text[1:-1].replace('"', '\\"') + '"'))
+        return ord(fastjson.loads('"' + text[1:-1].replace('"', '\\"') + '"'))
     try:
-        return json.loads(text)
+        return fastjson.loads(text)
     except ValueError:
         return text[1:-1].encode().decode("unicode_escape")
 

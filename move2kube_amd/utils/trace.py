@@ -13,7 +13,6 @@ Perfetto.  Disabled, a span costs one global read.
 
 import atexit
 import contextlib
-import json
 import os
 import threading
 import time
@@ -68,6 +67,7 @@ def flush():
         data = {"traceEvents": list(_events), "displayTimeUnit": "ms"}
     d = os.path.dirname(os.path.abspath(_path))
     os.makedirs(d, exist_ok=True)
+    import json
     with open(_path, "w") as f:
         json.dump(data, f)
     return _path

@@ -19,7 +19,6 @@ the go-yaml key comparator (Go maps).
 """
 
 import contextlib
-import copy
 import functools
 import math
 import re
@@ -767,6 +766,7 @@ def _tree_copy(o):
         return [v if type(v) in _ATOMS else _tree_copy(v) for v in o]
     if t in _ATOMS:
         return o
+    import copy
     return copy.deepcopy(o)
 
 

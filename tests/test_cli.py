@@ -4,6 +4,7 @@ name/root overrides, the plan/source flag rules (``translate.go:93-177``),
 QA-cache slices, version output (``version.go``)."""
 
 import os
+import re
 import shutil
 
 import pytest
@@ -63,9 +64,12 @@ def test_plan_bad_source_is_fatal(work, bad):
     assert cli.main(["plan", "-s", str(work / bad)]) == 1
 
 
-def test_plan_requires_source(work):
-    with pytest.raises(SystemExit):
-        cli.main(["plan"])
+def test_plan_requires_source(work, capsys):
+    # cobra MarkFlagRequired (plan.go:102): error + usage, then log.Fatalf
+    assert cli.main(["plan"]) == 1
+    err = capsys.readouterr().err
+    assert err.startswith('Error: required flag(s) "source" not set\nUsage:\n  move2kube plan [flags]\n')
+    assert re.search(r'FATA\[\d{4}\] Error: "required flag\(s\) \\"source\\" not set"', err)
 
 
 def test_translate_without_plan_plans_and_curates(work):

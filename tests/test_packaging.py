@@ -33,6 +33,22 @@ def test_builddist_and_install(tmp_path):
                           cwd=str(elsewhere), env=env)
     assert long.stdout.decode().splitlines()[:3] == ["version: v0.3.1+unreleased", "gitCommit: abc123",
                                                       "gitTreeState: clean"]
+    # the launcher starts the interpreter without site (-S) and still finds
+    # site-packages modules (PyYAML) for the optional paths
+    probe = prefix / "probe.py"
+    probe.write_text("import sys, yaml; print(sys.flags.no_site, yaml.__name__)\n")
+    launcher = os.path.realpath(str(prefix / "bin" / "move2kube"))
+    entry = os.path.join(os.path.dirname(launcher), "m2k_main.py")
+    with open(entry) as f:
+        code = f.read().replace("from move2kube_amd.cli.main import main  # noqa: E402\n\nsys.exit(main())\n",
+                                "exec(open(%r).read())\n" % str(probe))
+    probe_entry = os.path.join(os.path.dirname(launcher), "probe_main.py")
+    with open(probe_entry, "w") as f:
+        f.write(code)
+    p = subprocess.run([sys.executable, "-S", probe_entry], stdout=subprocess.PIPE, check=True, env=env)
+    assert p.stdout.decode().split() == ["1", "yaml"]
+    with open(launcher) as f:
+        assert '-S "$HERE/bin/m2k_main.py"' in f.read()
 
 
 def test_cli_version_and_help():
