@@ -57,7 +57,13 @@ def build_native(force=False, out=None, sanitize=None):
         return out
     inc = sysconfig.get_paths()["include"]
     cxx = os.environ.get("CXX", "g++")
-    opt = ["-O3"] if not sanitize else ["-O1", "-g"] + SANITIZERS[sanitize]
+    # The release build links libstdc++/libgcc statically with unused sections
+    # dropped and their symbols kept local: a CLI process then maps one 0.6 MB
+    # object instead of also loading and relocating the 2 MB libstdc++ (the
+    # extension's import went from 1.9 to 0.5 ms; every command imports it).
+    opt = (["-O3", "-fvisibility-inlines-hidden", "-ffunction-sections", "-fdata-sections", "-Wl,--gc-sections",
+            "-Wl,-O1", "-static-libstdc++", "-static-libgcc", "-Wl,--exclude-libs,ALL", "-s"]
+           if not sanitize else ["-O1", "-g"] + SANITIZERS[sanitize])
     _run([cxx] + opt + ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall",
                         "-I" + pybind11.get_include(), "-I" + inc] + srcs + ["-o", out + ".tmp", "-lpthread"])
     os.replace(out + ".tmp", out)
