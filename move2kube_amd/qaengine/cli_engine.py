@@ -1,11 +1,16 @@
 """Interactive terminal engine (reference ``internal/qaengine/cliengine.go``).
 
-The reference uses AlecAivazis/survey prompts; this engine renders the same
-prompt text (``"<id>. <desc> \\nHints: \\n <context>\\n"``) with numbered
-options on plain stdin/stdout, so it also works when scripted through a pipe.
+On a terminal (stdin and stdout both TTYs) the questions are asked with the
+survey-style raw-mode prompts of :mod:`.survey` - arrow-key Select and
+MultiSelect with filtering, Confirm, Input, Multiline, masked Password - as
+the reference does through AlecAivazis/survey.  When either side is not a
+terminal (a pipe, a script; survey itself fails there) or ``M2K_QA_PLAIN=1``,
+the same prompt text (``"<id>. <desc> \\nHints: \\n <context>\\n"``) is
+printed with numbered options and answers are read line by line.
 """
 
 import getpass
+import os
 import sys
 
 from ..models import qa
@@ -42,7 +47,22 @@ class CliEngine(Engine):
         self._out.write(s)
         self._out.flush()
 
+    def _terminal(self):
+        """A :class:`survey.Terminal` when both ends are TTYs, else None."""
+        if os.environ.get("M2K_QA_PLAIN", "") not in ("", "0"):
+            return None
+        try:
+            if not (os.isatty(self._in.fileno()) and os.isatty(self._out.fileno())):
+                return None
+        except (AttributeError, OSError, ValueError):
+            return None
+        from .survey import Terminal
+        return Terminal(self._in, self._out)
+
     def fetch_answer(self, prob):
+        term = self._terminal()
+        if term is not None:
+            return self._fetch_survey(term, prob)
         t = prob.type
         try:
             if t == qa.SELECT:
@@ -60,6 +80,39 @@ class CliEngine(Engine):
         except EOFError as e:
             log.fatal("Error while asking a question : %s", e)
         log.fatal("Unknown type found: %s", t)
+
+    def _fetch_survey(self, term, prob):
+        """cliengine.go:38-197 with the survey-style prompts."""
+        from . import survey
+        msg = self._message(prob)
+        t = prob.type
+        try:
+            if t == qa.SELECT:
+                d = prob.default[0] if prob.default else prob.options[0]
+                ans = [survey.select(term, msg, list(prob.options), d)]
+            elif t == qa.MULTISELECT:
+                ans = survey.multi_select(term, msg, list(prob.options), list(prob.default))
+            elif t == qa.CONFIRM:
+                d = False
+                if prob.default:
+                    try:
+                        from ..utils.common import cast_to_bool
+                        d = cast_to_bool(prob.default[0])
+                    except ValueError as e:
+                        log.warning("Unable to parse default value : %s", e)
+                ans = ["true" if survey.confirm(term, msg, d) else "false"]
+            elif t == qa.INPUT:
+                ans = [survey.input_line(term, msg, prob.default[0] if prob.default else "")]
+            elif t == qa.MULTILINE:
+                ans = [survey.multiline(term, msg, prob.default[0] if prob.default else "")]
+            elif t == qa.PASSWORD:
+                ans = [survey.password(term, msg)]
+            else:
+                log.fatal("Unknown type found: %s", t)
+        except (survey.Interrupt, EOFError, ValueError) as e:
+            log.fatal("Error while asking a question : %s", e)
+        prob.set_answer(ans)
+        return prob
 
     def _select(self, prob):
         d = prob.default[0] if prob.default else prob.options[0]
