@@ -669,6 +669,31 @@ def _marshal_fields(d, typ):
     return out
 
 
+_native_fn = None
+
+
+def _native_marshal():
+    """``schema_marshal`` of the native extension (ops/csrc/k8s_marshal.cpp),
+    compiled from ``_STRUCTS`` on first use; False when it is unavailable or
+    ``M2K_NATIVE_MARSHAL=0``.  This module stays its specification."""
+    global _native_fn
+    if _native_fn is None:
+        _native_fn = False
+        import os
+        if os.environ.get("M2K_NATIVE_MARSHAL", "1") != "0":
+            from ..ops import native
+            m = native.module()
+            if m is not None and hasattr(m, "schema_marshal"):
+                m.schema_init(_STRUCTS, _marshal_value)
+                _native_fn = m.schema_marshal
+    return _native_fn
+
+
+def _struct(d, typ):
+    fn = _native_marshal()
+    return fn(d, typ) if fn else _marshal_struct(d, typ)
+
+
 def marshal(obj):
     """Go json.Marshal of a typed Kubernetes object given as a JSON-shaped dict."""
     typ = type_for(obj)
@@ -676,12 +701,12 @@ def marshal(obj):
         out = dict(obj)
         md = out.get("metadata")
         if isinstance(md, dict):
-            out["metadata"] = _marshal_struct(md, "ObjectMeta")
+            out["metadata"] = _struct(md, "ObjectMeta")
         elif "metadata" not in out:
-            out["metadata"] = _marshal_struct({}, "ObjectMeta")
+            out["metadata"] = _struct({}, "ObjectMeta")
         return out
-    return _marshal_struct(obj, typ)
+    return _struct(obj, typ)
 
 
 def marshal_as(d, typ):
-    return _marshal_struct(d, typ)
+    return _struct(d, typ)

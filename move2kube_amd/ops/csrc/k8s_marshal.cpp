@@ -1,0 +1,432 @@
+// Go encoding/json struct-tag marshalling of the typed Kubernetes objects:
+// the native twin of move2kube_amd/k8s/schema.py::_marshal_struct, run on
+// every manifest `translate` writes (reference
+// internal/transformer/transformer.go:162-204 marshals each object through
+// its Go struct before the YAML encoder).
+//
+// schema.py stays the executable specification.  At first use it hands its
+// struct table (name -> [(json name, field type, omitempty)]) to
+// `schema_init`, which compiles every field type once; `schema_marshal(obj,
+// type)` then walks the JSON-shaped Python tree with the raw CPython API and
+// returns the same dict tree the Python code builds (same keys, same key
+// order, the same shared per-type empty-struct dicts).  Anything outside the
+// plain shapes - a non-dict where a struct is expected, a non-dict map, the
+// bytes / RawExtension field types - is handed back to the Python
+// implementation (`fallback(value, type)`), so both paths raise the same
+// errors on malformed objects.
+
+#include <Python.h>
+
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace m2kschema {
+
+enum Kind { K_IDENT, K_PTR, K_SLICE, K_MAP_PLAIN, K_MAP_OF, K_STR, K_BOOL, K_TIME, K_STRUCT, K_FALLBACK };
+enum Empty { E_NEVER, E_STR, E_INT, E_BOOL, E_LEN, E_ANY };
+enum Absent { A_SKIP, A_NONE, A_EMPTY_STRUCT, A_ZERO_STR, A_ZERO_INT, A_ZERO_BOOL };
+
+struct Type {
+  Kind kind;
+  int inner;   // element / pointee type (index into types)
+  int strct;   // struct index for K_STRUCT
+  PyObject* name;  // type string (for the fallback call)
+};
+
+struct Field {
+  PyObject* jname;
+  int type;
+  bool omit;
+  bool inline_;
+  Empty empty;
+  Absent absent;
+};
+
+struct Struct {
+  std::string name;
+  std::vector<Field> fields;
+  PyObject* keyed = nullptr;  // json name -> field index (PyLong)
+  std::vector<int> inlines;   // struct indices
+  PyObject* base = nullptr;   // fields an absent key still produces
+  PyObject* empty = nullptr;  // the marshalled empty struct (shared)
+  bool building = false;
+};
+
+struct Schema {
+  std::vector<Type> types;
+  std::unordered_map<std::string, int> type_index;
+  std::vector<Struct> structs;
+  std::unordered_map<std::string, int> struct_index;
+  PyObject* fallback = nullptr;  // (value, type) -> marshalled value
+  PyObject* zero = nullptr;      // 0
+  PyObject* empty_str = nullptr;  // ""
+};
+
+static Schema* g = nullptr;
+
+static int compile_type(const std::string& t);
+
+static int add_type(const std::string& t, Kind k, int inner, int strct) {
+  Type ty{k, inner, strct, PyUnicode_FromStringAndSize(t.data(), (Py_ssize_t)t.size())};
+  g->types.push_back(ty);
+  int ix = (int)g->types.size() - 1;
+  g->type_index[t] = ix;
+  return ix;
+}
+
+static int compile_type(const std::string& t) {
+  auto it = g->type_index.find(t);
+  if (it != g->type_index.end()) return it->second;
+  if (t.rfind("*", 0) == 0) return add_type(t, K_PTR, compile_type(t.substr(1)), -1);
+  if (t.rfind("[]", 0) == 0) return add_type(t, K_SLICE, compile_type(t.substr(2)), -1);
+  if (t == "map") return add_type(t, K_MAP_PLAIN, -1, -1);
+  if (t.rfind("map:", 0) == 0) return add_type(t, K_MAP_OF, compile_type(t.substr(4)), -1);
+  if (t == "bytes" || t == "RawExtension") return add_type(t, K_FALLBACK, -1, -1);
+  if (t == "Time") return add_type(t, K_TIME, -1, -1);
+  if (t == "string" || t == "Quantity" || t == "ArrayOrString") return add_type(t, K_STR, -1, -1);
+  if (t == "bool") return add_type(t, K_BOOL, -1, -1);
+  auto s = g->struct_index.find(t);
+  if (s != g->struct_index.end()) return add_type(t, K_STRUCT, -1, s->second);
+  return add_type(t, K_IDENT, -1, -1);  // int, IntOrString, any, unknown
+}
+
+static Empty empty_kind(const std::string& t) {
+  if (t.rfind("*", 0) == 0) return E_NEVER;
+  if (t == "string") return E_STR;
+  if (t == "int") return E_INT;
+  if (t == "bool") return E_BOOL;
+  if (t.rfind("[]", 0) == 0 || t.rfind("map", 0) == 0 || t == "bytes") return E_LEN;
+  if (t == "any") return E_ANY;
+  return E_NEVER;
+}
+
+static Absent absent_kind(const std::string& t, bool omit) {
+  if (g->struct_index.count(t)) return A_EMPTY_STRUCT;
+  if (t == "Time") return A_NONE;
+  if (omit) return A_SKIP;
+  if (t.rfind("*", 0) == 0 || t.rfind("[]", 0) == 0 || t.rfind("map", 0) == 0 || t == "any" || t == "bytes")
+    return A_NONE;
+  if (t == "string" || t == "ArrayOrString") return A_ZERO_STR;
+  if (t == "int" || t == "IntOrString") return A_ZERO_INT;
+  if (t == "bool") return A_ZERO_BOOL;
+  return A_NONE;
+}
+
+static PyObject* marshal_value(PyObject* v, int type);
+static PyObject* marshal_struct(PyObject* d, int strct);
+
+// the marshalled empty struct of `strct` (borrowed; cached)
+static PyObject* empty_struct(int strct);
+
+static PyObject* base_of(int strct) {
+  Struct& s = g->structs[strct];
+  if (s.base) return s.base;
+  PyObject* base = PyDict_New();
+  if (!base) return nullptr;
+  for (const Field& f : s.fields) {
+    if (f.inline_ || f.absent == A_SKIP) continue;
+    PyObject* v = nullptr;
+    switch (f.absent) {
+      case A_EMPTY_STRUCT: {
+        PyObject* e = empty_struct(g->types[f.type].strct);
+        if (!e) { Py_DECREF(base); return nullptr; }
+        Py_INCREF(e);
+        v = e;
+        break;
+      }
+      case A_ZERO_STR: Py_INCREF(g->empty_str); v = g->empty_str; break;
+      case A_ZERO_INT: Py_INCREF(g->zero); v = g->zero; break;
+      case A_ZERO_BOOL: Py_INCREF(Py_False); v = Py_False; break;
+      default: Py_INCREF(Py_None); v = Py_None; break;
+    }
+    int rc = PyDict_SetItem(base, f.jname, v);
+    Py_DECREF(v);
+    if (rc < 0) { Py_DECREF(base); return nullptr; }
+  }
+  s.base = base;
+  return base;
+}
+
+static PyObject* empty_struct(int strct) {
+  Struct& s = g->structs[strct];
+  if (s.empty) return s.empty;
+  if (s.building) {
+    PyErr_SetString(PyExc_RecursionError, "recursive struct type");
+    return nullptr;
+  }
+  s.building = true;
+  PyObject* base = base_of(strct);
+  PyObject* out = base ? PyDict_Copy(base) : nullptr;
+  if (out) {
+    for (int in : s.inlines) {
+      PyObject* e = empty_struct(in);
+      if (!e || PyDict_Update(out, e) < 0) { Py_CLEAR(out); break; }
+    }
+  }
+  s.building = false;
+  s.empty = out;
+  return out;
+}
+
+static int is_empty(PyObject* v, Empty e) {
+  switch (e) {
+    case E_NEVER: return 0;
+    case E_STR: return PyObject_RichCompareBool(v, g->empty_str, Py_EQ);
+    case E_INT: return PyObject_RichCompareBool(v, g->zero, Py_EQ);
+    case E_BOOL: return v == Py_False;
+    case E_LEN: {
+      Py_ssize_t n = PyObject_Length(v);
+      return n < 0 ? -1 : n == 0;
+    }
+    case E_ANY: {
+      if (PyDict_Check(v) || PyList_Check(v) || PyUnicode_Check(v)) {
+        Py_ssize_t n = PyObject_Length(v);
+        if (n < 0) return -1;
+        if (n == 0) return 1;
+      }
+      if (v == Py_False) return 1;
+      return PyObject_RichCompareBool(v, g->zero, Py_EQ);
+    }
+  }
+  return 0;
+}
+
+static PyObject* fallback(PyObject* v, int type) {
+  return PyObject_CallFunctionObjArgs(g->fallback, v, g->types[type].name, nullptr);
+}
+
+static PyObject* marshal_fields(PyObject* d, int strct) {
+  Struct& s = g->structs[strct];
+  PyObject* base = base_of(strct);
+  if (!base) return nullptr;
+  PyObject* out = PyDict_Copy(base);
+  if (!out) return nullptr;
+  for (int in : s.inlines) {
+    PyObject* sub = marshal_struct(d, in);
+    if (!sub) { Py_DECREF(out); return nullptr; }
+    int rc = PyDict_Update(out, sub);
+    Py_DECREF(sub);
+    if (rc < 0) { Py_DECREF(out); return nullptr; }
+  }
+  Py_ssize_t pos = 0;
+  PyObject *k, *v;
+  while (PyDict_Next(d, &pos, &k, &v)) {
+    PyObject* fi = PyDict_GetItemWithError(s.keyed, k);
+    if (!fi) {
+      if (PyErr_Occurred()) { Py_DECREF(out); return nullptr; }
+      continue;
+    }
+    if (v == Py_None) continue;
+    const Field& f = s.fields[PyLong_AsSsize_t(fi)];
+    if (f.omit) {
+      int e = is_empty(v, f.empty);
+      if (e < 0) { Py_DECREF(out); return nullptr; }
+      if (e) {
+        if (PyDict_DelItem(out, k) < 0) {
+          if (!PyErr_ExceptionMatches(PyExc_KeyError)) { Py_DECREF(out); return nullptr; }
+          PyErr_Clear();
+        }
+        continue;
+      }
+    }
+    PyObject* mv = marshal_value(v, f.type);
+    if (!mv) { Py_DECREF(out); return nullptr; }
+    int rc = PyDict_SetItem(out, k, mv);
+    Py_DECREF(mv);
+    if (rc < 0) { Py_DECREF(out); return nullptr; }
+  }
+  return out;
+}
+
+static PyObject* marshal_struct(PyObject* d, int strct) {
+  int truth = PyObject_IsTrue(d);
+  if (truth < 0) return nullptr;
+  if (!truth) {
+    PyObject* e = empty_struct(strct);
+    Py_XINCREF(e);
+    return e;
+  }
+  if (!PyDict_Check(d)) {  // not a JSON object: the Python code decides (and raises)
+    PyObject* name = PyUnicode_FromString(g->structs[strct].name.c_str());
+    if (!name) return nullptr;
+    PyObject* r = PyObject_CallFunctionObjArgs(g->fallback, d, name, nullptr);
+    Py_DECREF(name);
+    return r;
+  }
+  return marshal_fields(d, strct);
+}
+
+static PyObject* marshal_value(PyObject* v, int type) {
+  const Type& t = g->types[type];
+  switch (t.kind) {
+    case K_IDENT:
+      Py_INCREF(v);
+      return v;
+    case K_PTR:
+      if (v == Py_None) Py_RETURN_NONE;
+      return marshal_value(v, t.inner);
+    case K_SLICE: {
+      if (v == Py_None) Py_RETURN_NONE;
+      PyObject* it = PyObject_GetIter(v);
+      if (!it) return nullptr;
+      PyObject* out = PyList_New(0);
+      if (!out) { Py_DECREF(it); return nullptr; }
+      PyObject* x;
+      while ((x = PyIter_Next(it))) {
+        PyObject* mx = marshal_value(x, t.inner);
+        Py_DECREF(x);
+        if (!mx || PyList_Append(out, mx) < 0) {
+          Py_XDECREF(mx);
+          Py_DECREF(it);
+          Py_DECREF(out);
+          return nullptr;
+        }
+        Py_DECREF(mx);
+      }
+      Py_DECREF(it);
+      if (PyErr_Occurred()) { Py_DECREF(out); return nullptr; }
+      return out;
+    }
+    case K_MAP_PLAIN: {
+      if (v == Py_None) Py_RETURN_NONE;
+      if (PyDict_Check(v)) {
+        PyObject* out = PyDict_New();
+        if (out && PyDict_Update(out, v) < 0) Py_CLEAR(out);
+        return out;
+      }
+      return PyObject_CallOneArg((PyObject*)&PyDict_Type, v);
+    }
+    case K_MAP_OF: {
+      if (v == Py_None) Py_RETURN_NONE;
+      if (!PyDict_Check(v)) return fallback(v, type);
+      PyObject* out = PyDict_New();
+      if (!out) return nullptr;
+      Py_ssize_t pos = 0;
+      PyObject *k, *x;
+      while (PyDict_Next(v, &pos, &k, &x)) {
+        PyObject* mx = marshal_value(x, t.inner);
+        if (!mx || PyDict_SetItem(out, k, mx) < 0) {
+          Py_XDECREF(mx);
+          Py_DECREF(out);
+          return nullptr;
+        }
+        Py_DECREF(mx);
+      }
+      return out;
+    }
+    case K_STR:
+      if (PyUnicode_Check(v)) { Py_INCREF(v); return v; }
+      if (v == Py_None) { Py_INCREF(g->empty_str); return g->empty_str; }
+      Py_INCREF(v);
+      return v;
+    case K_BOOL: {
+      int b = PyObject_IsTrue(v);
+      if (b < 0) return nullptr;
+      return PyBool_FromLong(b);
+    }
+    case K_TIME: {
+      int b = PyObject_IsTrue(v);
+      if (b < 0) return nullptr;
+      if (!b) Py_RETURN_NONE;
+      Py_INCREF(v);
+      return v;
+    }
+    case K_STRUCT: {
+      int b = PyObject_IsTrue(v);
+      if (b < 0) return nullptr;
+      if (!b) {
+        PyObject* e = empty_struct(t.strct);
+        Py_XINCREF(e);
+        return e;
+      }
+      return marshal_struct(v, t.strct);
+    }
+    case K_FALLBACK:
+      return fallback(v, type);
+  }
+  Py_INCREF(v);
+  return v;
+}
+
+}  // namespace m2kschema
+
+using namespace m2kschema;
+
+// schema_init(structs: {name: [(jname, ftype, omit)]}, fallback) -> None
+extern "C" PyObject* m2k_schema_init(PyObject* structs, PyObject* fb) {
+  if (!PyDict_Check(structs)) {
+    PyErr_SetString(PyExc_TypeError, "structs must be a dict");
+    return nullptr;
+  }
+  if (g == nullptr) g = new Schema();
+  if (!g->structs.empty()) Py_RETURN_NONE;  // already compiled (the table never changes)
+  g->zero = PyLong_FromLong(0);
+  g->empty_str = PyUnicode_FromString("");
+  Py_INCREF(fb);
+  g->fallback = fb;
+  Py_ssize_t pos = 0;
+  PyObject *name, *fields;
+  while (PyDict_Next(structs, &pos, &name, &fields)) {
+    Struct s;
+    s.name = PyUnicode_AsUTF8(name);
+    g->struct_index[s.name] = (int)g->structs.size();
+    g->structs.push_back(std::move(s));
+  }
+  pos = 0;
+  int ix = 0;
+  while (PyDict_Next(structs, &pos, &name, &fields)) {
+    Struct& s = g->structs[ix++];
+    s.keyed = PyDict_New();
+    PyObject* seq = PySequence_Fast(fields, "fields must be a sequence");
+    if (!seq) return nullptr;
+    Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      PyObject* item = PySequence_Fast_GET_ITEM(seq, i);
+      PyObject *jn, *ft, *om;
+      if (!PyArg_ParseTuple(item, "UUO", &jn, &ft, &om)) { Py_DECREF(seq); return nullptr; }
+      std::string jname = PyUnicode_AsUTF8(jn), ftype = PyUnicode_AsUTF8(ft);
+      bool omit = PyObject_IsTrue(om) == 1;
+      Field f;
+      Py_INCREF(jn);
+      f.jname = jn;
+      f.omit = omit;
+      f.inline_ = jname == "inline";
+      f.type = compile_type(ftype);
+      f.empty = omit ? empty_kind(ftype) : E_NEVER;
+      f.absent = f.inline_ ? A_SKIP : absent_kind(ftype, omit);
+      if (f.inline_) {
+        auto si = g->struct_index.find(ftype);
+        if (si == g->struct_index.end()) {
+          PyErr_Format(PyExc_ValueError, "inline type %s is not a struct", ftype.c_str());
+          Py_DECREF(seq);
+          return nullptr;
+        }
+        s.inlines.push_back(si->second);
+      } else {
+        PyObject* idx = PyLong_FromSsize_t((Py_ssize_t)s.fields.size());
+        PyDict_SetItem(s.keyed, jn, idx);
+        Py_DECREF(idx);
+      }
+      s.fields.push_back(f);
+    }
+    Py_DECREF(seq);
+  }
+  Py_RETURN_NONE;
+}
+
+// schema_marshal(obj, type name) -> marshalled dict tree
+extern "C" PyObject* m2k_schema_marshal(PyObject* obj, PyObject* type_name) {
+  if (g == nullptr || g->structs.empty()) {
+    PyErr_SetString(PyExc_RuntimeError, "schema_init was not called");
+    return nullptr;
+  }
+  const char* tn = PyUnicode_AsUTF8(type_name);
+  if (!tn) return nullptr;
+  auto it = g->struct_index.find(tn);
+  if (it == g->struct_index.end()) {
+    PyErr_Format(PyExc_KeyError, "%s", tn);
+    return nullptr;
+  }
+  return marshal_struct(obj, it->second);
+}

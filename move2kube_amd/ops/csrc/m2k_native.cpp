@@ -895,6 +895,21 @@ static py::object yaml_load(py::object text, int mode, bool multi, py::object re
   return py::reinterpret_steal<py::object>(r);
 }
 
+extern "C" PyObject* m2k_schema_init(PyObject* structs, PyObject* fallback);
+extern "C" PyObject* m2k_schema_marshal(PyObject* obj, PyObject* type_name);
+
+static py::object schema_init(py::object structs, py::object fallback) {
+  PyObject* r = m2k_schema_init(structs.ptr(), fallback.ptr());
+  if (!r) throw py::error_already_set();
+  return py::reinterpret_steal<py::object>(r);
+}
+
+static py::object schema_marshal(py::object obj, py::object type_name) {
+  PyObject* r = m2k_schema_marshal(obj.ptr(), type_name.ptr());
+  if (!r) throw py::error_already_set();
+  return py::reinterpret_steal<py::object>(r);
+}
+
 PYBIND11_MODULE(_m2k_native, m) {
   m.doc() = "move2kube_amd native runtime (walk, sniff, spawn pool, hashes, edit distance)";
   m.def("walk", &walk, py::arg("root"));
@@ -914,6 +929,8 @@ PYBIND11_MODULE(_m2k_native, m) {
         py::arg("style_fn"), py::arg("sort_fn"));
   m.def("yaml_load", &yaml_load, py::arg("text"), py::arg("mode"), py::arg("multi"), py::arg("resolve_number"),
         py::arg("unsupported"));
+  m.def("schema_init", &schema_init, py::arg("structs"), py::arg("fallback"));
+  m.def("schema_marshal", &schema_marshal, py::arg("obj"), py::arg("type_name"));
   m.def("run_commands", &run_commands, py::arg("argvs"), py::arg("cwds"), py::arg("parallel") = 8,
         py::arg("timeout_s") = 0.0);
 }
