@@ -28,7 +28,8 @@ class Collector:
 
 class CommandError(RuntimeError):
     def __init__(self, argv, code, output=b""):
-        super().__init__("exit status %d" % code if code >= 0 else "signal: %d" % -code)
+        from ..utils.common import go_exit_status
+        super().__init__(go_exit_status(code))
         self.argv = argv
         self.code = code
         self.output = output
@@ -39,18 +40,20 @@ _SERIAL_CLIS = {"cf": threading.Lock()}
 
 def run(argv, combined=False, timeout=300):
     """Run a command; stdout bytes (stdout+stderr with ``combined``). Raises
-    :class:`CommandError` on a non-zero exit and FileNotFoundError if missing.
+    :class:`CommandError` on a non-zero exit and FileNotFoundError if missing
+    (worded like Go's ``exec: "cf": executable file not found in $PATH``).
 
     Collectors run concurrently, but two ``cf`` commands never do: the cf
     CLI rewrites ``~/.cf/config.json`` when it refreshes its token."""
+    from ..utils.common import run_command
     lock = _SERIAL_CLIS.get(os.path.basename(argv[0])) if argv else None
+    kw = dict(stdout=subprocess.PIPE, stderr=subprocess.STDOUT if combined else subprocess.PIPE,
+              stdin=subprocess.DEVNULL, timeout=timeout)
     if lock is not None:
         with lock:
-            p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT if combined else subprocess.PIPE,
-                               stdin=subprocess.DEVNULL, timeout=timeout)
+            p = run_command(argv, **kw)
     else:
-        p = subprocess.run(argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT if combined else subprocess.PIPE,
-                           stdin=subprocess.DEVNULL, timeout=timeout)
+        p = run_command(argv, **kw)
     if p.returncode != 0:
         raise CommandError(argv, p.returncode, p.stdout)
     return p.stdout

@@ -289,8 +289,8 @@ def parallel_map(fn, items, workers=None):
 
 
 def _run(cmd, timeout=600):
-    return subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
-                          timeout=timeout)
+    return common.run_command(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                              timeout=timeout)
 
 
 class ContainerRuntimeProvider:
@@ -417,7 +417,9 @@ class PackProvider:
             except (OSError, subprocess.TimeoutExpired) as e:
                 log.warning("Error while getting supported buildpacks for builder %s : %s", b, e)
                 continue
-            if p.returncode != 0:
+            if p.returncode != 0:  # cmd.Output() returns an *ExitError (packprovider.go:131-136)
+                log.warning("Error while getting supported buildpacks for builder %s : %s", b,
+                            common.go_exit_status(p.returncode))
                 continue
             for m in rx.findall(p.stdout.decode("utf-8", "replace")):
                 out.setdefault(b, []).append(m.split()[-1])

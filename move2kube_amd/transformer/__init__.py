@@ -321,7 +321,8 @@ class K8sTransformer(Transformer):
                 return False
             if rc != 0:
                 out.seek(0)
-                log.warning("Error during operator creation : exit status %d, %s", rc, out.read().decode("utf-8", "replace"))
+                log.warning("Error during operator creation : %s, %s", common.go_exit_status(rc),
+                            out.read().decode("utf-8", "replace"))
                 return False
             return True
         finally:

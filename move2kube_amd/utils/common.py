@@ -397,6 +397,55 @@ def unique_strings(xs):
     return out
 
 
+class GoExecNotFoundError(FileNotFoundError):
+    """A command that could not be started, worded as Go's ``os/exec`` does:
+    ``exec: "cf": executable file not found in $PATH`` for a name looked up on
+    PATH, ``fork/exec /x/cf: no such file or directory`` for a path."""
+
+    def __str__(self):
+        return self.args[1] if len(self.args) > 1 else super().__str__()
+
+
+def go_exec_error(e, name):
+    """``e`` (a FileNotFoundError from starting ``name``) with Go's message."""
+    if "/" in name:
+        text = "fork/exec %s: no such file or directory" % name
+    else:
+        text = "exec: %s: executable file not found in $PATH" % log.go_quote(name)
+    err = GoExecNotFoundError(e.errno, text)
+    err.filename = name
+    return err
+
+
+_GO_SIGNALS = ("", "hangup", "interrupt", "quit", "illegal instruction", "trace/breakpoint trap", "aborted",
+               "bus error", "floating point exception", "killed", "user defined signal 1", "segmentation fault",
+               "user defined signal 2", "broken pipe", "alarm clock", "terminated", "stack fault", "child exited",
+               "continued", "stopped (signal)", "stopped", "stopped (tty input)", "stopped (tty output)",
+               "urgent I/O condition", "CPU time limit exceeded", "file size limit exceeded",
+               "virtual timer expired", "profiling timer expired", "window changed", "I/O possible",
+               "power failure", "bad system call")
+
+
+def go_exit_status(returncode):
+    """Go's ``*exec.ExitError`` text for a subprocess return code
+    (``exit status 2``, ``signal: killed``; linux/amd64 signal names)."""
+    if returncode >= 0:
+        return "exit status %d" % returncode
+    sig = -returncode
+    return "signal: " + (_GO_SIGNALS[sig] if 0 < sig < len(_GO_SIGNALS) else "signal %d" % sig)
+
+
+def run_command(argv, **kw):
+    """``subprocess.run`` whose missing-executable error reads like Go's."""
+    import subprocess
+    try:
+        return subprocess.run(argv, **kw)
+    except FileNotFoundError as e:
+        if e.filename in (argv[0], os.fsencode(argv[0]) if isinstance(argv[0], str) else argv[0]):
+            raise go_exec_error(e, os.fsdecode(argv[0])) from None
+        raise
+
+
 def go_rel(base, target):
     """Go ``filepath.Rel`` (lexical; error if one is absolute and the other is not)."""
     if os.path.isabs(base) != os.path.isabs(target):

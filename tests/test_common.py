@@ -191,3 +191,20 @@ def test_cgroup_cpu_limit(tmp_path):
     (v1 / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
     assert _cgroup_cpu_limit(str(v1)) is None
     assert _cgroup_cpu_limit(str(tmp_path / "none")) is None
+
+
+def test_exec_errors_read_like_go(tmp_path):
+    """os/exec start failures and *ExitError texts (collectors, CNB providers,
+    operator-sdk) as the reference prints them."""
+    import pytest as _pytest
+    from move2kube_amd.utils import common as c
+    with _pytest.raises(FileNotFoundError) as ei:
+        c.run_command(["m2k-no-such-tool", "x"])
+    assert str(ei.value) == 'exec: "m2k-no-such-tool": executable file not found in $PATH'
+    missing = str(tmp_path / "nope")
+    with _pytest.raises(FileNotFoundError) as ei:
+        c.run_command([missing])
+    assert str(ei.value) == "fork/exec %s: no such file or directory" % missing
+    assert c.go_exit_status(0) == "exit status 0" and c.go_exit_status(3) == "exit status 3"
+    assert c.go_exit_status(-9) == "signal: killed" and c.go_exit_status(-15) == "signal: terminated"
+    assert c.go_exit_status(-11) == "signal: segmentation fault" and c.go_exit_status(-40) == "signal: signal 40"

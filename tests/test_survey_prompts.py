@@ -112,12 +112,14 @@ class Pty:
 
     def _settle(self):
         """Wait until the drained output stops growing (the prompt has returned)."""
+        import select
         import time
         n, stable = -1, 0
         while stable < 3:
             time.sleep(0.02)
+            pending = select.select([self.master], [], [], 0)[0]
             m = sum(len(x) for x in self.out)
-            stable = stable + 1 if m == n else 0
+            stable = stable + 1 if (m == n and not pending) else 0
             n = m
 
     def screen(self):
@@ -126,15 +128,20 @@ class Pty:
         s.feed(b"".join(self.out).decode("utf-8", "replace"))
         return s
 
-    def wait_for(self, text, timeout=10.0):
-        """The screen once ``text`` appears on it (a prompt thread renders)."""
+    def wait_for(self, text, timeout=30.0):
+        """The screen once ``text`` appears on it (a prompt thread renders)
+        and the output has settled."""
         import time
         end = time.time() + timeout
         while True:
             s = Screen()
             s.feed(b"".join(self.out).decode("utf-8", "replace"))
-            if text in s.text() or time.time() > end:
+            if text in s.text():
+                self._settle()
+                s = Screen()
+                s.feed(b"".join(self.out).decode("utf-8", "replace"))
                 return s
+            assert time.time() < end, "timed out waiting for %r; screen:\n%s" % (text, s.text())
             time.sleep(0.02)
 
     def raw_output(self):
@@ -142,9 +149,12 @@ class Pty:
         return b"".join(self.out).decode("utf-8", "replace")
 
     def close(self):
+        # slave side first: the drain thread's read then fails and it exits
+        # before the master's fd number can be reused by the next test's pty
         self.fin.close()
         self.fout.close()
         os.close(self.slave)
+        self._t.join(10)
         os.close(self.master)
 
 
