@@ -13,6 +13,7 @@ import sys
 from .. import assets
 from ..models import plan as plantypes
 from ..utils import fsindex, log, yamlio
+from ..utils.common import go_path_error
 from ..utils.constants import (APP_NAME_SHORT, DEFAULT_DIRECTORY_PERMISSION, DEFAULT_PLAN_FILE, DEFAULT_PROJECT_NAME,
                                QA_CACHE_FILE, settings)
 from ..utils.lazyre import LazyModule
@@ -66,13 +67,13 @@ def create_output_directory_and_cache_file(out):
     try:
         os.makedirs(out, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
     except OSError as e:
-        log.fatal("Failed to create the output directory at path %s Error: %r", out, str(e))
+        log.fatal("Failed to create the output directory at path %s Error: %r", out, go_path_error(e, "mkdir"))
     cache = os.path.join(out, QA_CACHE_FILE)
     log.debug("Creating the cache file at path %s", cache)
     try:
         qaengine.set_write_cache(cache)
     except OSError as e:
-        log.warning("Unable to write the cache file to path %r Error: %r", cache, str(e))
+        log.warning("Unable to write the cache file to path %r Error: %r", cache, go_path_error(e, "open"))
 
 
 def translate_handler(a):
@@ -146,7 +147,7 @@ def plan_handler(a):
             os.makedirs(d, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
         plantypes.write_plan(planfile, p)
     except OSError as e:
-        log.error("Unable to write plan file (%s) : %s", planfile, e)
+        log.error("Unable to write plan file (%s) : %s", planfile, go_path_error(e, "open"))
         return
     log.info("Plan can be found at [%s].", planfile)
 
@@ -256,7 +257,7 @@ def main(argv=None):
     try:
         assets.setup()
     except OSError as e:
-        log.error("Unable to create the assets directory. Error: %r", str(e))
+        log.error("Unable to create the assets directory. Error: %r", go_path_error(e, "mkdir"))
         return 1
     try:
         with yamlio.parse_cache():  # one command = one parse of each YAML document

@@ -110,7 +110,8 @@ def collect(input_path, output_path, annotations=()):
     try:
         os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
     except OSError as e:
-        log.fatal("Unable to create output directory at path %r Error: %r", output_path, str(e))
+        from ..utils.common import go_path_error
+        log.fatal("Unable to create output directory at path %r Error: %r", output_path, go_path_error(e, "mkdir"))
     log.info("Begin collection")
     selected = [c for c in get_collectors()
                 if not annotations or has_overlap(annotations, c.get_annotations())]

@@ -50,7 +50,7 @@ class CfAppsCollector(Collector):
         try:
             os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
         except OSError as e:
-            log.error("Unable to create outputPath %s : %s", output_path, e)
+            log.error("Unable to create outputPath %s : %s", output_path, common.go_path_error(e, "mkdir"))
         inst = collection.CfInstanceApps()
         file_name = "instanceapps_"
         log.debug("Detected %d apps", len(apps))

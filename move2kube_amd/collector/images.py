@@ -132,4 +132,4 @@ class ImagesCollector(Collector):
             try:
                 common.write_yaml(path, info)
             except OSError as e:
-                log.error("Unable to write file %s : %s", path, e)
+                log.error("Unable to write file %s : %s", path, common.go_path_error(e, "open"))

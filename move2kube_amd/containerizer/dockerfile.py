@@ -79,7 +79,8 @@ class DockerfileContainerizer(Containerizer):
         try:
             template = common.read_text(tpl_path)
         except OSError as e:
-            log.error("Unable to read the Dockerfile template at path %r Error: %r", tpl_path, str(e))
+            log.error("Unable to read the Dockerfile template at path %r Error: %r", tpl_path,
+                      common.go_path_error(e, "open"))
             raise ContainerizerError(str(e)) from e
         srcs = service.source_artifacts.get(plantypes.SOURCE_DIRECTORY_ARTIFACT) or []
         if not srcs:
@@ -128,6 +129,6 @@ class DockerfileContainerizer(Containerizer):
             try:
                 container.add_file(common.go_join(rel, name), common.read_text(f))
             except OSError as e:
-                log.error("Failed to read the file at path %r Error: %r", f, str(e))
+                log.error("Failed to read the file at path %r Error: %r", f, common.go_path_error(e, "open"))
                 raise ContainerizerError(str(e)) from e
         return container

@@ -69,7 +69,7 @@ class S2IContainerizer(DockerfileContainerizer):
             try:
                 tpl = common.read_text(f)
             except OSError as e:
-                log.error("Skipping path %r . Failed to read the template. Error: %r", f, str(e))
+                log.error("Skipping path %r . Failed to read the template. Error: %r", f, common.go_path_error(e, "open"))
                 continue
             try:
                 contents = common.get_string_from_template(tpl, m)

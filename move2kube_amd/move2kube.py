@@ -251,7 +251,8 @@ def _emit(p, ir, outpath, qadisablecli):
         try:
             remover = _remove_output(outpath)
         except OSError as e:
-            log.error("Failed to remove the existing file/directory at the output path %r Error: %r", outpath, str(e))
+            log.error("Failed to remove the existing file/directory at the output path %r Error: %r", outpath,
+                      common.go_path_error(e, "unlinkat"))
             log.error("Anything in the output path will get overwritten.")
     try:
         _emit_artifacts(p, ir, outpath, qadisablecli)

@@ -132,7 +132,7 @@ class Any2KubeTranslator(Translator):
             try:
                 text = common.read_text(fp)
             except OSError as e:
-                log.warning("Failed to open the .m2kignore file at path %r Error: %r", fp, str(e))
+                log.warning("Failed to open the .m2kignore file at path %r Error: %r", fp, common.go_path_error(e, "open"))
                 continue
             base = os.path.dirname(fp)
             for raw in text.splitlines():

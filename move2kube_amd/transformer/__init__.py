@@ -42,7 +42,7 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
     try:
         _mkdir(cpath)
     except OSError as e:
-        log.error("Unable to create directory %s : %s", cpath, e)
+        log.error("Unable to create directory %s : %s", cpath, common.go_path_error(e, "mkdir"))
     log.debug("Total number of containers : %d", len(containers))
     buildscripts, dockerimages, manualimages = [], [], []
     batch = []
@@ -64,7 +64,7 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
                 try:
                     _mkdir(d)
                 except OSError as e:
-                    log.error("Unable to create directory %s : %s", d, e)
+                    log.error("Unable to create directory %s : %s", d, common.go_path_error(e, "mkdir"))
                     continue
                 made.add(d)
             mode = DEFAULT_FILE_PERMISSION
@@ -120,7 +120,7 @@ def write_transformed_objects(path, objs):
     try:
         _mkdir(path)
     except OSError as e:
-        log.error("Unable to create directory %s : %s", path, e)
+        log.error("Unable to create directory %s : %s", path, common.go_path_error(e, "mkdir"))
         raise
     batch, kinds = [], []
     for obj in objs:
@@ -428,5 +428,5 @@ class CICDTransformer(Transformer):
         try:
             _mkdir(p)
         except OSError as e:
-            log.fatal("Failed to create the CI/CD directory at path %r. Error: %r", p, str(e))
+            log.fatal("Failed to create the CI/CD directory at path %r. Error: %r", p, common.go_path_error(e, "mkdir"))
         write_transformed_objects(p, self.cached_objs)

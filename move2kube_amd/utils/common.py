@@ -397,6 +397,28 @@ def unique_strings(xs):
     return out
 
 
+def go_errno_text(errno_):
+    """Go's ``syscall.Errno`` text (``no such file or directory``)."""
+    msg = os.strerror(errno_) if errno_ else ""
+    return msg[:1].lower() + msg[1:]
+
+
+def go_path_error(e, op):
+    """An OSError as Go's ``*os.PathError`` prints it: ``<op> <path>: <errno
+    text>`` (``mkdir /out: permission denied``, ``open /x/plan: not a
+    directory``).  ``os.MkdirAll`` over an existing non-directory reports
+    ENOTDIR where Python's ``makedirs`` says EEXIST.  Errors without a path
+    keep Python's text."""
+    path = getattr(e, "filename", None)
+    if path is None or not getattr(e, "errno", None):
+        return str(e)
+    import errno as _errno
+    code = e.errno
+    if op == "mkdir" and code == _errno.EEXIST:
+        code = _errno.ENOTDIR
+    return "%s %s: %s" % (op, os.fsdecode(path), go_errno_text(code))
+
+
 class GoExecNotFoundError(FileNotFoundError):
     """A command that could not be started, worded as Go's ``os/exec`` does:
     ``exec: "cf": executable file not found in $PATH`` for a name looked up on

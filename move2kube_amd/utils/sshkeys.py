@@ -12,7 +12,7 @@ import shutil
 import subprocess
 import tempfile
 
-from . import log
+from . import common, log
 from .knownhosts import KnownHostsError, parse_known_hosts
 
 DOMAIN_TO_PUBLIC_KEYS = {
@@ -76,7 +76,7 @@ def _load_ssh_keys_of_current_user():
     try:
         names = sorted(os.listdir(d))
     except OSError as e:
-        log.error("Failed to read the ssh directory at path %r Error: %r", d, str(e))
+        log.error("Failed to read the ssh directory at path %r Error: %r", d, common.go_path_error(e, "open"))
         return
     if not names:
         log.warning("No key files where found in %s", d)

@@ -208,3 +208,23 @@ def test_exec_errors_read_like_go(tmp_path):
     assert c.go_exit_status(0) == "exit status 0" and c.go_exit_status(3) == "exit status 3"
     assert c.go_exit_status(-9) == "signal: killed" and c.go_exit_status(-15) == "signal: terminated"
     assert c.go_exit_status(-11) == "signal: segmentation fault" and c.go_exit_status(-40) == "signal: signal 40"
+
+
+def test_os_errors_read_like_go_path_errors(tmp_path):
+    import errno
+    import os
+    from move2kube_amd.utils import common as c
+    f = tmp_path / "file"
+    f.write_text("x")
+    try:
+        os.makedirs(str(f), exist_ok=True)
+    except OSError as e:
+        # os.MkdirAll over an existing regular file: ENOTDIR
+        assert c.go_path_error(e, "mkdir") == "mkdir %s: not a directory" % f
+    try:
+        open(str(f / "x"))
+    except OSError as e:
+        assert c.go_path_error(e, "open") == "open %s: not a directory" % (f / "x")
+    e = PermissionError(errno.EACCES, "Permission denied", "/out")
+    assert c.go_path_error(e, "mkdir") == "mkdir /out: permission denied"
+    assert c.go_path_error(OSError("no path"), "open") == "no path"
