@@ -156,12 +156,26 @@ def write_text(path, text, mode=DEFAULT_FILE_PERMISSION):
 
 
 def yaml_attr_present(path, attr):
+    """``YamlAttrPresent`` (utils.go:122-140): decode into a
+    ``map[string]interface{}`` and look the attribute up."""
     try:
-        data = yamlio.load(read_text(path))
-    except (OSError, yamlio.YAMLError) as e:
-        log.warning("Error in reading/unmarshalling yaml file %s: %s. Skipping", path, e)
+        text = read_text(path)
+    except OSError as e:
+        log.warning("Error in reading yaml file %s: %s. Skipping", path, go_path_error(e, "open"))
+        return False, None
+    try:
+        data = yamlio.load(text)
+    except yamlio.YAMLError as e:
+        log.warning("Error in unmarshalling yaml file %s: %s. Skipping", path, e)
+        return False, None
+    if data is not None and not isinstance(data, dict):
+        tag = "!!seq" if isinstance(data, list) else "!!bool" if isinstance(data, bool) else \
+            "!!int" if isinstance(data, int) else "!!float" if isinstance(data, float) else "!!str"
+        log.warning("Error in unmarshalling yaml file %s: %s. Skipping", path,
+                    "yaml: unmarshal errors:\n  line 1: cannot unmarshal %s into map[string]interface {}" % tag)
         return False, None
     if isinstance(data, dict) and attr in data:
+        log.debug("%s file has %s attribute", path, attr)
         return True, data[attr]
     return False, None
 
