@@ -490,8 +490,33 @@ class Parser {
     return none();
   }
 
+  // go-yaml v3 refuses a mapping whose keys repeat (decode.go: same node
+  // Kind and Value, i.e. the decoded text of a quoted key or the source text
+  // of a plain one).  Such a document is left to the PyYAML path, which
+  // reports the keys with their lines (yamlio.py: _duplicate_keys).
+  static std::string key_value(PyObject* key, const char* raw, size_t rawlen) {
+    if (PyUnicode_Check(key)) {
+      Py_ssize_t n = 0;
+      const char* u = PyUnicode_AsUTF8AndSize(key, &n);
+      if (u) return std::string(u, (size_t)n);
+      PyErr_Clear();
+    }
+    while (rawlen > 0 && raw[rawlen - 1] == ' ') rawlen--;
+    return std::string(raw, rawlen);
+  }
+
+  static void check_unique(PyObject* d, PyObject* key, std::vector<std::string>& seen, std::string v) {
+    int has = PyDict_Contains(d, key);
+    if (has < 0) throw PyErrorSet();
+    if (has) throw Unsupported();
+    for (const std::string& s : seen)
+      if (s == v) throw Unsupported();
+    seen.push_back(std::move(v));
+  }
+
   PyObject* block_map(int col) {
     Ref d(PyDict_New());
+    std::vector<std::string> seen;
     for (;;) {
       const Line& ln = L_[li_];
       int kend, colon;
@@ -501,6 +526,7 @@ class Parser {
       if (!qk) check_plain_start(ln, col, false);
       Ref key(qk ? str(qkey.data(), qkey.size()) : plain(ln.s + col, (size_t)(kend - col)));
       if (PyObject_Hash(key.get()) == -1) throw PyErrorSet();
+      check_unique(d.get(), key.get(), seen, key_value(key.get(), ln.s + col, (size_t)(kend - col)));
       int p = colon + 1;
       while (p < ln.len && ln.s[p] == ' ') p++;
       Ref val;
@@ -638,6 +664,7 @@ class Parser {
     const bool is_seq = ln.s[pos] == '[';
     const char close = is_seq ? ']' : '}';
     Ref coll(is_seq ? PyList_New(0) : PyDict_New());
+    std::vector<std::string> seen;
     int p = pos + 1;
     while (p < ln.len && ln.s[p] == ' ') p++;
     if (p < ln.len && ln.s[p] == close) {
@@ -653,6 +680,7 @@ class Parser {
         key = Ref(flow_scalar(ln, p, p, true));
         if (p - kstart > kMaxSimpleKey) throw Unsupported();
         if (PyObject_Hash(key.get()) == -1) throw PyErrorSet();
+        check_unique(coll.get(), key.get(), seen, key_value(key.get(), ln.s + kstart, (size_t)(p - kstart)));
         while (p < ln.len && ln.s[p] == ' ') p++;
         if (!(p < ln.len && ln.s[p] == ':' && p + 1 < ln.len && ln.s[p + 1] == ' ')) throw Unsupported();
         p += 2;

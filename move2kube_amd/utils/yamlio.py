@@ -787,7 +787,8 @@ def _memoized(kind, text, parse):
         raise val.with_traceback(None)
     # (self-containing anchors were refused by _check_aliasing; a document too
     # deep to copy raises RecursionError and its caller skips the file)
-    return _tree_copy(val)
+    docs, dups = val
+    return _tree_copy(docs), dups
 
 
 _MISS = object()
@@ -937,7 +938,77 @@ def _too_deep(text, limit=MAX_DEPTH):
     return False
 
 
+def _duplicate_keys(root):
+    """go-yaml v3 ``decoder.mapping`` duplicate-key errors of one composed
+    document, in its decode order: within a mapping every later key with the
+    same node kind and value as an earlier one (``line 5: mapping key "a"
+    already defined at line 2``); a mapping that has such keys is not
+    descended into.  Nodes shared through aliases are looked at once."""
+    import yaml
+    out = []
+    seen = set()
+
+    def ident(node):
+        return (type(node).__name__, node.value if isinstance(node, yaml.ScalarNode) else "")
+
+    stack = [root]
+    while stack:
+        node = stack.pop()
+        if id(node) in seen:
+            continue
+        seen.add(id(node))
+        if isinstance(node, yaml.MappingNode):
+            pairs = node.value
+            first = {}
+            errs = []
+            for j, (k, _v) in enumerate(pairs):
+                key = ident(k)
+                for i, ki in first.get(key, ()):
+                    errs.append((i, j, "line %d: mapping key %s already defined at line %d"
+                                 % (k.start_mark.line + 1, _go_quote(k.value if key[1] else ""),
+                                    ki.start_mark.line + 1)))
+                first.setdefault(key, []).append((j, k))
+            if errs:
+                out.extend(e for _i, _j, e in sorted(errs, key=lambda x: (x[0], x[1])))
+                continue
+            stack.extend(v for _k, v in reversed(pairs))
+        elif isinstance(node, yaml.SequenceNode):
+            stack.extend(reversed(node.value))
+    return out
+
+
+def _go_quote(s):
+    from .log import go_quote
+    return go_quote(s)
+
+
+def _pyyaml_load(loader_cls, text, multi):
+    """``yaml.load`` / ``yaml.load_all`` with the duplicate-key scan of each
+    composed document before it is constructed."""
+    loader = loader_cls(text)
+    dups = []
+    try:
+        if multi:
+            docs = []
+            while loader.check_node():
+                node = loader.get_node()
+                dups.extend(_duplicate_keys(node))
+                docs.append(loader.construct_document(node))
+        else:
+            node = loader.get_single_node()
+            docs = None
+            if node is not None:
+                dups = _duplicate_keys(node)
+                docs = loader.construct_document(node)
+    finally:
+        loader.dispose()
+    return docs, dups
+
+
 def _parse(text, mode, multi):
+    """-> (document(s), go-yaml v3 duplicate-key errors).  Only the v3 entry
+    points raise on the second part: go-yaml v2 (compose files, and Kubernetes
+    objects through sigs.k8s.io/yaml) keeps the last value of a repeated key."""
     nl = _native_loader()
     if nl and isinstance(text, str):
         try:
@@ -946,21 +1017,18 @@ def _parse(text, mode, multi):
             r = _UNSUPPORTED
         except ValueError as e:   # nesting past go-yaml's limit (yaml_parse.cpp TooDeep)
             raise _lz().yaml.YAMLError(str(e)) from None
-        if r is not _UNSUPPORTED:
-            return r
+        if r is not _UNSUPPORTED:   # (it never decodes a document with repeated keys)
+            return r, ()
     if isinstance(text, str) and _too_deep(text):
         raise _lz().yaml.YAMLError("yaml: exceeded max depth of %d" % MAX_DEPTH)
     lz = _lz()
     loader = (lz.typed, lz.v2, lz.raw)[mode]
     try:
-        if multi:
-            docs = list(lz.yaml.load_all(text, Loader=loader))
-        else:
-            docs = lz.yaml.load(text, Loader=loader)
+        docs, dups = _pyyaml_load(loader, text, multi)
         if "*" in text:
             for d in (docs if multi else (docs,)):
                 _check_aliasing(d, lz.yaml.YAMLError)
-        return docs
+        return docs, tuple(dups)
     except UnicodeError as e:
         # bytes that are not UTF-8 (kept as surrogates by read_text): a parse
         # error of this document, as go-yaml reports "invalid leading UTF-8
@@ -968,13 +1036,26 @@ def _parse(text, mode, multi):
         raise lz.yaml.YAMLError("invalid UTF-8 in document: %s" % e) from None
 
 
+def _v3(result):
+    """The decoded document(s) of a go-yaml v3 ``Unmarshal``: repeated keys
+    fail the whole decode (``*yaml.TypeError``)."""
+    docs, dups = result
+    if dups:
+        raise _lz().yaml.YAMLError("yaml: unmarshal errors:\n  " + "\n  ".join(dups))
+    return docs
+
+
+def _v2(result):
+    return result[0]
+
+
 def load(text):
     """Decode like go-yaml v3 into ``interface{}``."""
-    return _memoized("typed", text, lambda t: _parse(t, _TYPED, False))
+    return _v3(_memoized("typed", text, lambda t: _parse(t, _TYPED, False)))
 
 
 def load_all(text):
-    return _memoized("typed*", text, lambda t: _parse(t, _TYPED, True))
+    return _v3(_memoized("typed*", text, lambda t: _parse(t, _TYPED, True)))
 
 
 _V2_ONLY_WORDS = _lazy_re(r"\b(?:[yYnN]|yes|Yes|YES|no|No|NO|on|On|ON|off|Off|OFF)\b")
@@ -985,16 +1066,16 @@ def load_v2(text):
     decoders differ only in the YAML 1.1 bool words, so a document that does
     not contain one anywhere shares the v3 parse (and its memo entry)."""
     if isinstance(text, str) and not _V2_ONLY_WORDS.search(text):
-        return load(text)
-    return _memoized("typed-v2", text, lambda t: _parse(t, _V2, False))
+        return _v2(_memoized("typed", text, lambda t: _parse(t, _TYPED, False)))
+    return _v2(_memoized("typed-v2", text, lambda t: _parse(t, _V2, False)))
 
 
 def load_all_v2(text):
     if isinstance(text, str) and not _V2_ONLY_WORDS.search(text):
-        return load_all(text)
-    return _memoized("typed-v2*", text, lambda t: _parse(t, _V2, True))
+        return _v2(_memoized("typed*", text, lambda t: _parse(t, _TYPED, True)))
+    return _v2(_memoized("typed-v2*", text, lambda t: _parse(t, _V2, True)))
 
 
 def load_raw(text):
     """Decode keeping scalars as raw strings (for typed struct decoding)."""
-    return _memoized("raw", text, lambda t: _parse(t, _RAW, False))
+    return _v3(_memoized("raw", text, lambda t: _parse(t, _RAW, False)))
