@@ -78,6 +78,31 @@ DRIVER = textwrap.dedent(r'''
             m.yaml_load(text[:i], mode, True, yamlio.go_resolve_number, unsup)
             m.yaml_load(text[:i], mode, False, yamlio.go_resolve_number, unsup)
     assert m.yaml_load(text, 0, True, yamlio.go_resolve_number, unsup)[0] == doc
+    # repeated keys are left to PyYAML
+    assert m.yaml_load("a: 1\nb: {c: 1, c: 2}\n", 0, False, yamlio.go_resolve_number, unsup) is unsup
+    # the struct marshaller (k8s_marshal.cpp) against its Python specification
+    from move2kube_amd.k8s import schema
+    m.schema_init(schema._STRUCTS, schema._marshal_value)
+    objs = [({"kind": "Deployment", "apiVersion": "apps/v1", "metadata": {"name": "d", "labels": {"a": "b"}},
+              "spec": {"replicas": 2, "template": {"spec": {"containers": [{"name": "c", "image": "i",
+              "ports": [{"containerPort": 80}], "env": [{"name": "X", "value": ""}]}]}}}}, "Deployment"),
+            ({"kind": "Secret", "data": {"k": "dg=="}, "type": ""}, "Secret"),
+            ({"spec": [1, 2]}, "Service"), ({}, "Route"), ([1], "Pod")]
+    def marshal():
+        for _ in range(100):
+            for o, t in objs:
+                try:
+                    got = m.schema_marshal(o, t)
+                except AttributeError:
+                    got = "err"
+                try:
+                    want = schema._marshal_struct(o, t)
+                except AttributeError:
+                    want = "err"
+                assert got == want, (t, got, want)
+    ts = [threading.Thread(target=marshal) for _ in range(4)]
+    for t in ts: t.start()
+    for t in ts: t.join()
     print("SANITIZER-DRIVER-OK")
 ''')
 
