@@ -983,8 +983,10 @@ def _go_quote(s):
 
 
 def _pyyaml_load(loader_cls, text, multi):
-    """``yaml.load`` / ``yaml.load_all`` with the duplicate-key scan of each
-    composed document before it is constructed."""
+    """``yaml.load_all``, or for a single load the first document only (go-yaml's
+    ``Unmarshal`` decodes the first document of a stream and never reads the
+    rest), with the duplicate-key scan of each composed document before it is
+    constructed."""
     loader = loader_cls(text)
     dups = []
     try:
@@ -995,14 +997,48 @@ def _pyyaml_load(loader_cls, text, multi):
                 dups.extend(_duplicate_keys(node))
                 docs.append(loader.construct_document(node))
         else:
-            node = loader.get_single_node()
             docs = None
-            if node is not None:
-                dups = _duplicate_keys(node)
-                docs = loader.construct_document(node)
+            if loader.check_node():
+                node = loader.get_node()
+                if node is not None:
+                    dups = _duplicate_keys(node)
+                    docs = loader.construct_document(node)
     finally:
         loader.dispose()
     return docs, dups
+
+
+def _go_error_texts(e, text):
+    """(go-yaml v3 text, go-yaml v2 text) of a PyYAML parse error, or None.
+    Both libraries are ports of libyaml, whose problem strings PyYAML's C
+    loader reports verbatim; they differ in the line they name (``parser.fail``:
+    v3 prefers the context mark, v2 the problem mark; scanner marks are one
+    line behind).  Marks are 0-based and line 0 is not printed."""
+    import yaml
+    if not isinstance(e, yaml.MarkedYAMLError):
+        return None
+    problem = e.problem or "unknown problem parsing YAML content"
+    if isinstance(e, yaml.composer.ComposerError) and problem.startswith("found undefined alias"):
+        name = ""
+        if e.problem_mark is not None and isinstance(text, str):
+            i = e.problem_mark.index + 1
+            j = i
+            while j < len(text) and text[j] not in " \t\r\n,[]{}":
+                j += 1
+            name = text[i:j]
+        msg = "yaml: unknown anchor '%s' referenced" % name
+        return msg, msg
+    scanner = isinstance(e, yaml.scanner.ScannerError)
+    cm = e.context_mark if e.context_mark is not None else (e.problem_mark if scanner else None)
+    cl = cm.line if cm is not None else 0
+    pl = e.problem_mark.line if e.problem_mark is not None else 0
+    bump = 1 if scanner else 0
+    v3 = cl + bump if cl else (pl + bump if pl else 0)
+    v2 = pl + bump if pl else cl
+
+    def fmt(line):
+        return "yaml: " + ("line %d: " % line if line else "") + problem
+    return fmt(v3), fmt(v2)
 
 
 def _parse(text, mode, multi):
@@ -1029,6 +1065,13 @@ def _parse(text, mode, multi):
             for d in (docs if multi else (docs,)):
                 _check_aliasing(d, lz.yaml.YAMLError)
         return docs, tuple(dups)
+    except lz.yaml.MarkedYAMLError as e:
+        texts = _go_error_texts(e, text)
+        if texts is None:
+            raise
+        err = lz.yaml.YAMLError(texts[1] if mode == _V2 else texts[0])
+        err.go_v2 = texts[1]
+        raise err from None
     except UnicodeError as e:
         # bytes that are not UTF-8 (kept as surrogates by read_text): a parse
         # error of this document, as go-yaml reports "invalid leading UTF-8
@@ -1049,6 +1092,18 @@ def _v2(result):
     return result[0]
 
 
+def _as_v2(memoized, kind, text, parse):
+    """A shared v3-flavoured parse answering a v2 caller: parse errors name
+    the line go-yaml v2 would."""
+    try:
+        return memoized(kind, text, parse)
+    except _lz().yaml.YAMLError as e:
+        v2 = getattr(e, "go_v2", None)
+        if v2 is None:
+            raise
+        raise _lz().yaml.YAMLError(v2) from None
+
+
 def load(text):
     """Decode like go-yaml v3 into ``interface{}``."""
     return _v3(_memoized("typed", text, lambda t: _parse(t, _TYPED, False)))
@@ -1066,13 +1121,13 @@ def load_v2(text):
     decoders differ only in the YAML 1.1 bool words, so a document that does
     not contain one anywhere shares the v3 parse (and its memo entry)."""
     if isinstance(text, str) and not _V2_ONLY_WORDS.search(text):
-        return _v2(_memoized("typed", text, lambda t: _parse(t, _TYPED, False)))
+        return _v2(_as_v2(_memoized, "typed", text, lambda t: _parse(t, _TYPED, False)))
     return _v2(_memoized("typed-v2", text, lambda t: _parse(t, _V2, False)))
 
 
 def load_all_v2(text):
     if isinstance(text, str) and not _V2_ONLY_WORDS.search(text):
-        return _v2(_memoized("typed*", text, lambda t: _parse(t, _TYPED, True)))
+        return _v2(_as_v2(_memoized, "typed*", text, lambda t: _parse(t, _TYPED, True)))
     return _v2(_memoized("typed-v2*", text, lambda t: _parse(t, _V2, True)))
 
 

@@ -160,8 +160,9 @@ def test_loader_entry_points_use_native(monkeypatch):
     assert yamlio.load("a: &x 1\nb: *x\n") == {"a": 1, "b": 1}  # anchors: PyYAML path
     with pytest.raises(yamlio.YAMLError):
         yamlio.load("a: b: c\n")
-    with pytest.raises(yamlio.YAMLError):
-        yamlio.load("a\n---\nb\n")
+    # go-yaml's Unmarshal decodes the first document of a stream
+    assert yamlio.load("a\n---\nb\n") == "a"
+    assert yamlio.load("---\nk: v\n---\n: bad\n") == {"k": "v"}
 
 
 # ---- generated documents ----------------------------------------------------
