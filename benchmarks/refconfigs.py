@@ -73,6 +73,7 @@ EXTRA_CONFIGS = {
 PROFILES = ("AWS-EKS", "Azure-AKS", "GCP-GKE", "IBM-IKS", "IBM-Openshift", "Kubernetes", "Openshift")
 GOLDEN_COVERAGE = os.path.join(GOLDEN_REF, "coverage")
 CARRIED_OVER = os.path.join(FIXTURES, "carried_over")
+CARRIED_OVER_KINDS = os.path.join(FIXTURES, "carried_over_kinds")
 GIT_REPOS = os.path.join(FIXTURES, "git_repos")
 Q_ARTIFACT = "Choose the artifact type:"
 Q_CLUSTER = "Choose the cluster type:"
@@ -90,6 +91,12 @@ def _coverage_configs():
     for p in ("Kubernetes", "Openshift", "AWS-EKS", "IBM-Openshift"):
         # old-version Kubernetes/OpenShift YAMLs carried over to each profile
         out["carried-over/" + p] = ("carried", "carried", {Q_CLUSTER: p}, False, None)
+    # kinds the target cluster lacks (Route/Ingress/LoadBalancer and NodePort
+    # Services, Pods, Jobs, ReplicationControllers, ConfigMaps/Secrets) carried
+    # over or generated for Kubernetes, Openshift and a custom cluster profile
+    # found in the source tree (ClusterMetadata "minimal-cluster")
+    for p in ("Kubernetes", "Openshift", "minimal-cluster"):
+        out["carried-over-kinds/" + p] = ("carried-kinds", "carried", {Q_CLUSTER: p}, False, None)
     # source trees that are git repos with an origin remote
     out["git-repos"] = ("git", "git", {}, False, None)
     return out
@@ -166,6 +173,8 @@ class Run:
             shutil.copytree(CF_APP, os.path.join(self.work, "cf"), symlinks=True)
         elif self.layout == "carried":
             shutil.copytree(CARRIED_OVER, self.src, symlinks=True)
+        elif self.layout == "carried-kinds":
+            shutil.copytree(CARRIED_OVER_KINDS, self.src, symlinks=True)
         elif self.layout == "git":
             _copy_git_repos(self.src)
         if self.answers:

@@ -168,3 +168,36 @@ def test_plan_records_repo_info(tmp_path):
                                                            "develop")
     node = by_name["nodeapp"].repo_info
     assert node.git_repo_dir == os.path.join(run.src, "move2kube-demos")
+
+
+def test_kind_conversions_to_the_cluster():
+    """coverage/carried-over-kinds: what a target that lacks a kind gets
+    (service.go:104-388, storage.go:75-196, deployment.go:66-171)."""
+    from move2kube_amd.utils import yamlio
+
+    def obj(profile, name):
+        path = os.path.join(refconfigs.golden_dir("carried-over-kinds/" + profile), "myproject", name)
+        with open(path) as f:
+            return yamlio.load(f.read())
+    # Kubernetes: the Route becomes an Ingress, a LoadBalancer Service an
+    # Ingress (one rule per port) plus the same Service as ClusterIP
+    ing = obj("Kubernetes", "shop-ingress.yaml")
+    assert ing["spec"]["rules"][0]["host"] == "shop.example.com"
+    assert ing["spec"]["rules"][0]["http"]["paths"][0]["backend"]["service"] == {"name": "shop",
+                                                                               "port": {"name": "http"}}
+    gw = obj("Kubernetes", "gateway-ingress.yaml")
+    assert [r["http"]["paths"][0]["path"] for r in gw["spec"]["rules"]] == ["/gateway/web", "/gateway/admin"]
+    assert obj("Kubernetes", "gateway-service.yaml")["spec"]["type"] == "ClusterIP"
+    # Openshift: an Ingress with two paths -> two Routes of one name, the last kept
+    front = obj("Openshift", "front-route.yaml")
+    assert front["spec"]["path"] == "/api" and front["spec"]["to"]["name"] == "gateway"
+    assert obj("Openshift", "gateway-route.yaml")["spec"]["port"]["targetPort"] == "admin"
+    # minimal profile: no Secret -> ConfigMap with decoded data; no Deployment
+    # -> ReplicationController; restart-on-failure workloads -> Pods; Ingress
+    # paths -> NodePort Services that replace the carried-over ones
+    assert obj("minimal-cluster", "app-secret-configmap.yaml")["data"] == {"password": "s3cr3t"}
+    assert obj("minimal-cluster", "legacy-rc-replicationcontroller.yaml")["kind"] == "ReplicationController"
+    assert obj("minimal-cluster", "migrate-pod.yaml")["spec"]["restartPolicy"] == "OnFailure"
+    assert obj("minimal-cluster", "seed-pod.yaml")["spec"]["restartPolicy"] == "OnFailure"
+    svc = obj("minimal-cluster", "gateway-service.yaml")["spec"]
+    assert svc == {"ports": [{"name": "web", "port": 0}], "type": "NodePort"}
