@@ -31,21 +31,6 @@ def kind_of(obj):
     return obj.get("kind", "")
 
 
-def new_object(gv, kind, name=None, labels=None, annotations=None):
-    md = {}
-    if name is not None:
-        md["name"] = name
-    if labels:
-        md["labels"] = dict(labels)
-    if annotations:
-        md["annotations"] = dict(annotations)
-    return {"apiVersion": gv, "kind": kind, "metadata": md}
-
-
-def meta(obj):
-    return obj.setdefault("metadata", {})
-
-
 def object_meta_copy(m):
     out = {}
     for k, v in (m or {}).items():
@@ -154,14 +139,8 @@ def _group_kind(obj):
 
 
 def _resource_key(obj):
-    """What ``_same_resource`` compares, or None for an object without a name
-    (such an object never matches another)."""
+    """``isSameResource`` (apiresource.go): namespace + name and group/kind, or
+    None for an object without a name (such an object never matches another)."""
     oid = _object_id(obj)
     return None if oid == "" else (oid, _group_kind(obj))
 
-
-def _same_resource(a, b):
-    ia, ib = _object_id(a), _object_id(b)
-    if ia == "" or ib == "" or ia != ib:
-        return False
-    return _group_kind(a) == _group_kind(b)
