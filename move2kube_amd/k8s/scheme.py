@@ -118,11 +118,6 @@ def is_registered(gv, kind, scheme="k8s"):
     return kind in table.get(gv, ())
 
 
-def versions_for_kind(kind, scheme="all"):
-    table = _K8S if scheme == "k8s" else _KNATIVE if scheme == "knative" else _ALL
-    return [gv for gv, kinds in table.items() if kind in kinds]
-
-
 def decode(data, scheme="k8s"):
     """UniversalDeserializer().Decode: first YAML document -> object dict.
 
@@ -165,14 +160,6 @@ def _decode(data, scheme):
 def decode_file(path, scheme="k8s"):
     from ..utils.common import read_bytes  # a FIFO in the tree is an error, not a hang
     return decode(read_bytes(path), scheme)
-
-
-def gvk(obj):
-    return obj.get("apiVersion", ""), obj.get("kind", "")
-
-
-def group_of(gv):
-    return gv.split("/", 1)[0] if "/" in gv else ""
 
 
 # version priority inside a group when it differs from the table order above

@@ -1,6 +1,8 @@
 """Interactive engines: the HTTP REST protocol the UI uses and the terminal engine."""
 
 import io
+
+import pytest
 import json
 import threading
 import urllib.error
@@ -111,6 +113,20 @@ def test_cli_engine_select_confirm_input_multiselect():
     assert ms.get_slice_answer() == ["x", "z"]
     assert e.fetch_answer(qa.new_input_problem("i2", [], "dflt")).get_string_answer() == "dflt"
     assert "Hints:" in out.getvalue()
+
+
+def test_cli_engine_plain_multiline_password_and_eof():
+    out = io.StringIO()
+    inp = io.StringIO("line 1\nline 2\n\n\ns3cret\n")
+    e = CliEngine(stdin=inp, stdout=out)
+    ml = e.fetch_answer(qa.new_multiline_input_problem("ml", [], "dflt"))
+    assert ml.get_string_answer() == "line 1\nline 2"
+    assert e.fetch_answer(qa.new_multiline_input_problem("ml2", [], "dflt")).get_string_answer() == "dflt"
+    assert e.fetch_answer(qa.new_password_problem("pw", [])).get_string_answer() == "s3cret"
+    # end of input while a question waits: Fatalf like the reference's survey error
+    from move2kube_amd.utils import log
+    with pytest.raises(log.FatalError):
+        e.fetch_answer(qa.new_input_problem("late", [], ""))
 
 
 def _cache_answers(path):
