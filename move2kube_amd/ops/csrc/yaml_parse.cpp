@@ -27,6 +27,7 @@
 
 #include <cstring>
 #include <string>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -505,18 +506,16 @@ class Parser {
     return std::string(raw, rawlen);
   }
 
-  static void check_unique(PyObject* d, PyObject* key, std::vector<std::string>& seen, std::string v) {
+  static void check_unique(PyObject* d, PyObject* key, std::unordered_set<std::string>& seen, std::string v) {
     int has = PyDict_Contains(d, key);
     if (has < 0) throw PyErrorSet();
     if (has) throw Unsupported();
-    for (const std::string& s : seen)
-      if (s == v) throw Unsupported();
-    seen.push_back(std::move(v));
+    if (!seen.insert(std::move(v)).second) throw Unsupported();
   }
 
   PyObject* block_map(int col) {
     Ref d(PyDict_New());
-    std::vector<std::string> seen;
+    std::unordered_set<std::string> seen;
     for (;;) {
       const Line& ln = L_[li_];
       int kend, colon;
@@ -664,7 +663,7 @@ class Parser {
     const bool is_seq = ln.s[pos] == '[';
     const char close = is_seq ? ']' : '}';
     Ref coll(is_seq ? PyList_New(0) : PyDict_New());
-    std::vector<std::string> seen;
+    std::unordered_set<std::string> seen;
     int p = pos + 1;
     while (p < ln.len && ln.s[p] == ' ') p++;
     if (p < ln.len && ln.s[p] == close) {
