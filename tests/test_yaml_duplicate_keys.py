@@ -64,3 +64,14 @@ def test_plan_with_a_repeated_key_is_refused(tmp_path):
     with pytest.raises(Exception) as ei:
         plantypes.read_plan(str(p))
     assert 'mapping key "name" already defined at line 4' in str(ei.value)
+
+
+def test_repeated_key_checks_are_linear():
+    import time
+    n = 50000
+    text = "".join("k%d: %d\n" % (i, i) for i in range(n))
+    t0 = time.perf_counter()
+    assert len(yamlio.load(text)) == n
+    with pytest.raises(yamlio.YAMLError):
+        yamlio.load(text + "k7: again\n")
+    assert time.perf_counter() - t0 < 20
