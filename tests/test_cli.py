@@ -194,3 +194,17 @@ def test_two_step_flow_matches_one_step_on_reference_samples(tmp_path, monkeypat
     descs = [s["description"] for s in two["spec"]["solutions"]]
     assert "Select all services that are needed:" not in descs
     assert "Select all services that should be exposed:" in descs
+
+
+def test_verbose_flag_turns_on_debug_lines(work, capsys):
+    """`-v` (move2kube.go:41-46, PersistentPreRunE) sets the Debug level for the
+    command: the planner's per-file debug lines appear, and go away again."""
+    from move2kube_amd.utils import log
+    try:
+        assert cli.main(["-v", "plan", "-s", str(work / "src"), "-p", str(work / "cwd" / "v.plan")]) == 0
+        err = capsys.readouterr().err
+        assert "DEBU[" in err and "INFO[" in err
+    finally:
+        log.set_verbose(False)
+    assert cli.main(["plan", "-s", str(work / "src"), "-p", str(work / "cwd" / "q.plan")]) == 0
+    assert "DEBU[" not in capsys.readouterr().err
