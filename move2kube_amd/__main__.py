@@ -1,5 +1,11 @@
+import gc
 import sys
 
-from .cli.main import main
+from . import _cli_process
 
+_cli_process()
+from .cli.main import main  # noqa: E402
+
+gc.freeze()
+gc.enable()
 sys.exit(main())

@@ -2,9 +2,11 @@
 
 * ``_m2k_native*.so`` - C++17 pybind11 module (host runtime), built with g++.
 * ``libm2k_ed_hip.so`` - HIP library for gfx950 (``hipcc --offload-arch=gfx950``).
+* ``move2kube_amd/_bytecode.bin`` - compiled code of every package module in
+  one file (``ops/bytecode.py``), read once per CLI process.
 
 Run ``python -m move2kube_amd.ops.build`` (or ``__graft_entry__.build()``).
-Builds are incremental: a target is rebuilt only when its source is newer.
+Builds are incremental: a target is rebuilt only when its sources changed.
 """
 
 import os
@@ -94,9 +96,18 @@ def build_hip(force=False, arch="gfx950"):
     return out
 
 
+def build_bytecode(force=False):
+    """The package's bytecode bundle (``ops/bytecode.py``)."""
+    from . import bytecode
+    if not force and not bytecode.stale():
+        return bytecode.target()
+    return bytecode.write()
+
+
 def build_all(force=False):
     outs = [build_native(force)]
     outs.append(build_hip(force))
+    outs.append(build_bytecode(force))
     return outs
 
 
@@ -108,7 +119,9 @@ def build_report(force=True):
     import time
     report = []
     for name, fn, target in (("_m2k_native (g++, C++17/pybind11)", build_native, native_target()),
-                             ("libm2k_ed_hip (hipcc --offload-arch=gfx950)", build_hip, hip_target())):
+                             ("libm2k_ed_hip (hipcc --offload-arch=gfx950)", build_hip, hip_target()),
+                             ("_bytecode.bin (package bytecode bundle)", build_bytecode,
+                              os.path.join(os.path.dirname(HERE), "_bytecode.bin"))):
         before = os.path.getmtime(target) if os.path.exists(target) else None
         t0 = time.perf_counter()
         out = fn(force)

@@ -278,7 +278,6 @@ class K8sTransformer(Transformer):
                         "executable file not found in $PATH")
             return None
         import subprocess
-        import tempfile
         opath = os.path.join(basepath, project + "-operator")
         if os.path.exists(opath):
             shutil.rmtree(opath, ignore_errors=True)
@@ -286,7 +285,7 @@ class K8sTransformer(Transformer):
         chart = os.path.abspath(os.path.join(basepath, project))
         span = trace.span("operator-sdk init (external tool)", "external")
         span.__enter__()
-        out = tempfile.TemporaryFile()  # not a pipe: nothing reads it until the tool exits
+        out = common.unnamed_temp_file()  # not a pipe: nothing reads it until the tool exits
         try:
             p = subprocess.Popen([sdk, "init", "--plugins=helm", "--helm-chart=" + chart, "--domain=io",
                                   "--group=" + project, "--version=v1alpha1"], cwd=opath, stdout=out,

@@ -471,6 +471,18 @@ def go_exit_status(returncode):
     return "signal: " + (_GO_SIGNALS[sig] if 0 < sig < len(_GO_SIGNALS) else "signal %d" % sig)
 
 
+def unnamed_temp_file():
+    """A read/write binary file with no name, gone when closed - what
+    ``tempfile.TemporaryFile`` makes on Linux (``O_TMPFILE`` in the temp dir),
+    without importing ``tempfile`` and ``random`` into a cold CLI process."""
+    try:
+        fd = os.open(os.environ.get("TMPDIR") or "/tmp", os.O_RDWR | os.O_TMPFILE | os.O_CLOEXEC, 0o600)
+    except (AttributeError, OSError):
+        import tempfile
+        return tempfile.TemporaryFile()
+    return open(fd, "w+b")
+
+
 def run_command(argv, **kw):
     """``subprocess.run`` whose missing-executable error reads like Go's."""
     import subprocess

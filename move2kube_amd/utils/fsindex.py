@@ -15,7 +15,6 @@ translator open one) indexes are reused; outside a scope each query walks
 afresh so callers never observe stale listings.
 """
 
-import contextlib
 import os
 import re
 import threading
@@ -38,8 +37,7 @@ def _cache():
     return getattr(_local, "cache", None)
 
 
-@contextlib.contextmanager
-def scope(keep_for=None, adopt=None):
+class scope:
     """Reuse file indexes for the duration of the block (nestable).
 
     ``keep_for=root``: when this (outermost) scope ends, its listings and
@@ -47,22 +45,30 @@ def scope(keep_for=None, adopt=None):
     - the plan and the translate of one ``translate`` command, which walk the
     same unchanged tree (see :func:`handoff_allowed`).  Anything kept and not
     adopted is dropped by the next keeping scope or :func:`drop_kept`."""
-    prev = _cache()
-    if prev is None:
-        kept = getattr(_local, "kept", None)
-        _local.kept = None
-        if adopt is not None and kept is not None and kept[0] == adopt:
-            _local.cache, _local.aux = kept[1], kept[2]
-        else:
-            _local.cache = {}
-    try:
-        yield
-    finally:
+
+    __slots__ = ("keep_for", "adopt", "prev")
+
+    def __init__(self, keep_for=None, adopt=None):
+        self.keep_for = keep_for
+        self.adopt = adopt
+
+    def __enter__(self):
+        self.prev = prev = _cache()
         if prev is None:
-            if keep_for is not None:
-                _local.kept = (keep_for, _local.cache, getattr(_local, "aux", None))
+            kept = getattr(_local, "kept", None)
+            _local.kept = None
+            if self.adopt is not None and kept is not None and kept[0] == self.adopt:
+                _local.cache, _local.aux = kept[1], kept[2]
+            else:
+                _local.cache = {}
+
+    def __exit__(self, *exc):
+        if self.prev is None:
+            if self.keep_for is not None:
+                _local.kept = (self.keep_for, _local.cache, getattr(_local, "aux", None))
             _local.cache = None
             _local.aux = None
+        return False
 
 
 def drop_kept():

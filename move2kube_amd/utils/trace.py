@@ -11,8 +11,6 @@ the command ends (or at interpreter exit) and opens in ``chrome://tracing`` /
 Perfetto.  Disabled, a span costs one global read.
 """
 
-import atexit
-import contextlib
 import os
 import threading
 import time
@@ -35,23 +33,46 @@ def enabled():
     return _events is not None
 
 
-@contextlib.contextmanager
+class _NoSpan:
+    __slots__ = ()
+
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NO_SPAN = _NoSpan()
+
+
+class _Span:
+    __slots__ = ("ev", "name", "cat", "args", "start")
+
+    def __init__(self, ev, name, cat, args):
+        self.ev, self.name, self.cat, self.args = ev, name, cat, args
+
+    def __enter__(self):
+        self.start = time.perf_counter_ns()
+
+    def __exit__(self, *exc):
+        end = time.perf_counter_ns()
+        rec = {"name": self.name, "cat": self.cat, "ph": "X", "pid": os.getpid(), "tid": threading.get_ident(),
+               "ts": (self.start - _t0) / 1000.0, "dur": (end - self.start) / 1000.0}
+        if self.args:
+            rec["args"] = {k: str(v) for k, v in self.args.items()}
+        with _lock:
+            self.ev.append(rec)
+        return False
+
+
 def span(name, cat="phase", **args):
+    """Context manager recording one complete event (a shared no-op while
+    tracing is off)."""
     ev = _events
     if ev is None:
-        yield
-        return
-    start = time.perf_counter_ns()
-    try:
-        yield
-    finally:
-        end = time.perf_counter_ns()
-        rec = {"name": name, "cat": cat, "ph": "X", "pid": os.getpid(), "tid": threading.get_ident(),
-               "ts": (start - _t0) / 1000.0, "dur": (end - start) / 1000.0}
-        if args:
-            rec["args"] = {k: str(v) for k, v in args.items()}
-        with _lock:
-            ev.append(rec)
+        return _NO_SPAN
+    return _Span(ev, name, cat, args)
 
 
 def events():
@@ -82,5 +103,6 @@ def summary():
 
 
 if os.environ.get("M2K_TRACE"):
+    import atexit
     enable(os.environ["M2K_TRACE"])
     atexit.register(flush)

@@ -18,7 +18,6 @@ field order) unless ``sort_maps=True``; a :class:`GoMap` is always sorted with
 the go-yaml key comparator (Go maps).
 """
 
-import contextlib
 import functools
 import math
 import re
@@ -738,21 +737,25 @@ _memo_depth = 0
 _memo_lock = threading.Lock()
 
 
-@contextlib.contextmanager
-def parse_cache():
+class parse_cache:
     """Memoize YAML parses for the duration of one command (nestable)."""
-    global _memo, _memo_depth
-    with _memo_lock:
-        if _memo_depth == 0:
-            _memo = {}
-        _memo_depth += 1
-    try:
-        yield
-    finally:
+
+    __slots__ = ()
+
+    def __enter__(self):
+        global _memo, _memo_depth
+        with _memo_lock:
+            if _memo_depth == 0:
+                _memo = {}
+            _memo_depth += 1
+
+    def __exit__(self, *exc):
+        global _memo, _memo_depth
         with _memo_lock:
             _memo_depth -= 1
             if _memo_depth == 0:
                 _memo = None
+        return False
 
 
 _ATOMS = (str, int, float, bool, type(None))

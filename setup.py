@@ -20,13 +20,15 @@ def _version():
 
 def _package_data():
     """Every non-Python file under move2kube_amd (assets incl. dot-files such
-    as .s2i/environment, native sources, built .so), relative to the package."""
+    as .s2i/environment, native sources, built .so), relative to the package.
+    Not the bytecode bundle: an installed file's mtime is the install time, so
+    its records would never match (ops/bytecode.py)."""
     root = os.path.join(HERE, "move2kube_amd")
     out = []
     for dp, dns, fns in os.walk(root):
         dns[:] = [d for d in dns if d != "__pycache__"]
         for fn in fns:
-            if fn.endswith((".py", ".pyc", ".tmp")):
+            if fn.endswith((".py", ".pyc", ".tmp")) or fn == "_bytecode.bin":
                 continue
             out.append(os.path.relpath(os.path.join(dp, fn), root))
     return sorted(out)

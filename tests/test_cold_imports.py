@@ -56,3 +56,23 @@ def test_fastjson_parse_int_hook_and_errors():
     for bad in ("", "{", "[1,]", "{} x", "'a'", "[1 2]"):
         with pytest.raises(ValueError):
             fastjson.loads(bad)
+
+
+def test_cli_entry_process_setup():
+    """``python -m move2kube_amd`` (like the release launcher) imports the CLI
+    with the cyclic collector off, then freezes those objects and turns it back
+    on; shutil comes without bz2/lzma and msvcrt is recorded as absent; a
+    library import of the package changes none of that."""
+    probe = ("import atexit, gc, sys\n"
+             "sys.argv = ['move2kube', 'version']\n"
+             "atexit.register(lambda: print(gc.isenabled(), gc.get_freeze_count() > 1000, 'bz2' in sys.modules,"
+             " sys.modules.get('msvcrt', 0) is None))\n"
+             "import runpy\nrunpy.run_module('move2kube_amd', run_name='__main__', alter_sys=True)\n")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    p = subprocess.run([sys.executable, "-S", "-c", probe], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       timeout=60)
+    assert p.stdout.decode().split() == ["v0.1.0", "True", "True", "False", "True"], p.stderr.decode()
+    lib = ("import gc, sys\nimport move2kube_amd.cli.main\n"
+           "print(gc.isenabled(), gc.get_freeze_count(), 'msvcrt' in sys.modules)\n")
+    p = subprocess.run([sys.executable, "-S", "-c", lib], env=env, stdout=subprocess.PIPE, timeout=60)
+    assert p.stdout.decode().split() == ["True", "0", "False"]

@@ -228,3 +228,16 @@ def test_os_errors_read_like_go_path_errors(tmp_path):
     e = PermissionError(errno.EACCES, "Permission denied", "/out")
     assert c.go_path_error(e, "mkdir") == "mkdir /out: permission denied"
     assert c.go_path_error(OSError("no path"), "open") == "no path"
+
+
+def test_unnamed_temp_file(tmp_path, monkeypatch):
+    from move2kube_amd.utils import common
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    with common.unnamed_temp_file() as f:
+        f.write(b"operator output")
+        f.seek(0)
+        assert f.read() == b"operator output"
+        assert os.listdir(str(tmp_path)) == []  # no name in the directory
+    monkeypatch.setenv("TMPDIR", str(tmp_path / "missing"))
+    with common.unnamed_temp_file() as f:  # falls back to tempfile's search
+        f.write(b"x")

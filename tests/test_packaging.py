@@ -36,17 +36,19 @@ def test_builddist_and_install(tmp_path):
     # the launcher starts the interpreter without site (-S) and still finds
     # site-packages modules (PyYAML) for the optional paths
     probe = prefix / "probe.py"
-    probe.write_text("import sys, yaml; print(sys.flags.no_site, yaml.__name__)\n")
+    probe.write_text("import sys, yaml\nimport move2kube_amd.cli.main as m\n"
+                     "print(sys.flags.no_site, yaml.__name__, type(m.__loader__).__name__)\n")
     launcher = os.path.realpath(str(prefix / "bin" / "move2kube"))
     entry = os.path.join(os.path.dirname(launcher), "m2k_main.py")
     with open(entry) as f:
-        code = f.read().replace("from move2kube_amd.cli.main import main  # noqa: E402\n\nsys.exit(main())\n",
-                                "exec(open(%r).read())\n" % str(probe))
+        code = f.read()
+    code = code[:code.index("from move2kube_amd.cli.main import main")] + "exec(open(%r).read())\n" % str(probe)
     probe_entry = os.path.join(os.path.dirname(launcher), "probe_main.py")
     with open(probe_entry, "w") as f:
         f.write(code)
     p = subprocess.run([sys.executable, "-S", probe_entry], stdout=subprocess.PIPE, check=True, env=env)
-    assert p.stdout.decode().split() == ["1", "yaml"]
+    # ... and the package's modules come from the archive's bytecode bundle
+    assert p.stdout.decode().split() == ["1", "yaml", "_BytecodeBundle"]
     with open(launcher) as f:
         assert '-S "$HERE/bin/m2k_main.py"' in f.read()
 
@@ -87,5 +89,6 @@ def test_wheel_with_the_images_setuptools(tmp_path):
     assert "move2kube_amd/cli/main.py" in names
     assert "move2kube_amd/assets/m2kassets/s2i/python/.s2i/environment" in names
     assert "move2kube_amd/assets/templates/k8sreadme.md.tpl" in names
+    assert "move2kube_amd/_bytecode.bin" not in names  # installed files get new mtimes: it would never be valid
     if os.path.exists(os.path.join(ROOT, "move2kube_amd", "ops", "libm2k_ed_hip.so")):
         assert "move2kube_amd/ops/libm2k_ed_hip.so" in names
