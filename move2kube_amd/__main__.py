@@ -1,11 +1,10 @@
 import gc
-import sys
 
-from . import _cli_process
+from . import _cli_exit, _cli_process
 
 _cli_process()
 from .cli.main import main  # noqa: E402
 
 gc.freeze()
 gc.enable()
-sys.exit(main())
+_cli_exit(main())

@@ -76,3 +76,41 @@ def test_cli_entry_process_setup():
            "print(gc.isenabled(), gc.get_freeze_count(), 'msvcrt' in sys.modules)\n")
     p = subprocess.run([sys.executable, "-S", "-c", lib], env=env, stdout=subprocess.PIPE, timeout=60)
     assert p.stdout.decode().split() == ["True", "0", "False"]
+
+
+@pytest.mark.parametrize("rc,code", [(None, 0), (0, 0), (3, 3), ("failed", 1)])
+def test_cli_exit_behaves_like_sys_exit(tmp_path, rc, code):
+    """``_cli_exit`` skips the interpreter teardown but keeps what ``sys.exit``
+    guarantees: non-daemon threads finish, atexit handlers run after them,
+    buffered stdout reaches the pipe, the status is the same."""
+    log = tmp_path / "order.txt"
+    probe = ("import atexit, sys, threading, time\n"
+             "import move2kube_amd\n"
+             "def note(s):\n    open(%r, 'a').write(s + '\\n')\n"
+             "atexit.register(note, 'atexit')\n"
+             "t = threading.Thread(target=lambda: (time.sleep(0.2), note('thread')))\nt.start()\n"
+             "sys.stdout.write('buffered output')\n"
+             "move2kube_amd._cli_exit(%r)\n" % (str(log), rc))
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    p = subprocess.run([sys.executable, "-c", probe], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       timeout=60)
+    assert p.returncode == code
+    assert p.stdout == b"buffered output"
+    assert log.read_text().split() == ["thread", "atexit"]
+    if isinstance(rc, str):
+        assert p.stderr.decode().strip() == rc
+
+
+def test_cli_runs_leave_no_unclosed_files(tmp_path):
+    """The fast exit relies on every file being closed by the code that opened
+    it: a translate under ``-X dev`` that ends through the full interpreter
+    teardown (where a leaked file would be finalized and warn) reports no
+    ResourceWarning."""
+    import refconfigs
+    run = refconfigs.Run("helm-openshift", str(tmp_path)).prepare()
+    env = dict(run.env(), PYTHONPATH=ROOT, PYTHONWARNINGS="always::ResourceWarning")
+    child = "import sys\nfrom move2kube_amd.cli.main import main\nsys.exit(main(%r))\n" % run.cli_commands()[-1]
+    p = subprocess.run([sys.executable, "-X", "dev", "-c", child], env=env,
+                       cwd=str(tmp_path), stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=120)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    assert "ResourceWarning" not in p.stderr.decode()
