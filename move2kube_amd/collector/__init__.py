@@ -102,7 +102,8 @@ def get_collectors():
 
 
 def has_overlap(a, b):
-    return any(x.casefold() == y.casefold() for x in a for y in b)
+    from ..utils.common import go_fold
+    return any(go_fold(x) == go_fold(y) for x in a for y in b)
 
 
 def collect(input_path, output_path, annotations=()):

@@ -37,10 +37,10 @@ class RegistryCustomizer:
         for c in ir.containers:
             if c.new:
                 newimages.extend(c.image_names)
-        new_folded = {x.casefold() for x in newimages}   # is_string_present, once per image
+        new_folded = {common.go_fold(x) for x in newimages}   # is_string_present, once per image
         for s in ir.sorted_services():
             for c in s.containers:
-                if c.get("image", "").casefold() not in new_folded:
+                if common.go_fold(c.get("image", "")) not in new_folded:
                     parts = c.get("image", "").split("/")
                     if len(parts) == 3:
                         reg_list.append(parts[0])
@@ -149,7 +149,7 @@ class RegistryCustomizer:
         for s in ir.sorted_services():
             for c in s.containers:
                 image = c.get("image", "")
-                if image.casefold() in new_folded:
+                if common.go_fold(image) in new_folded:
                     parts = image.split("/")
                     name, tag = common.get_image_name_and_tag(parts[-1])
                     if ir.kubernetes.registry_url and ir.kubernetes.registry_namespace:

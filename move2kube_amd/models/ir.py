@@ -348,7 +348,7 @@ class IR:
             for pos, c in enumerate(self.containers):
                 bt = c.container_build_type
                 for n in c.image_names:
-                    b = buckets.setdefault((bt, n.casefold()), [])
+                    b = buckets.setdefault((bt, common.go_fold(n)), [])
                     if not b or b[-1] != pos:
                         b.append(pos)
             idx = self._cidx = [self.containers, len(self.containers), buckets]
@@ -360,14 +360,14 @@ class IR:
         bt = container.container_build_type
         best = -1
         for n in container.image_names:
-            b = buckets.get((bt, n.casefold()))
+            b = buckets.get((bt, common.go_fold(n)))
             if b and (best < 0 or b[0] < best):
                 best = b[0]
         if best >= 0:
             c = self.containers[best]
             if c.merge(container):
                 for n in c.image_names:
-                    b = buckets.setdefault((bt, n.casefold()), [])
+                    b = buckets.setdefault((bt, common.go_fold(n)), [])
                     if best not in b:
                         b.append(best)
                         b.sort()
@@ -375,7 +375,7 @@ class IR:
         pos = len(self.containers)
         self.containers.append(container)
         for n in container.image_names:
-            b = buckets.setdefault((bt, n.casefold()), [])
+            b = buckets.setdefault((bt, common.go_fold(n)), [])
             if not b or b[-1] != pos:
                 b.append(pos)
         idx[1] = len(self.containers)

@@ -71,9 +71,9 @@ class Problem:
         if self.type in (SELECT, MULTISELECT):
             ok = True
             self.answer = []
-            folded = {o.casefold() for o in self.options} if len(answer) > 1 else None
+            folded = {common.go_fold(o) for o in self.options} if len(answer) > 1 else None
             for a in answer:
-                if (a.casefold() not in folded) if folded is not None else not common.is_string_present(self.options, a):
+                if (common.go_fold(a) not in folded) if folded is not None else not common.is_string_present(self.options, a):
                     log.warning("No matching value in options for %s. Ignoring.", a)
                     ok = False
                     continue
@@ -244,14 +244,14 @@ def _matcher(s1):
     new problem against every cached one.  The regex is compiled on the first
     comparison its literals do not rule out (``_NOT_COMPILED`` until then,
     None if it does not compile)."""
-    return [s1.casefold(), required_literals(s1), _NOT_COMPILED]
+    return [common.go_fold(s1), required_literals(s1), _NOT_COMPILED]
 
 
 def _match_string(s1, s2):
     """``strings.EqualFold(s1, s2)`` or ``regexp.MatchString(s1, s2)``
     (reference ``internal/types/qaengine/problem.go:matchString``)."""
     m = _matcher(s1)
-    if m[0] == s2.casefold():
+    if m[0] == common.go_fold(s2):
         return True
     lits = m[1]
     if lits is not None:
@@ -284,9 +284,9 @@ def _new_problem(t, desc, context, default, opts):
     if t == MULTISELECT:
         if len(opts) == 0:
             resolved = True
-        folded = {o.casefold() for o in opts}   # common.is_string_present for every default at once
+        folded = {common.go_fold(o) for o in opts}   # common.is_string_present for every default at once
         for d in default:
-            if d.casefold() not in folded:
+            if common.go_fold(d) not in folded:
                 raise ProblemError("Default value [%s] not present in options [%s]" % (d, opts))
     elif t == SELECT:
         if len(opts) == 0:
@@ -388,7 +388,7 @@ class _DescIndex:
         return problems is self.problems and len(problems) == self.size
 
     def add(self, pos, desc):
-        fold = desc.casefold()
+        fold = common.go_fold(desc)
         self.fold.setdefault(fold, set()).add(pos)
         lits = _matcher(desc)[1]
         gram = None
@@ -424,7 +424,7 @@ class _DescIndex:
             self.grams[gram].discard(pos)
 
     def candidates(self, desc):
-        out = set(self.fold.get(desc.casefold(), ()))
+        out = set(self.fold.get(common.go_fold(desc), ()))
         out |= self.always
         grams, q = self.grams, self.Q
         for i in range(len(desc) - q + 1):

@@ -101,7 +101,7 @@ def fnv64a(data):
 
 def get_sha256_hash(s):
     import hashlib  # OpenSSL start-up cost; only long names need it
-    return hashlib.sha256(s.encode()).hexdigest()
+    return hashlib.sha256(s.encode("utf-8", "surrogateescape")).hexdigest()
 
 
 # ---------------------------------------------------------------------------
@@ -265,8 +265,41 @@ def normalize_for_filename(name):
     return processed + "-" + format(crc64_ecma(name.encode()), "x")
 
 
+def go_lower(s):
+    """Go ``strings.ToLower``: the simple (one-to-one) lowercase mapping of
+    every rune.  ``str.lower`` applies the full mapping, which differs for one
+    character only: U+0130 (capital I with dot) becomes "i" + U+0307 there and
+    "i" in Go."""
+    if s.isascii():
+        return s.lower()
+    return s.replace("\u0130", "i").lower()
+
+
+_FOLD = {}
+
+
+def _go_fold_char(c):
+    f = c.casefold()
+    if len(f) != 1:        # a full (one-to-many) folding: Go folds simply
+        f = c.lower()
+        if len(f) != 1:
+            f = c
+    _FOLD[c] = f
+    return f
+
+
+def go_fold(s):
+    """Key under which Go ``strings.EqualFold`` calls two strings equal: the
+    simple case folding of every rune.  ``str.casefold`` applies the full
+    folding, so it equates "Straße" with "STRASSE", which EqualFold does not."""
+    if s.isascii():
+        return s.lower()
+    fold = _FOLD
+    return "".join([fold.get(c) or _go_fold_char(c) for c in s])
+
+
 def normalize_for_service_name(svc_name):
-    new = svc_name.replace(".", "-").replace("_", "-").lower()  # [._] -> "-" (utils.go:297-305)
+    new = go_lower(svc_name.replace(".", "-").replace("_", "-"))  # [._] -> "-" (utils.go:297-305)
     if new != svc_name:
         log.info("Changing service name to %s from %s", svc_name, new)
     return new
@@ -276,9 +309,9 @@ def is_string_present(lst, value):
     """Case-insensitive membership (Go ``strings.EqualFold``)."""
     if not lst:
         return False
-    v = value.casefold()
+    v = go_fold(value)
     for x in lst:
-        if x == value or x.casefold() == v:
+        if x == value or go_fold(x) == v:
             return True
     return False
 
@@ -352,26 +385,36 @@ _DNS_INVALID = _lazy_re(r"[^a-z0-9\-.]")
 
 
 def make_string_dns_name_compliant(s):
-    low = s.lower()
+    low = go_lower(s)
     name = _DNS_INVALID.sub("-", low) if low.translate(_DROP_DNS_OK) else low
     if name and (name[0] in "-." or name[-1] in "-."):
         log.warning("The first and/or last characters of the string %r are not alphanumeric.", s)
     return name
 
 
+def _go_byte_prefix(s, n):
+    """``s[:n]`` of a Go string: its first n UTF-8 bytes.  A rune cut in two
+    leaves bytes that Go reads one invalid byte at a time; here they become
+    one lone surrogate each, which the DNS pattern replaces like Go does."""
+    return s.encode("utf-8", "surrogateescape")[:n].decode("utf-8", "surrogateescape")
+
+
 def make_string_dns_subdomain_name_compliant(s):
+    """MakeStringDNSSubdomainNameCompliant (utils.go:461-469): lengths are
+    UTF-8 byte counts, as in Go."""
     name = s
-    if len(name) > 253:
+    if len(name.encode("utf-8", "surrogateescape")) > 253:
         h = get_sha256_hash(name)
-        name = name[:253 - 65] + "-" + h
+        name = _go_byte_prefix(name, 253 - 65) + "-" + h
     return make_string_dns_name_compliant(name)
 
 
 def make_string_dns_label_name_compliant(s):
+    """MakeStringDNSLabelNameCompliant (utils.go:477-486), byte lengths."""
     name = s
-    if len(name) > 63:
+    if len(name.encode("utf-8", "surrogateescape")) > 63:
         h = get_sha256_hash(name)[:32]
-        name = name[:63 - 33] + "-" + h
+        name = _go_byte_prefix(name, 63 - 33) + "-" + h
     return make_string_dns_name_compliant(name)
 
 
@@ -581,7 +624,7 @@ def get_closest_matching_strings(options, searches):
     from ..ops import editdistance
     if not options or not searches:
         return [""] * len(searches)
-    toks = [_TOKEN_RE.sub("", o).lower() for o in options]
-    qs = [_TOKEN_RE.sub("", s).lower() for s in searches]
+    toks = [go_lower(_TOKEN_RE.sub("", o)) for o in options]
+    qs = [go_lower(_TOKEN_RE.sub("", s)) for s in searches]
     idx, _ = editdistance.closest_index_list(toks, qs)
     return [options[i] for i in idx]

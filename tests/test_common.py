@@ -241,3 +241,41 @@ def test_unnamed_temp_file(tmp_path, monkeypatch):
     monkeypatch.setenv("TMPDIR", str(tmp_path / "missing"))
     with common.unnamed_temp_file() as f:  # falls back to tempfile's search
         f.write(b"x")
+
+
+def test_go_case_helpers():
+    """strings.ToLower / strings.EqualFold use simple (one-to-one) case
+    mappings; Python's lower/casefold apply the full ones."""
+    from move2kube_amd.utils import common
+    assert common.go_lower("MyApp") == "myapp"
+    assert common.go_lower("İstanbul") == "istanbul"          # str.lower: "i̇stanbul"
+    assert common.go_fold("STRASSE") != common.go_fold("Straße")  # casefold equates them
+    assert common.go_fold("ẞ") == common.go_fold("ß")        # capital sharp s folds to sharp s
+    assert common.go_fold("K") == common.go_fold("k")             # Kelvin sign
+    assert common.go_fold("ſ") == common.go_fold("S")             # long s
+    assert common.go_fold("İ") != common.go_fold("i")
+    assert common.is_string_present(["Straße"], "STRASSE") is False
+    assert common.is_string_present(["STRAẞE"], "straße") is True
+    assert common.normalize_for_service_name("İzmir_App.v2") == "izmir-app-v2"
+
+
+def test_dns_names_count_utf8_bytes_like_go():
+    """MakeStringDNSLabelNameCompliant / ...SubdomainNameCompliant
+    (utils.go:461-486) compare and cut Go string lengths, i.e. UTF-8 bytes;
+    a rune cut in two leaves one invalid byte each, replaced by '-'."""
+    import hashlib
+    from move2kube_amd.utils import common
+    assert common.make_string_dns_label_name_compliant("My_App") == "my-app"
+    s = "é" * 40                                  # 40 characters, 80 bytes
+    h = hashlib.sha256(s.encode()).hexdigest()[:32]
+    assert common.make_string_dns_label_name_compliant(s) == "-" * 15 + "-" + h
+    s = "a" + "é" * 20                           # 41 bytes: cut at 30 splits the 15th rune
+    s = s + "b" * 30                                   # 71 bytes
+    h = hashlib.sha256(s.encode()).hexdigest()[:32]
+    out = common.make_string_dns_label_name_compliant(s)
+    assert out == "a" + "-" * 14 + "-" + "-" + h      # 14 whole runes, 1 stray byte, then the hyphen
+    assert len(out) == 1 + 14 + 1 + 1 + 32   # each non-ASCII rune became one '-'
+    s = "x" * 200 + "中" * 20                      # 260 bytes
+    out = common.make_string_dns_subdomain_name_compliant(s)
+    assert out == "x" * 188 + "-" + hashlib.sha256(s.encode()).hexdigest() and len(out) == 253
+    assert common.make_string_dns_subdomain_name_compliant("x" * 200 + "中" * 17) == "x" * 200 + "-" * 17
