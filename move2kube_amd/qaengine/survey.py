@@ -402,8 +402,11 @@ def paginate(page_size, choices, sel):
 
 
 def _filtered(options, flt):
-    f = flt.lower()
-    return [(i, o) for i, o in enumerate(options) if f in o.lower()]
+    """survey's DefaultFilterFn: ``strings.Contains(strings.ToLower(option),
+    strings.ToLower(filter))``."""
+    from ..utils.common import go_lower
+    f = go_lower(flt)
+    return [(i, o) for i, o in enumerate(options) if f in go_lower(o)]
 
 
 # -- prompts --------------------------------------------------------------------

@@ -42,7 +42,7 @@ SUPPORTED_V2 = {"2", "2.0", "2.1"}
 
 
 def _normalize_project_name(s):
-    return re.sub(r"[^a-z0-9]", "", s.lower())
+    return re.sub(r"[^a-z0-9]", "", common.go_lower(s))
 
 
 def _read_raw(path):
@@ -436,7 +436,7 @@ class V1V2Loader:
                     ir.add_container(ReuseDockerfileContainerizer().get_container(plan, service))
                 except Exception as e:  # noqa: BLE001
                     log.warning("Unable to get containization script even though build parameters are present : %s", e)
-            cname = cs["container_name"].lower()
+            cname = common.go_lower(cs["container_name"])
             if cname != cs["container_name"]:
                 log.debug("Container name in service %r has been changed from %r to %r", name, cs["container_name"], cname)
             cont["name"] = cname or sc.name

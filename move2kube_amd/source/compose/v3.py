@@ -378,7 +378,7 @@ class V3Loader:
                 cont["args"] = cs["command"]
             if cs["stdin_open"]:
                 cont["stdin"] = True
-            cont["name"] = cs["container_name"].lower() or sc.name.lower()
+            cont["name"] = common.go_lower(cs["container_name"]) or common.go_lower(sc.name)
             if cs["tty"]:
                 cont["tty"] = True
             cont["ports"] = self.get_ports(cs["ports"], cs["expose"])
