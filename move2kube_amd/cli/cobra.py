@@ -85,58 +85,13 @@ def _go_q(s):
 
 
 def _parse_bool(s):
-    """strconv.ParseBool."""
-    if s in ("1", "t", "T", "TRUE", "true", "True"):
-        return True
-    if s in ("0", "f", "F", "FALSE", "false", "False"):
-        return False
-    raise ValueError("strconv.ParseBool: parsing %s: invalid syntax" % _go_q(s))
-
-
-def _underscore_ok(s):
-    """strconv ``underscoreOK``: ``_`` only between digits or after a base prefix."""
-    s = s[1:] if s[:1] in "+-" else s
-    saw, i, hexa = "^", 0, False
-    if len(s) >= 2 and s[0] == "0" and s[1].lower() in "box":
-        i, saw, hexa = 2, "0", s[1].lower() == "x"
-    for ch in s[i:]:
-        if ch.isdigit() or (hexa and ch.lower() in "abcdef"):
-            saw = "0"
-        elif ch == "_":
-            if saw != "0":
-                return False
-            saw = "_"
-        elif saw == "_":
-            return False
-        else:
-            saw = "!"
-    return saw != "_"
-
-
-_DIGITS = {16: "0123456789abcdefABCDEF", 10: "0123456789", 8: "01234567", 2: "01"}
+    from ..utils.common import go_parse_bool
+    return go_parse_bool(s)
 
 
 def _parse_int(s):
-    """strconv.ParseInt(s, 0, 64) (base prefixes, Go underscore rules)."""
-    err = "strconv.ParseInt: parsing %s: " % _go_q(s)
-    t = s[1:] if s[:1] in "+-" else s
-    base, body = 10, t
-    if len(t) >= 2 and t[0] == "0":
-        p = t[1].lower()
-        base, body = ({"x": 16, "o": 8, "b": 2}[p], t[2:]) if p in "xob" else (8, t[1:])
-    elif t == "0":
-        body = "0"
-    if "_" in body:
-        if not _underscore_ok(s):
-            raise ValueError(err + "invalid syntax")
-        body = body.replace("_", "")
-    if not body or any(c not in _DIGITS[base] for c in body):
-        raise ValueError(err + "invalid syntax")
-    v = int(body, base)
-    v = -v if s[:1] == "-" else v
-    if not -(1 << 63) <= v < (1 << 63):
-        raise ValueError(err + "value out of range")
-    return v
+    from ..utils.common import go_parse_int
+    return go_parse_int(s)
 
 
 def _read_csv(val):

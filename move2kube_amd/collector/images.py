@@ -12,20 +12,6 @@ from ..utils.lazyre import lazy as _lazy_re
 _NUM = _lazy_re(r"[0-9]+")
 
 
-def cast_to_int_e(s):
-    """spf13/cast ``ToIntE`` for strings (base prefix aware, "1.0" -> 1)."""
-    if isinstance(s, bool):
-        return int(s)
-    if isinstance(s, int):
-        return s
-    t = str(s)
-    if "." in t:
-        head, _, tail = t.partition(".")
-        if tail.strip("0") == "":
-            t = head
-    return int(t, 0)
-
-
 def get_image_info(data):
     info = ImageInfo()
     try:
@@ -37,17 +23,19 @@ def get_image_info(data):
         cfg = image.get("ContainerConfig") or {}
         info.tags = list(image.get("RepoTags") or [])
         try:
-            info.user_id = cast_to_int_e(cfg.get("User", ""))
+            info.user_id = common.cast_to_int(cfg.get("User", ""))
         except (ValueError, TypeError):
             log.debug("UserID not available in image metadata for [%s]", (info.tags or [""])[0])
             info.user_id = -1
         info.accessed_dirs.append(cfg.get("WorkingDir", ""))
         for key in sorted(cfg.get("ExposedPorts") or {}):
             m = _NUM.search(key)
-            if m is None:
+            try:
+                if m is None:
+                    raise ValueError(key)
+                info.ports.append(common.cast_to_int(m.group(0)))   # "0123" is octal, "080" an error
+            except ValueError:
                 log.debug("PortNumber not available in image metadata for [%s]", (info.tags or [""])[0])
-                continue
-            info.ports.append(int(m.group(0)))
     return info
 
 

@@ -493,11 +493,12 @@ class V3Loader:
                 rl["memory"] = cu.format_quantity_decimal_exponent(r["memory"])
             if r["cpus"] != "":
                 try:
-                    cpu = float(r["cpus"])
-                except ValueError:
-                    log.warning("Unable to convert cpu limits resources value : %s", r["cpus"])
+                    cpu = common.cast_to_float(r["cpus"])
+                except ValueError as e:
+                    log.warning("Unable to convert cpu limits %s value : %s",
+                                "resources" if key == "limits" else "reservation", e)
                     cpu = 0.0
-                milli = int(cpu * 1000)
+                milli = common.go_float_to_int64(cpu * 1000)
                 if milli != 0:
                     rl["cpu"] = cu.format_milli_quantity(milli)
             res[out] = rl

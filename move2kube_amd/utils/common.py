@@ -583,35 +583,149 @@ def go_dir(p):
     return go_clean(d) if d else "."
 
 
+# ---------------------------------------------------------------------------
+# strconv / spf13/cast (v1.3.1) parsing
+# ---------------------------------------------------------------------------
+
+def go_parse_bool(s):
+    """strconv.ParseBool."""
+    if s in ("1", "t", "T", "TRUE", "true", "True"):
+        return True
+    if s in ("0", "f", "F", "FALSE", "false", "False"):
+        return False
+    raise ValueError("strconv.ParseBool: parsing %s: invalid syntax" % log.go_quote(s))
+
+
+def _underscore_ok(s):
+    """strconv ``underscoreOK``: ``_`` only between digits or after a base prefix."""
+    s = s[1:] if s[:1] in "+-" else s
+    saw, i, hexa = "^", 0, False
+    if len(s) >= 2 and s[0] == "0" and s[1] in "bBoOxX":
+        i, saw, hexa = 2, "0", s[1] in "xX"
+    for ch in s[i:]:
+        if "0" <= ch <= "9" or (hexa and ch in "abcdefABCDEF"):
+            saw = "0"
+        elif ch == "_":
+            if saw != "0":
+                return False
+            saw = "_"
+        elif saw == "_":
+            return False
+        else:
+            saw = "!"
+    return saw != "_"
+
+
+_DIGITS = {16: "0123456789abcdefABCDEF", 10: "0123456789", 8: "01234567", 2: "01"}
+
+
+def go_parse_int(s, bits=64):
+    """strconv.ParseInt(s, 0, bits): sign, base prefixes 0x/0o/0b and a
+    leading 0 for octal, underscores by Go's rules, range checked."""
+    err = "strconv.ParseInt: parsing %s: " % log.go_quote(s)
+    t = s[1:] if s[:1] in "+-" else s
+    base, body = 10, t
+    if len(t) >= 2 and t[0] == "0":
+        p = t[1]
+        base, body = ({"x": 16, "X": 16, "o": 8, "O": 8, "b": 2, "B": 2}[p], t[2:]) if p in "xXoObB" else (8, t[1:])
+    if "_" in body:
+        if not _underscore_ok(s):
+            raise ValueError(err + "invalid syntax")
+        body = body.replace("_", "")
+    if not body or any(c not in _DIGITS[base] for c in body):
+        raise ValueError(err + "invalid syntax")
+    v = int(body, base)
+    v = -v if s[:1] == "-" else v
+    if not -(1 << (bits - 1)) <= v < (1 << (bits - 1)):
+        raise ValueError(err + "value out of range")
+    return v
+
+
+_FLOAT_DEC = _lazy_re(r"(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?\Z")
+_FLOAT_HEX = _lazy_re(r"0[xX](?:[0-9a-fA-F]+\.?[0-9a-fA-F]*|\.[0-9a-fA-F]+)[pP][+-]?[0-9]+\Z")
+
+
+def go_parse_float(s):
+    """strconv.ParseFloat(s, 64): Go float syntax only (no surrounding
+    spaces, no ``+nan``, hexadecimal mantissas need a ``p`` exponent,
+    underscores by Go's rules); a finite-looking value beyond float64 is a
+    range error rather than infinity."""
+    err = "strconv.ParseFloat: parsing %s: " % log.go_quote(s)
+    body = s[1:] if s[:1] in "+-" else s
+    low = body.lower()
+    if low in ("inf", "infinity"):
+        return float("-inf") if s[:1] == "-" else float("inf")
+    if low == "nan" and body == s:
+        return float("nan")
+    if not s.isascii():
+        raise ValueError(err + "invalid syntax")
+    if "_" in body:
+        if not _underscore_ok(s):
+            raise ValueError(err + "invalid syntax")
+        body = body.replace("_", "")
+    try:
+        if _FLOAT_HEX.match(body):
+            v = float.fromhex(body)
+        elif _FLOAT_DEC.match(body):
+            v = float(body)
+        else:
+            raise ValueError(err + "invalid syntax")
+    except OverflowError:
+        v = float("inf")
+    if v in (float("inf"), float("-inf")):
+        raise ValueError(err + "value out of range")
+    return -v if s[:1] == "-" else v
+
+
 def cast_to_bool(s):
-    """spf13/cast ToBoolE for strings (strconv.ParseBool)."""
+    """spf13/cast ToBoolE (strconv.ParseBool for strings)."""
     if isinstance(s, bool):
         return s
     if isinstance(s, (int, float)):
         return s != 0
-    t = str(s)
-    if t in ("1", "t", "T", "TRUE", "true", "True"):
-        return True
-    if t in ("0", "f", "F", "FALSE", "false", "False"):
+    if s is None:
         return False
-    raise ValueError("strconv.ParseBool: parsing %r: invalid syntax" % t)
+    return go_parse_bool(str(s))
 
 
 def cast_to_int(s):
-    """spf13/cast ToIntE (base-0 parsing for strings)."""
+    """spf13/cast v1.3.1 ToIntE: strings through strconv.ParseInt(s, 0, 0),
+    no trimming; nil is 0."""
+    if s is None:
+        return 0
     if isinstance(s, bool):
         return int(s)
     if isinstance(s, int):
         return s
     if isinstance(s, float):
-        return int(s)
-    t = str(s).strip()
+        return go_float_to_int64(s)
+    t = str(s)
     try:
-        return int(t, 0)
+        return go_parse_int(t)
     except ValueError:
-        if re.match(r"^[-+]?0\d+$", t):
-            return int(t, 8)
-        raise ValueError("unable to cast %r of type string to int" % t)
+        raise ValueError("unable to cast %s of type string to int" % log.go_quote(t)) from None
+
+
+def cast_to_float(s):
+    """spf13/cast v1.3.1 ToFloat64E: strings through strconv.ParseFloat."""
+    if s is None:
+        return 0.0
+    if isinstance(s, (bool, int, float)):
+        return float(s)
+    t = str(s)
+    try:
+        return go_parse_float(t)
+    except ValueError:
+        raise ValueError("unable to cast %s of type string to float64" % log.go_quote(t)) from None
+
+
+def go_float_to_int64(f):
+    """Go ``int64(f)`` on amd64: truncation toward zero; NaN, infinities and
+    out-of-range values give the CVTTSD2SI "integer indefinite" value,
+    math.MinInt64."""
+    if f != f or f in (float("inf"), float("-inf")) or not -9.223372036854775808e18 <= f < 9.223372036854775808e18:
+        return -(1 << 63)
+    return int(f)
 
 
 def go_bool_str(b):

@@ -279,3 +279,46 @@ def test_dns_names_count_utf8_bytes_like_go():
     out = common.make_string_dns_subdomain_name_compliant(s)
     assert out == "x" * 188 + "-" + hashlib.sha256(s.encode()).hexdigest() and len(out) == 253
     assert common.make_string_dns_subdomain_name_compliant("x" * 200 + "中" * 17) == "x" * 200 + "-" * 17
+
+
+@pytest.mark.parametrize("text,want", [
+    ("1.5", 1.5), ("1_000.5", 1000.5), ("0x1p-2", 0.25), (".5", 0.5), ("5.", 5.0), ("-2e3", -2000.0),
+    ("Infinity", float("inf")), ("-inf", float("-inf")), ("1e-400", 0.0),
+    ("0x1.8", "invalid syntax"), ("+nan", "invalid syntax"), (" 1", "invalid syntax"), ("1e", "invalid syntax"),
+    ("1__0", "invalid syntax"), ("٣", "invalid syntax"), ("1e400", "value out of range"),
+])
+def test_go_parse_float(text, want):
+    """strconv.ParseFloat, not float(): no spaces, no signed NaN, hex needs
+    'p', ASCII digits only, overflow is an error."""
+    from move2kube_amd.utils import common
+    if isinstance(want, str):
+        with pytest.raises(ValueError) as ei:
+            common.go_parse_float(text)
+        assert str(ei.value).endswith(want)
+    else:
+        assert common.go_parse_float(text) == want
+
+
+@pytest.mark.parametrize("text,want", [
+    ("80", 80), ("010", 8), ("0x1F", 31), ("-0b101", -5), ("0o17", 15), ("1_000", 1000), ("0", 0), (None, 0),
+    (7.9, 7), (True, 1),
+    ("080", None), ("08", None), (" 80", None), ("80 ", None), ("1.0", None), ("", None), ("+", None),
+    ("9223372036854775808", None), ("_1", None), ("١٢", None),
+])
+def test_cast_to_int_is_cast_v1_3_1(text, want):
+    """spf13/cast v1.3.1 ToIntE = strconv.ParseInt(s, 0, 0): no trimming, no
+    "1.0" (that came with cast v1.4), octal by a leading 0."""
+    from move2kube_amd.utils import common
+    if want is None:
+        with pytest.raises(ValueError) as ei:
+            common.cast_to_int(text)
+        assert str(ei.value) == 'unable to cast "%s" of type string to int' % text
+    else:
+        assert common.cast_to_int(text) == want
+
+
+def test_go_float_to_int64():
+    from move2kube_amd.utils import common
+    assert common.go_float_to_int64(2.9) == 2 and common.go_float_to_int64(-2.9) == -2
+    for f in (float("nan"), float("inf"), float("-inf"), 1e19):
+        assert common.go_float_to_int64(f) == -(1 << 63)

@@ -123,3 +123,33 @@ def test_compose_v3_non_string_keys_fail_the_file(tmp_path, env, where):
     p.write_text("version: '3'\nservices:\n  s:\n    image: busybox\n    environment:\n      %s\n" % env)
     with pytest.raises(v3.ComposeError, match="Non-string key in " + where.replace(".", "\\.")):
         v3.parse_v3(str(p))
+
+
+@pytest.mark.parametrize("cpus,limit,warning", [
+    ("'0.5'", {"cpu": "500m"}, None),
+    ("'1_0'", {"cpu": "10"}, None),                       # underscores: Go float syntax
+    ("' 0.5'", {}, 'Unable to convert cpu limits resources value : unable to cast " 0.5" of type string to float64'),
+    ("'1e400'", {}, 'Unable to convert cpu limits resources value : unable to cast "1e400" of type string to float64'),
+    ("'inf'", {"cpu": "-9223372036854775808m"}, None),   # int64(+Inf) on amd64
+])
+def test_deploy_cpus_parse_like_cast_to_float64(tmp_path, monkeypatch, capsys, cpus, limit, warning):
+    """deploy.resources.*.cpus goes through cast.ToFloat64E and int64(x*1000)
+    (v3.go:246-269); reservations warn with their own wording."""
+    from move2kube_amd.utils import log
+    monkeypatch.setenv("M2K_NO_NETWORK", "1")
+    monkeypatch.setenv("M2K_DISABLE_CNB", "1")
+    monkeypatch.setattr(settings, "compat", "fixed")
+    src = tmp_path / "app"
+    src.mkdir()
+    (src / "docker-compose.yaml").write_text(
+        "version: '3.7'\nservices:\n  s:\n    image: busybox\n    deploy:\n      resources:\n"
+        "        limits:\n          cpus: %s\n        reservations:\n          cpus: 'x'\n" % cpus)
+    log.set_verbose(False)
+    out = api.translate(str(src), str(tmp_path / "out"), name="c")
+    err = capsys.readouterr().err
+    dep = yamlio.load(open(os.path.join(out, "c", "s-deployment.yaml")).read())
+    res = dep["spec"]["template"]["spec"]["containers"][0]["resources"]
+    assert res.get("limits", {}) == limit and res.get("requests", {}) == {}
+    assert 'Unable to convert cpu limits reservation value : unable to cast "x" of type string to float64' in err
+    if warning:
+        assert warning in err
