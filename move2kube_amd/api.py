@@ -8,7 +8,7 @@ import sys
 from . import assets, move2kube, qaengine
 from .containerizer import cnb
 from .models import plan as plantypes
-from .utils import fsindex, sshkeys, yamlio
+from .utils import common, fsindex, sshkeys, yamlio
 from .utils.constants import QA_CACHE_FILE, settings
 
 
@@ -52,12 +52,12 @@ class Session:
         """``move2kube collect -s src -o outdir -a ...``: metadata under
         ``outdir/m2k_collect``; no provider probe of an earlier run is reused."""
         reset_state()
-        move2kube.collect(os.path.abspath(src) if src else "", os.path.join(outdir, "m2k_collect"), list(annotations))
+        move2kube.collect(common.go_abs(src) if src else "", os.path.join(outdir, "m2k_collect"), list(annotations))
 
     def plan(self, src, name="myproject"):
         self._start()
         with yamlio.parse_cache():
-            return move2kube.create_plan(os.path.abspath(src), name)
+            return move2kube.create_plan(common.go_abs(src), name)
 
     def translate(self, src, outdir, name="myproject", plan=None, curate=True):
         """``move2kube translate -s src -o outdir -n name`` (new plan unless one is
@@ -68,12 +68,12 @@ class Session:
 
     def _translate(self, src, outdir, name, plan, curate):
         if plan is None:
-            src = os.path.abspath(src)
+            src = common.go_abs(src)
             p = move2kube.create_plan(src, name, keep_index=fsindex.handoff_allowed(
-                src, os.path.join(os.path.abspath(outdir), name)))
+                src, os.path.join(common.go_abs(outdir), name)))
         else:
             p = plan if isinstance(plan, plantypes.Plan) else plantypes.read_plan(plan)
-        out = os.path.join(os.path.abspath(outdir), p.name)
+        out = os.path.join(common.go_abs(outdir), p.name)
         os.makedirs(out, exist_ok=True)
         qaengine.set_write_cache(os.path.join(out, QA_CACHE_FILE))
         if curate:

@@ -13,7 +13,7 @@ import sys
 from .. import assets
 from ..models import plan as plantypes
 from ..utils import fsindex, log, yamlio
-from ..utils.common import go_path_error
+from ..utils.common import go_abs, go_clean, go_join, go_path_error
 from ..utils.constants import (APP_NAME_SHORT, DEFAULT_DIRECTORY_PERMISSION, DEFAULT_PLAN_FILE, DEFAULT_PROJECT_NAME,
                                QA_CACHE_FILE, settings)
 from ..utils.lazyre import LazyModule
@@ -25,7 +25,7 @@ qaengine = LazyModule("move2kube_amd.qaengine")
 
 
 def _abs(p):
-    return os.path.abspath(p) if p else p
+    return go_abs(p) if p else p
 
 
 def _go_stat(path):
@@ -164,7 +164,7 @@ def collect_handler(a):
             log.fatal("Error while accessing directory: %s. ", srcpath)
         if not stat.S_ISDIR(st.st_mode):
             log.fatal("Source path is a file, expected directory: %s.", srcpath)
-    outpath = os.path.join(os.path.normpath(outpath), APP_NAME_SHORT + "_collect")
+    outpath = go_join(go_clean(outpath), APP_NAME_SHORT + "_collect")
     annotations = a.annotations.split(",") if a.annotations else []
     from .. import collector  # move2kube.collect without loading the orchestration layer
     collector.collect(srcpath, outpath, annotations)

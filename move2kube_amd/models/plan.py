@@ -451,7 +451,7 @@ def read_plan(path):
     """Read a plan converting relative paths to absolute (planutils.go:165-178)."""
     data = common.read_move2kube_yaml(path)
     plan = Plan.from_yaml(data)
-    plan.root_dir = os.path.abspath(plan.root_dir) if plan.root_dir else os.getcwd()
+    plan.root_dir = common.go_abs(plan.root_dir) if plan.root_dir else os.getcwd()
     _convert_paths(plan, plan.get_absolute_path)
     return plan
 

@@ -419,7 +419,7 @@ def make_string_dns_label_name_compliant(s):
 
 
 def clean_and_find_common_directory(paths):
-    return find_common_directory([os.path.normpath(p) if p else "." for p in paths])
+    return find_common_directory([go_clean(p) for p in paths])
 
 
 def find_common_directory(paths):
@@ -560,6 +560,13 @@ def go_clean(p):
     if c.startswith("//"):
         c = "/" + c.lstrip("/")
     return c
+
+
+def go_abs(p):
+    """Go ``filepath.Abs``: joined with the working directory and cleaned
+    (``os.path.abspath`` keeps a leading ``//``, which POSIX allows and Go's
+    Clean folds to ``/``)."""
+    return go_clean(os.path.abspath(p))
 
 
 def go_ext(p):

@@ -322,3 +322,11 @@ def test_go_float_to_int64():
     assert common.go_float_to_int64(2.9) == 2 and common.go_float_to_int64(-2.9) == -2
     for f in (float("nan"), float("inf"), float("-inf"), 1e19):
         assert common.go_float_to_int64(f) == -(1 << 63)
+
+
+def test_go_abs_cleans_a_double_leading_slash(tmp_path, monkeypatch):
+    from move2kube_amd.utils import common
+    assert common.go_abs("//tmp//x/../y") == "/tmp/y"
+    monkeypatch.chdir(str(tmp_path))
+    assert common.go_abs("a/./b/") == os.path.join(os.path.realpath(str(tmp_path)), "a", "b") or \
+        common.go_abs("a/./b/") == os.path.join(str(tmp_path), "a", "b")
