@@ -11,6 +11,7 @@ Versions are finally ordered by the global group policy: ``*.openshift.io``,
 group.
 """
 
+import functools
 import json
 import os
 import re
@@ -23,6 +24,61 @@ from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
 from . import Collector, CommandError, run
 
 GLOBAL_GROUP_ORDER = [r"^.+\.openshift\.io$", r"^.+\.k8s\.io$", r"^apps$", r"^extensions$"]
+
+# Masterminds/semver v3.1.1 (go.mod:9): NewVersion's pattern and Compare
+_SEMVER_RE = re.compile(r"v?([0-9]+)(\.[0-9]+)?(\.[0-9]+)?(-([0-9A-Za-z\-]+(\.[0-9A-Za-z\-]+)*))?"
+                        r"(\+([0-9A-Za-z\-]+(\.[0-9A-Za-z\-]+)*))?\Z")
+
+
+def _semver(v):
+    """(major, minor, patch, prerelease) or None when NewVersion fails."""
+    m = _SEMVER_RE.match(v)
+    if not m:
+        return None
+    pre = m.group(5) or ""
+    for part in pre.split(".") if pre else ():
+        if part.isdigit() and len(part) > 1 and part[0] == "0":
+            return None               # ErrInvalidPrerelease: numeric identifier with a leading zero
+    nums = [int(x.lstrip(".")) if x else 0 for x in (m.group(1), m.group(2), m.group(3))]
+    if any(n >= 1 << 64 for n in nums):
+        return None
+    return nums[0], nums[1], nums[2], pre
+
+
+def _semver_pre_part(s, o):
+    if s == o:
+        return 0
+    if s == "":
+        return -1
+    if o == "":
+        return 1
+    sn, on = s.isdigit() and int(s) < 1 << 64, o.isdigit() and int(o) < 1 << 64
+    if not sn and not on:
+        return 1 if s > o else -1
+    if not sn:
+        return 1
+    if not on:
+        return -1
+    return 1 if int(s) > int(o) else -1
+
+
+def _semver_compare(a, b):
+    for x, y in zip(a[:3], b[:3]):
+        if x != y:
+            return 1 if x > y else -1
+    ps, po = a[3], b[3]
+    if ps == po == "":
+        return 0
+    if ps == "":
+        return 1
+    if po == "":
+        return -1
+    sp, op = ps.split("."), po.split(".")
+    for i in range(max(len(sp), len(op))):
+        d = _semver_pre_part(sp[i] if i < len(sp) else "", op[i] if i < len(op) else "")
+        if d:
+            return d
+    return 0
 
 
 def _gv_string(group, version):
@@ -262,22 +318,45 @@ class ClusterCollector(Collector):
             kinds[kind] = ordered if ordered else gvs
 
     @staticmethod
-    def _version_key(v):
-        """Kubernetes-style version priority: GA > beta > alpha, higher numbers first."""
-        m = re.match(r"^v(\d+)(?:(alpha|beta)(\d+))?$", v)
-        if not m:
-            return (0, 0, 0, v)
-        stage = {"alpha": 1, "beta": 2, None: 3}[m.group(2)]
-        return (stage, int(m.group(1)), int(m.group(3) or 0), v)
+    def sort_versions(versions):
+        """``sortVersionList`` (clustercollector.go:412-456): ``alpha``/``beta``
+        become ``-alpha.``/``-beta.`` so Masterminds semver v3 reads ``v1beta2``
+        as 1.0.0-beta.2, the list is sorted newest first by semver precedence
+        (``v2beta1`` ranks above ``v1``), and the names are restored.  A
+        version semver rejects is logged and, where the reference's sort would
+        dereference its nil entry and panic, kept after the others."""
+        parsed, bad = [], []
+        for v in versions:
+            for key in ("alpha", "beta"):
+                if key in v:
+                    v = v.replace(key, "-%s." % key)
+                    break
+            sv = _semver(v)
+            if sv is None:
+                log.warning("Skipping Version: %s", v)
+                bad.append(v)
+            else:
+                parsed.append((sv, v))
+        parsed.sort(key=functools.cmp_to_key(lambda a, b: _semver_compare(a[0], b[0])), reverse=True)
+        out = []
+        for _sv, v in parsed + [(None, b) for b in bad]:
+            for key in ("alpha", "beta"):
+                if "-%s." % key in v:
+                    v = v.replace("-%s." % key, key)
+                    break
+            out.append(v)
+        return out
 
     def cluster_by_groups_and_sort_versions(self, gvs):
+        """``clusterByGroupsAndSortVersions``; groups in sorted order (the
+        reference ranges over a map)."""
         by_group = {}
         for gv in gvs:
             g, v = _parse_gv(gv)
             by_group.setdefault(g, []).append(v)
         out = []
         for g in sorted(by_group):
-            for v in sorted(by_group[g], key=self._version_key, reverse=True):
+            for v in self.sort_versions(by_group[g]):
                 out.append(_gv_string(g, v))
         return out
 

@@ -336,3 +336,25 @@ def test_cf_commands_never_overlap(tmp_path, monkeypatch):
     for t in threads:
         t.join()
     assert not (tmp_path / "overlaps").exists()
+
+
+def test_version_sort_is_semver_precedence():
+    """sortVersionList (clustercollector.go:412-456) ranks versions by
+    Masterminds semver after alpha/beta become prerelease tags: a newer major
+    beta comes before the older GA version."""
+    from move2kube_amd.collector.cluster import ClusterCollector
+    assert ClusterCollector.sort_versions(["v1", "v2beta1", "v2beta2"]) == ["v2beta2", "v2beta1", "v1"]
+    assert ClusterCollector.sort_versions(["v1beta1", "v1", "v1alpha1", "v1beta2", "v2alpha1", "v1beta10"]) == \
+        ["v2alpha1", "v1", "v1beta10", "v1beta2", "v1beta1", "v1alpha1"]
+    assert ClusterCollector().cluster_by_groups_and_sort_versions(
+        ["autoscaling/v1", "autoscaling/v2beta1", "v1", "batch/v1beta1", "batch/v1"]) == \
+        ["v1", "autoscaling/v2beta1", "autoscaling/v1", "batch/v1", "batch/v1beta1"]
+
+
+def test_version_sort_keeps_unparsable_versions_last(capsys):
+    from move2kube_amd.collector.cluster import ClusterCollector
+    from move2kube_amd.utils import log
+    log.set_verbose(False)
+    assert ClusterCollector.sort_versions(["v1beta", "v1", "latest"]) == ["v1", "v1beta", "latest"]
+    err = capsys.readouterr().err
+    assert "Skipping Version: v1-beta." in err and "Skipping Version: latest" in err
