@@ -133,8 +133,9 @@ class ClusterCollector(Collector):
             if desc:
                 log.warning("Error while running %s. %s", self.get_cluster_command(), desc)
             else:
+                # exec.Cmd's String(): the looked-up path and the arguments
                 log.warning("Error while fetching storage classes using command [%s get sc -o yaml]",
-                            self.get_cluster_command())
+                            shutil.which(self.get_cluster_command()) or self.get_cluster_command())
             raise
         doc = yamlio.load(out.decode("utf-8", "replace")) or {}
         names = []

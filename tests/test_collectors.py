@@ -358,3 +358,29 @@ def test_version_sort_keeps_unparsable_versions_last(capsys):
     assert ClusterCollector.sort_versions(["v1beta", "v1", "latest"]) == ["v1", "v1beta", "latest"]
     err = capsys.readouterr().err
     assert "Skipping Version: v1-beta." in err and "Skipping Version: latest" in err
+
+
+@pytest.mark.parametrize("output,warning", [
+    ("error: You must be logged in to the server (Unauthorized)",
+     "Error while running kubectl. Please configure the cluster authentication with following instructions: "
+     "[https://kubernetes.io/docs/reference/kubectl/cheatsheet/#kubectl-context-and-configuration]"),
+    ("The connection to the server localhost:8080 was refused",
+     "Error while fetching storage classes using command [%s get sc -o yaml]" % os.path.join(STUBS, "kubectl")),
+])
+def test_storage_class_errors_are_interpreted(stub_path, monkeypatch, capsys, output, warning):
+    """getStorageClasses / interpretError (clustercollector.go:124-173)."""
+    from move2kube_amd.collector import CommandError
+    from move2kube_amd.utils import log
+    log.set_verbose(False)
+    monkeypatch.setenv("M2K_STUB_SC_ERROR", output)
+    with pytest.raises(CommandError):
+        ClusterCollector().get_storage_classes()
+    assert warning in capsys.readouterr().err
+
+
+def test_interpret_error_for_oc():
+    c = ClusterCollector()
+    c.cluster_cmd = "oc"
+    assert c.interpret_error("error: Username or password wrong") == \
+        "Please login to cluster before running collect. (e.g. oc login <cluster url> --token=<token string>)"
+    assert c.interpret_error("no route to host") == ""
