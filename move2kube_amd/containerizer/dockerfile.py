@@ -34,9 +34,18 @@ def _port_from(m):
     return None
 
 
+def _go_list(items):
+    """fmt ``%v`` / ``%s`` of a ``[]string``."""
+    return "[" + " ".join(items) + "]"
+
+
 class DockerfileContainerizer(Containerizer):
     build_type = plantypes.NEW_DOCKERFILE
     script = DOCKERFILE_DETECT_SCRIPT
+    # log texts of dockerfilecontainerizer.go:49-81 (s2icontainerizer.go has its own)
+    kind_name = "Dockerfile"
+    fetch_warning = "Unable to fetch files to recognize docker detect scripts : %s"
+    detected_debug = "Detected Dockerfile containerization options : %s"
 
     def __init__(self):
         self.detectors = []
@@ -45,26 +54,39 @@ class DockerfileContainerizer(Containerizer):
         try:
             files = common.get_files_by_name(path, [self.script])
         except (OSError, ValueError) as e:
-            log.warning("Unable to fetch files to recognize detect scripts : %s", e)
+            log.warning(self.fetch_warning, e)
             files = []
         for f in files:
             self.detectors.append(os.path.dirname(f))
-        log.debug("Detected %s containerization options : %s", self.build_type, self.detectors)
+        log.debug(self.detected_debug, _go_list(self.detectors))
 
     def get_target_options_batch(self, plan, paths):
         jobs = [(d, self.script, p) for p in paths for d in self.detectors]
         res = run_detect_jobs(jobs)
         out = []
         k = 0
-        for _ in paths:
+        verbose = log.debug_enabled()
+        for p in paths:
             opts = []
             for d in self.detectors:
                 r = res[k]
                 k += 1
+                if verbose:
+                    self._log_detect(d, p, r)
                 if r.ok:
                     opts.append(d)
             out.append(opts)
         return out
+
+    def _log_detect(self, d, p, r):
+        """The per-detector debug lines of ``GetTargetOptions``/``detect``
+        (``cmd`` prints as exec.Cmd's String(): path and arguments)."""
+        log.debug("Executing detect script %s on %s : %s", d, p, "/bin/sh %s %s" % (self.script, p))
+        if r.ok:
+            log.debug("Output of %s containerizer detect script %s : %s", self.kind_name, d, r.stdout)
+        else:
+            log.debug("%s detector cannot containerize %s Error: %s", d, p,
+                      log.go_quote(common.go_exit_status(r.code)))
 
     def get_target_options(self, plan, path):
         return self.get_target_options_batch(plan, [path])[0]

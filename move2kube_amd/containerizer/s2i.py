@@ -25,6 +25,10 @@ S2I_DETECT_SCRIPT = "m2ks2idetect.sh"
 class S2IContainerizer(DockerfileContainerizer):
     build_type = plantypes.S2I
     script = S2I_DETECT_SCRIPT
+    # s2icontainerizer.go:51-80 (the trailing space is the reference's)
+    kind_name = "S2I"
+    fetch_warning = "Unable to fetch files to recognize s2i detect files : %s"
+    detected_debug = "Detected S2I containerization options : %s "
 
     def get_container(self, plan, service):
         if service.container_build_type != self.build_type or not service.target_options:

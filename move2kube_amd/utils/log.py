@@ -1,9 +1,14 @@
-"""Structured logging in the style of the reference's logrus output.
+"""Logging in the format of the reference's logger: logrus v1.7.0
+(``go.mod:28``) with its default ``TextFormatter``, Info level, Debug with
+``-v`` (``cmd/move2kube/move2kube.go:41-46``).
 
-The reference prints ``INFO[0000] message`` lines and raises the level to
-Debug with ``-v`` (``cmd/move2kube/move2kube.go:41-46``).  ``fatal`` logs and
-raises :class:`FatalError` (the CLI turns it into exit code 1) instead of
-calling ``os.Exit`` so that the library is usable in-process and in tests.
+The formatter looks at its output once: on a terminal each line is
+``\x1b[36mINFO\x1b[0m[0012] <message padded to 44 runes> `` (level colour,
+seconds since start; one trailing newline of the message dropped), anywhere
+else ``time="<RFC 3339 local time>" level=info msg=<message>`` with the
+message ``%q``-quoted unless it only has letters, digits and ``-._/@^+``.
+``fatal`` logs and raises :class:`FatalError` (the CLI turns it into exit
+code 1) instead of calling ``os.Exit``, so the library works in-process.
 """
 
 import sys
@@ -13,6 +18,9 @@ import time
 _START = time.time()
 DEBUG, INFO, WARNING, ERROR, CRITICAL = 10, 20, 30, 40, 50
 _LEVEL_NAMES = {DEBUG: "DEBU", INFO: "INFO", WARNING: "WARN", ERROR: "ERRO", CRITICAL: "FATA"}
+_LEVEL_WORDS = {DEBUG: "debug", INFO: "info", WARNING: "warning", ERROR: "error", CRITICAL: "fatal"}
+_LEVEL_COLORS = {DEBUG: 37, INFO: 36, WARNING: 33, ERROR: 31, CRITICAL: 31}   # gray, blue, yellow, red
+_BARE = frozenset("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789-._/@^+")
 
 
 _GO_ESC = {"\a": "\\a", "\b": "\\b", "\f": "\\f", "\n": "\\n", "\r": "\\r", "\t": "\\t",
@@ -63,15 +71,53 @@ class FatalError(RuntimeError):
     """Raised where the reference calls ``log.Fatalf``."""
 
 
+def _rfc3339(t):
+    """time.RFC3339 of a local time (logrus' default timestamp format)."""
+    lt = time.localtime(t)
+    off = lt.tm_gmtoff
+    stamp = time.strftime("%Y-%m-%dT%H:%M:%S", lt)
+    if off == 0:
+        return stamp + "Z"
+    sign = "+" if off > 0 else "-"
+    off = abs(off)
+    return "%s%s%02d:%02d" % (stamp, sign, off // 3600, off % 3600 // 60)
+
+
+def format_line(level, text, now, colored):
+    """One logrus TextFormatter line."""
+    if colored:
+        if text.endswith("\n"):
+            text = text[:-1]
+        return "\x1b[%dm%s\x1b[0m[%04d] %-44s \n" % (_LEVEL_COLORS.get(level, 36), _LEVEL_NAMES.get(level, "INFO"),
+                                                     int(now - _START), text)
+    line = 'time="%s" level=%s' % (_rfc3339(now), _LEVEL_WORDS.get(level, "info"))
+    if text:
+        line += " msg=" + (text if _BARE.issuperset(text) else go_quote(text))
+    return line + "\n"
+
+
 class _Logger:
-    """Minimal logrus-style logger (``LEVL[ssss] message`` on stderr).  The
-    stdlib ``logging`` package is not imported: it is a measurable part of a
-    cold CLI start and nothing here needs handlers or hierarchies."""
+    """Minimal logrus-style logger on stderr.  The stdlib ``logging`` package
+    is not imported: it is a measurable part of a cold CLI start and nothing
+    here needs handlers or hierarchies."""
 
     def __init__(self):
         self.level = INFO
         self.stream = None  # None = the current sys.stderr
         self._lock = threading.Lock()
+        self._tty_of = None   # the stream whose terminal check is cached
+        self._tty = False
+
+    def _colored(self, stream):
+        """logrus checks once whether its output is a terminal; a process has
+        one stderr, so the check is cached per stream object."""
+        if stream is not self._tty_of:
+            try:
+                self._tty = stream.isatty()
+            except (AttributeError, ValueError, OSError):
+                self._tty = False
+            self._tty_of = stream
+        return self._tty
 
     def isEnabledFor(self, level):
         return level >= self.level
@@ -87,12 +133,12 @@ class _Logger:
             text = _format(msg, args) if args else msg
         except (TypeError, ValueError):
             text = "%s %r" % (msg, args)
-        line = "%s[%04d] %s\n" % (_LEVEL_NAMES.get(level, "INFO"), int(time.time() - _START), text)
+        stream = self.stream or sys.stderr
+        line = format_line(level, text, time.time(), self._colored(stream))
         held = getattr(_held, "lines", None)
         if held is not None:
             held.append(line)
             return
-        stream = self.stream or sys.stderr
         with self._lock:
             stream.write(line)
             stream.flush()
@@ -169,6 +215,11 @@ def _off(msg, *args):
 
 
 debug = _off
+
+
+def debug_enabled():
+    """Whether ``log.debug`` writes anything (guards debug-only work)."""
+    return debug is not _off
 
 
 def _rebind():

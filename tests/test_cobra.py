@@ -7,8 +7,11 @@ import re
 
 import pytest
 
+import logparse
+
 from move2kube_amd.cli import cobra
 from move2kube_amd.cli import main as cli
+from move2kube_amd.utils import log
 
 ROOT_HELP = """\
 move2kube is a tool to help optimally translate from platforms such as docker-swarm, CF to Kubernetes.
@@ -109,7 +112,8 @@ def test_flag_errors_print_error_and_usage(capsys, argv, msg):
     assert cli.main(argv) == 1
     err = capsys.readouterr().err
     assert err.startswith("Error: %s\nUsage:\n  move2kube %s [flags]\n" % (msg, argv[0]))
-    assert re.search(r"\nFATA\[\d{4}\] Error: ", err)
+    # main.go: log.Fatalf("Error: %q", err)
+    assert logparse.messages(err)[-1] == ("fatal", "Error: " + log.go_quote(msg))
 
 
 def test_value_forms_and_interspersed_arguments():

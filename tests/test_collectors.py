@@ -4,6 +4,8 @@ import os
 
 import pytest
 
+import logparse
+
 from move2kube_amd import collector
 from move2kube_amd.collector import cf as cfc
 from move2kube_amd.collector.cluster import ClusterCollector
@@ -258,7 +260,7 @@ def test_collectors_run_concurrently_with_ordered_logs(monkeypatch, tmp_path):
     t0 = time.perf_counter()
     coll.collect("", str(tmp_path / "out"), ["x"])
     assert time.perf_counter() - t0 < 0.55
-    msgs = [line.split("] ", 1)[1] for line in buf.getvalue().splitlines()]
+    msgs = [m for _lv, m in logparse.messages(buf.getvalue())]
     assert msgs == ["Begin collection", "[a] Begin collection", "a working", "[a] Done", "[b] Begin collection",
                     "b working", '[b] failed. Error: "boom"', "[c] Begin collection", "c working", "[c] Done",
                     "Collection done"]
@@ -267,7 +269,7 @@ def test_collectors_run_concurrently_with_ordered_logs(monkeypatch, tmp_path):
     monkeypatch.setattr(coll, "get_collectors", lambda: [Slow("a", 0.1), Slow("f", 0.0, "fatal"), Slow("c", 0.0)])
     with pytest.raises(log.FatalError):
         coll.collect("", str(tmp_path / "out"), ["x"])
-    msgs = [line.split("] ", 1)[1] for line in buf.getvalue().splitlines()]
+    msgs = [m for _lv, m in logparse.messages(buf.getvalue())]
     assert msgs[-1] == "f cannot go on" and "[a] Done" in msgs and "[c] Done" not in msgs
 
 
@@ -292,7 +294,7 @@ def test_held_log_lines_nest(monkeypatch):
         log.info("three")
     assert buf.getvalue() == ""
     log.emit(outer.lines)
-    assert [l.split("] ", 1)[1] for l in buf.getvalue().splitlines()] == ["one", "two", "three"]
+    assert [m for _lv, m in logparse.messages(buf.getvalue())] == ["one", "two", "three"]
 
 
 def test_images_collector_inspects_concurrently(tmp_path, monkeypatch):
@@ -375,7 +377,7 @@ def test_storage_class_errors_are_interpreted(stub_path, monkeypatch, capsys, ou
     monkeypatch.setenv("M2K_STUB_SC_ERROR", output)
     with pytest.raises(CommandError):
         ClusterCollector().get_storage_classes()
-    assert warning in capsys.readouterr().err
+    assert logparse.logged(capsys.readouterr().err, warning, "warning")
 
 
 def test_interpret_error_for_oc():

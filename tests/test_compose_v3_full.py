@@ -10,6 +10,8 @@ import shutil
 
 import pytest
 
+import logparse
+
 from move2kube_amd import api
 from move2kube_amd.source.compose import utils as cutils
 from move2kube_amd.utils import common, yamlio
@@ -150,6 +152,7 @@ def test_deploy_cpus_parse_like_cast_to_float64(tmp_path, monkeypatch, capsys, c
     dep = yamlio.load(open(os.path.join(out, "c", "s-deployment.yaml")).read())
     res = dep["spec"]["template"]["spec"]["containers"][0]["resources"]
     assert res.get("limits", {}) == limit and res.get("requests", {}) == {}
-    assert 'Unable to convert cpu limits reservation value : unable to cast "x" of type string to float64' in err
+    assert logparse.logged(err, 'Unable to convert cpu limits reservation value : unable to cast "x" of type string '
+                                'to float64', "warning")
     if warning:
-        assert warning in err
+        assert logparse.logged(err, warning, "warning")

@@ -1,0 +1,72 @@
+"""The logger writes logrus v1.7.0 TextFormatter lines (``utils/log.py``):
+coloured and padded on a terminal, ``key=value`` otherwise."""
+
+import os
+import pty
+import re
+import subprocess
+import sys
+import time
+
+from move2kube_amd.utils import log
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_plain_lines_are_key_value():
+    now = time.time()
+    stamp = log._rfc3339(now)
+    assert re.fullmatch(r"\d{4}-\d\d-\d\dT\d\d:\d\d:\d\d(Z|[+-]\d\d:\d\d)", stamp)
+    assert log.format_line(log.INFO, "Planning Translation", now, False) == \
+        'time="%s" level=info msg="Planning Translation"\n' % stamp
+    assert log.format_line(log.WARNING, "done", now, False) == 'time="%s" level=warning msg=done\n' % stamp
+    assert log.format_line(log.DEBUG, "a/b-c_d.e@f^g+h", now, False) == \
+        'time="%s" level=debug msg=a/b-c_d.e@f^g+h\n' % stamp
+    assert log.format_line(log.CRITICAL, 'Error: "x"\n', now, False) == \
+        'time="%s" level=fatal msg="Error: \\"x\\"\\n"\n' % stamp
+    assert log.format_line(log.ERROR, "", now, False) == 'time="%s" level=error\n' % stamp
+
+
+def test_terminal_lines_are_coloured_and_padded():
+    t = log._START + 12.5
+    assert log.format_line(log.INFO, "Planning Translation", t, True) == \
+        "\x1b[36mINFO\x1b[0m[0012] Planning Translation" + " " * 24 + " \n"
+    assert log.format_line(log.WARNING, "x" * 50 + "\n", t, True) == "\x1b[33mWARN\x1b[0m[0012] " + "x" * 50 + " \n"
+    assert log.format_line(log.DEBUG, "é", t, True).startswith("\x1b[37mDEBU\x1b[0m[0012] é" + " " * 43)
+    assert log.format_line(log.ERROR, "e", t, True).startswith("\x1b[31mERRO")
+    assert log.format_line(log.CRITICAL, "f", t, True).startswith("\x1b[31mFATA")
+
+
+def _run_cli(args, stderr):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    return subprocess.run([sys.executable, "-m", "move2kube_amd"] + args, env=env, stdout=subprocess.DEVNULL,
+                          stderr=stderr, timeout=60)
+
+
+def test_cli_picks_the_format_from_its_stderr(tmp_path):
+    missing = str(tmp_path / "nope")
+    p = _run_cli(["plan", "-s", missing], subprocess.PIPE)
+    line = p.stderr.decode().splitlines()[-1]
+    assert re.fullmatch(r'time="[^"]+" level=fatal msg="Unable to access source directory : stat %s: no such file '
+                        r'or directory"' % re.escape(missing), line), line
+    master, slave = pty.openpty()
+    try:
+        p = _run_cli(["plan", "-s", missing], slave)
+        os.close(slave)
+        slave = None
+        out = b""
+        while True:
+            try:
+                chunk = os.read(master, 4096)
+            except OSError:
+                break
+            if not chunk:
+                break
+            out += chunk
+    finally:
+        if slave is not None:
+            os.close(slave)
+        os.close(master)
+    text = out.decode().replace("\r\n", "\n")
+    assert p.returncode == 1
+    assert re.search(r"\x1b\[31mFATA\x1b\[0m\[\d{4}\] \S", text), text
