@@ -131,6 +131,13 @@ class ImageInfo:
         self.accessed_dirs = []
         self.user_id = 0
 
+    def go_v(self):
+        """fmt ``%v`` of the Go struct: ``{{apiVersion kind} {name} {[tags] [ports] [dirs] userID}}``."""
+        def lst(xs):
+            return "[" + " ".join(str(x) for x in xs) + "]"
+        return "{{%s %s} {%s} {%s %s %s %d}}" % (self.api_version, self.kind, self.name, lst(self.tags),
+                                                 lst(self.ports), lst(self.accessed_dirs), self.user_id)
+
     def to_yaml(self):
         d = _typemeta(self, {})
         d["spec"] = {"tags": list(self.tags), "ports": list(self.ports),

@@ -216,7 +216,7 @@ def new_container(container_build_type, image_name, new):
 def new_container_from_image_info(info):
     name = info.tags[0] if info.tags else ""
     if not info.tags:
-        log.error("The image info %r has no tags. Leaving the tag empty for the container.", info.name)
+        log.error("The image info %s has no tags. Leaving the tag empty for the container.", info.go_v())
     c = Container(plantypes.REUSE, name, False)
     c.image_names = list(info.tags)
     c.exposed_ports = list(info.ports)

@@ -343,8 +343,17 @@ def merge_string_maps(a, b):
 
 
 def get_string_from_template(tpl, config):
-    from .gotemplate import render
-    return render(tpl, config)
+    """GetStringFromTemplate (utils.go:347-357): a template that fails to
+    execute is reported with its text and data before the error is returned
+    (a parse error panics in the reference, ``template.Must``; it raises here)."""
+    from . import gotemplate
+    t = gotemplate.compiled(tpl)
+    try:
+        return t.execute(config)
+    except gotemplate.TemplateError:
+        log.warning("Unable to translate template %s to string using the data %s", log.go_quote(tpl),
+                    gotemplate.go_sprint(config))
+        raise
 
 
 def write_template_to_file(tpl, config, write_path, mode):

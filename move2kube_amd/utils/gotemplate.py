@@ -80,6 +80,16 @@ def go_sprint(v, top=True):
     return str(v)
 
 
+_GO_TYPE_NAMES = {bool: "bool", int: "int", float: "float64", str: "string", list: "[]interface {}",
+                  tuple: "[]interface {}", dict: "map[string]interface {}", bytes: "[]uint8"}
+
+
+def _go_type_name(v):
+    """reflect type name of a decoded value in Go's error texts (JSON numbers
+    are float64, objects map[string]interface {})."""
+    return _GO_TYPE_NAMES.get(type(v), type(v).__name__)
+
+
 def _sort_key(k):
     if isinstance(k, (int, float)) and not isinstance(k, bool):
         return (0, k, "")
@@ -877,7 +887,7 @@ class _State:
                 if callable(val):
                     val = val()
             else:
-                raise TemplateError("can't evaluate field %s in type %s" % (name, type(val).__name__))
+                raise TemplateError("can't evaluate field %s in type %s" % (name, _go_type_name(val)))
         return val
 
 
@@ -1030,11 +1040,16 @@ _BUILTINS = {
 _CACHE = {}
 
 
-def render(src, data, funcs=None):
-    """Parse (cached) and execute a Go template against ``data``."""
+def compiled(src):
+    """The parsed template of ``src`` (cached); a parse error raises."""
     t = _CACHE.get(src)
     if t is None:
         t = Template(src)
         if len(_CACHE) < 512:
             _CACHE[src] = t
-    return t.execute(data, funcs)
+    return t
+
+
+def render(src, data, funcs=None):
+    """Parse (cached) and execute a Go template against ``data``."""
+    return compiled(src).execute(data, funcs)

@@ -330,3 +330,31 @@ def test_go_abs_cleans_a_double_leading_slash(tmp_path, monkeypatch):
     monkeypatch.chdir(str(tmp_path))
     assert common.go_abs("a/./b/") == os.path.join(os.path.realpath(str(tmp_path)), "a", "b") or \
         common.go_abs("a/./b/") == os.path.join(str(tmp_path), "a", "b")
+
+
+def test_template_execution_failure_is_reported_with_its_data(capsys):
+    """GetStringFromTemplate (utils.go:347-357) warns with the template (%q)
+    and its data (%v) before returning the error; JSON numbers are float64."""
+    import logparse
+    from move2kube_amd.utils import common, log
+    from move2kube_amd.utils.gotemplate import TemplateError
+    log.set_verbose(False)
+    with pytest.raises(TemplateError) as ei:
+        common.get_string_from_template("FROM {{.port.x}}", {"port": 8080.0, "app": "a b", "n": None})
+    assert str(ei.value) == "can't evaluate field x in type float64"
+    assert logparse.logged(capsys.readouterr().err, 'Unable to translate template "FROM {{.port.x}}" to string '
+                           "using the data map[app:a b n:<nil> port:8080]", "warning")
+
+
+def test_image_info_without_tags_is_logged_as_go_value(capsys):
+    import logparse
+    from move2kube_amd.models import ir
+    from move2kube_amd.models.collection import ImageInfo
+    from move2kube_amd.utils import log
+    log.set_verbose(False)
+    info = ImageInfo()
+    info.name, info.ports, info.accessed_dirs, info.user_id = "img", [8080], ["/app"], -1
+    c = ir.new_container_from_image_info(info)
+    assert c.image_names == []
+    assert logparse.logged(capsys.readouterr().err, "The image info {{move2kube.konveyor.io/v1alpha1 ImageMetadata} "
+                           "{img} {[] [8080] [/app] -1}} has no tags. Leaving the tag empty for the container.", "error")
