@@ -9,12 +9,11 @@
   foundations) instead of the reference's per-name nested scans.
 """
 
-import json
 import os
 
 from ..models import collection
 from ..models import plan as plantypes
-from ..utils import common, log
+from ..utils import common, fastjson, log
 from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
 from . import Collector, concurrently, run
 
@@ -23,7 +22,7 @@ def _cf_apps():
     out = run(["cf", "curl", "/v2/apps"])
     log.debug("Cf Curl output %s", out)
     try:
-        data = json.loads(out)
+        data = fastjson.loads(out)
     except ValueError as e:
         log.error("Error in unmarshalling yaml: %s. Skipping.", e)
         raise

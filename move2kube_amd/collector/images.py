@@ -1,10 +1,9 @@
 """Image metadata via ``docker inspect`` (reference ``internal/collector/imagescollector.go``)."""
 
-import json
 import os
 
 from ..models.collection import ImageInfo
-from ..utils import common, log
+from ..utils import common, fastjson, log
 from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
 from . import Collector, CommandError, concurrently, run
 from ..utils.lazyre import lazy as _lazy_re
@@ -15,7 +14,7 @@ _NUM = _lazy_re(r"[0-9]+")
 def get_image_info(data):
     info = ImageInfo()
     try:
-        images = json.loads(data)
+        images = fastjson.loads(data)
     except ValueError as e:
         log.error("Unable to unmarshal image info : %s", e)
         images = []

@@ -20,7 +20,7 @@ import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 from ..models import qa
-from ..utils import log
+from ..utils import fastjson, log
 from .engine import Engine
 
 PROBLEMS_URL = "/problems"
@@ -35,6 +35,30 @@ def free_port():
     s.close()
     return port
 
+
+
+def _json_kind(v):
+    """UnmarshalTypeError's name for a decoded JSON value."""
+    if isinstance(v, bool):
+        return "bool"
+    if isinstance(v, (int, float)):
+        return "number"
+    if isinstance(v, str):
+        return "string"
+    return "array" if isinstance(v, list) else "object"
+
+
+def _string_slice(v):
+    """``json.Unmarshal(body, &sol)`` into a ``[]string``: null is an empty
+    answer; another type is Go's UnmarshalTypeError (null elements stay "")."""
+    if v is None:
+        return None
+    if not isinstance(v, list):
+        raise ValueError("json: cannot unmarshal %s into Go value of type []string" % _json_kind(v))
+    for x in v:
+        if x is not None and not isinstance(x, str):
+            raise ValueError("json: cannot unmarshal %s into Go value of type string" % _json_kind(x))
+    return ["" if x is None else x for x in v]
 
 class HTTPRESTEngine(Engine):
     interactive = True  # may block on a person: the write cache is flushed first
@@ -81,9 +105,7 @@ class HTTPRESTEngine(Engine):
                 try:
                     n = int(self.headers.get("Content-Length") or 0)
                     body = self.rfile.read(max(0, n))
-                    sol = json.loads(body.decode("utf-8") or "null")
-                    if sol is not None and not (isinstance(sol, list) and all(isinstance(x, str) for x in sol)):
-                        raise ValueError("solution must be a JSON array of strings")
+                    sol = _string_slice(fastjson.loads(body))
                 except ValueError as e:
                     self._send(500, "Error in un-marshalling solution in QA engine: %s\n" % e, "text/plain")
                     return

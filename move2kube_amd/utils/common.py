@@ -241,9 +241,9 @@ def write_json(output_path, data):
 
 
 def read_json(path):
-    import json
-    with open(path) as f:
-        return json.load(f)
+    from . import fastjson
+    with open(path, "rb") as f:
+        return fastjson.loads(f.read())
 
 
 # ---------------------------------------------------------------------------

@@ -1,13 +1,26 @@
 """JSON decoding straight on the C scanner (``_json.make_scanner``), the one
 the stdlib ``json`` package wraps, so the read paths of a command (cluster
 profiles, detector output, ``~/.docker/config.json``) do not import the
-four-module ``json`` package.  Same results and errors class as
-``json.loads`` (``ValueError``); encoding still goes through ``json``.
+four-module ``json`` package.  Encoding still goes through ``json``.
+
+What is accepted and the error text follow Go's ``encoding/json`` (what the
+reference decodes detector output, ``docker inspect`` and the CLI tools' JSON
+with): ``NaN``/``Infinity`` and a byte-order mark are syntax errors, invalid
+UTF-8 inside a string becomes U+FFFD per byte, and a failure raises
+``ValueError`` with the message Go's scanner gives (``invalid character 'x'
+looking for beginning of value``, ``unexpected end of JSON input``), found by
+re-scanning the input the way ``encoding/json/scanner.go`` does.
 """
 
 import _json
 
-_CONSTANTS = {"-Infinity": float("-inf"), "Infinity": float("inf"), "NaN": float("nan")}
+
+class _GoRejects(Exception):
+    """NaN / Infinity: valid for Python's scanner, not for Go's."""
+
+
+def _reject_constant(name):
+    raise _GoRejects(name)
 
 
 class _Context:
@@ -19,7 +32,7 @@ class _Context:
         self.object_pairs_hook = None
         self.parse_float = float
         self.parse_int = parse_int
-        self.parse_constant = _CONSTANTS.__getitem__
+        self.parse_constant = _reject_constant
         self.memo = {}
 
 
@@ -27,25 +40,226 @@ _scanners = {}
 _WS = " \t\n\r"
 
 
+def _text(s):
+    """str of the input; invalid UTF-8 bytes become one U+FFFD each, as Go's
+    decoder replaces them."""
+    if not isinstance(s, (bytes, bytearray)):
+        return s
+    try:
+        return bytes(s).decode("utf-8")
+    except UnicodeDecodeError:
+        t = bytes(s).decode("utf-8", "surrogateescape")
+        return "".join("\ufffd" if "\udc80" <= c <= "\udcff" else c for c in t)
+
+
 def loads(s, parse_int=int):
-    if isinstance(s, (bytes, bytearray)):
-        s = s.decode("utf-8-sig" if s[:3] == b"\xef\xbb\xbf" else "utf-8")
+    text = _text(s)
     scan = _scanners.get(parse_int)
     if scan is None:
         scan = _scanners[parse_int] = _json.make_scanner(_Context(parse_int))
-    i, n = 0, len(s)
-    while i < n and s[i] in _WS:
+    i, n = 0, len(text)
+    while i < n and text[i] in _WS:
         i += 1
     try:
-        obj, end = scan(s, i)
-    except StopIteration as e:
-        raise ValueError("Expecting value: char %d" % e.value) from None
-    while end < n and s[end] in _WS:
-        end += 1
-    if end != n:
-        raise ValueError("Extra data: char %d" % end)
+        obj, end = scan(text, i)
+        while end < n and text[end] in _WS:
+            end += 1
+        if end != n:
+            raise ValueError("extra data")
+    except (StopIteration, ValueError, _GoRejects, RecursionError):
+        raw = s if isinstance(s, (bytes, bytearray)) else s.encode("utf-8", "surrogatepass")
+        raise ValueError(go_syntax_error(bytes(raw)) or "invalid JSON") from None
     return obj
 
 
 def load(f, parse_int=int):
     return loads(f.read(), parse_int)
+
+
+# ---------------------------------------------------------------------------
+# Go's scanner, for the error text only
+# ---------------------------------------------------------------------------
+
+def _quote_char(c):
+    """``quoteChar`` of encoding/json: the byte as a Go character literal."""
+    if c == 0x27:
+        return "'\\''"
+    if c == 0x22:
+        return "'\"'"
+    from .log import go_quote
+    return "'" + go_quote(chr(c))[1:-1] + "'"
+
+
+_SPACE = b" \t\r\n"
+_DIGITS = b"0123456789"
+_HEX = b"0123456789abcdefABCDEF"
+_MAX_DEPTH = 10000
+
+
+def go_syntax_error(data):
+    """The ``SyntaxError`` text ``json.Unmarshal`` returns for ``data``, or
+    None when Go's scanner accepts it."""
+    stack = []          # "obj" / "arr": what the value being scanned belongs to
+    i, n = 0, len(data)
+
+    def err(c, context):
+        return "invalid character %s %s" % (_quote_char(c), context)
+
+    # state: "value" (begin value), "value_or_close" (after '['), "key_or_close"
+    # (after '{'), "key" (after ','), "colon" (after a key), "end" (after a value)
+    state = "value"
+    while True:
+        if state in ("value", "value_or_close", "key_or_close", "key", "colon", "end"):
+            while i < n and data[i] in _SPACE:
+                i += 1
+            if i >= n:
+                if state == "end" and not stack:
+                    return None
+                return "unexpected end of JSON input"
+            c = data[i]
+        if state == "value_or_close":
+            if c == 0x5D:   # ]
+                i += 1
+                stack.pop()
+                state = "end"
+                continue
+            state = "value"
+        if state == "key_or_close":
+            if c == 0x7D:   # }
+                i += 1
+                stack.pop()
+                state = "end"
+                continue
+            state = "key"
+        if state == "key":
+            if c != 0x22:
+                return err(c, "looking for beginning of object key string")
+            r = _scan_string(data, i + 1)
+            if isinstance(r, str):
+                return r
+            i = r
+            state = "colon"
+            continue
+        if state == "colon":
+            if c != 0x3A:
+                return err(c, "after object key")
+            i += 1
+            state = "value"
+            continue
+        if state == "end":
+            if not stack:
+                return err(c, "after top-level value")
+            if stack[-1] == "obj":
+                if c == 0x2C:
+                    i += 1
+                    state = "key"
+                    continue
+                if c == 0x7D:
+                    i += 1
+                    stack.pop()
+                    continue
+                return err(c, "after object key:value pair")
+            if c == 0x2C:
+                i += 1
+                state = "value"
+                continue
+            if c == 0x5D:
+                i += 1
+                stack.pop()
+                continue
+            return err(c, "after array element")
+        # state == "value"
+        if c in (0x7B, 0x5B):
+            if len(stack) >= _MAX_DEPTH:
+                return "exceeded max depth"
+            stack.append("obj" if c == 0x7B else "arr")
+            i += 1
+            state = "key_or_close" if c == 0x7B else "value_or_close"
+            continue
+        if c == 0x22:
+            r = _scan_string(data, i + 1)
+            if isinstance(r, str):
+                return r
+            i = r
+        elif c == 0x2D or c in _DIGITS:
+            r = _scan_number(data, i)
+            if isinstance(r, str):
+                return r
+            i = r
+        elif c in b"tfn":
+            word = {0x74: b"true", 0x66: b"false", 0x6E: b"null"}[c]
+            for j in range(1, len(word)):
+                if i + j >= n:
+                    return "unexpected end of JSON input"
+                if data[i + j] != word[j]:
+                    return err(data[i + j], "in literal %s (expecting %s)" % (word.decode(), _quote_char(word[j])))
+            i += len(word)
+        else:
+            return err(c, "looking for beginning of value")
+        state = "end"
+
+
+def _scan_string(data, i):
+    """Index after the closing quote of a string whose body starts at i, or
+    the error text."""
+    n = len(data)
+    while i < n:
+        c = data[i]
+        if c == 0x22:
+            return i + 1
+        if c == 0x5C:
+            i += 1
+            if i >= n:
+                break
+            e = data[i]
+            if e == 0x75:   # u
+                for j in range(1, 5):
+                    if i + j >= n:
+                        return "unexpected end of JSON input"
+                    if data[i + j] not in _HEX:
+                        return "invalid character %s in \\u hexadecimal character escape" % _quote_char(data[i + j])
+                i += 5
+                continue
+            if e not in b'bfnrt\\/"':
+                return "invalid character %s in string escape code" % _quote_char(e)
+            i += 1
+            continue
+        if c < 0x20:
+            return "invalid character %s in string literal" % _quote_char(c)
+        i += 1
+    return "unexpected end of JSON input"
+
+
+def _scan_number(data, i):
+    """Index after a number starting at i, or the error text."""
+    n = len(data)
+    if data[i] == 0x2D:
+        i += 1
+        if i >= n:
+            return "unexpected end of JSON input"
+        if data[i] not in _DIGITS:
+            return "invalid character %s in numeric literal" % _quote_char(data[i])
+    if data[i] == 0x30:
+        i += 1
+    else:
+        while i < n and data[i] in _DIGITS:
+            i += 1
+    if i < n and data[i] == 0x2E:
+        i += 1
+        if i >= n:
+            return "unexpected end of JSON input"
+        if data[i] not in _DIGITS:
+            return "invalid character %s after decimal point in numeric literal" % _quote_char(data[i])
+        while i < n and data[i] in _DIGITS:
+            i += 1
+    if i < n and data[i] in b"eE":
+        i += 1
+        if i < n and data[i] in b"+-":
+            i += 1
+        if i >= n:
+            return "unexpected end of JSON input"
+        if data[i] not in _DIGITS:
+            return "invalid character %s in exponent of numeric literal" % _quote_char(data[i])
+        while i < n and data[i] in _DIGITS:
+            i += 1
+    return i

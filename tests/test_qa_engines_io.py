@@ -90,8 +90,14 @@ def test_rest_engine_concurrent_gets_and_bad_requests():
         for g in getters:
             g.join(20)
         assert seen == ["first"] * 4
-        assert _post(e.port, "/problems/current/solution", "{not json")[0] == 500
-        assert _post(e.port, "/problems/current/solution", '[1, 2]')[0] == 500
+        # json.Unmarshal(body, &sol []string) errors, http.Error text (httprestengine.go)
+        pre = "Error in un-marshalling solution in QA engine: "
+        assert _post(e.port, "/problems/current/solution", "{not json") == \
+            (500, pre + "invalid character 'n' looking for beginning of object key string\n")
+        assert _post(e.port, "/problems/current/solution", '[1, 2]') == \
+            (500, pre + "json: cannot unmarshal number into Go value of type string\n")
+        assert _post(e.port, "/problems/current/solution", '{"a": "b"}') == \
+            (500, pre + "json: cannot unmarshal object into Go value of type []string\n")
         assert _post(e.port, "/problems/current/solution", '["one"]')[0] == 200
         assert json.loads(_get(e.port, "/problems/current")[1])["description"] == "second"
         assert _post(e.port, "/problems/current/solution", '["two"]')[0] == 200
