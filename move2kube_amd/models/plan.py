@@ -230,18 +230,27 @@ class Service:
         """Fill ``repo_info`` from the git repo containing ``path`` (plan.go:218-247).
 
         Returns (found_repo, error)."""
+        import stat
         from ..utils import git
         try:
-            if not os.path.isdir(path):
-                path = os.path.dirname(path)
+            st = os.stat(path)
         except OSError as e:
+            log.error("Failed to stat the path %r Error %r", path, common.go_path_error(e, "stat"))
             return False, e
+        if not stat.S_ISDIR(st.st_mode):
+            parent = common.go_dir(path)
+            log.debug("The path %r is not a directory. Using %r instead.", path, parent)
+            path = parent
         preferred = "upstream"
+        err = None
         try:
             remotes = git.remote_names(path)
-        except git.GitError:
-            remotes = []
-        if remotes and not common.is_string_present(remotes, preferred):
+        except git.GitError as e:
+            remotes, err = [], e
+        if err is not None or not remotes:
+            # %q of a nil error prints %!q(<nil>)
+            log.debug("No remotes found at path %r Error: %s", path, log.go_quote(str(err)) if err else "%!q(<nil>)")
+        elif not common.is_string_present(remotes, preferred):
             preferred = "origin" if common.is_string_present(remotes, "origin") else remotes[0]
         try:
             urls, branch, repo_dir = git.repo_details(path, preferred)
@@ -249,7 +258,9 @@ class Service:
             log.debug("Failed to get the git repo at path %r Error: %r", path, str(e))
             return False, e
         self.repo_info.git_repo_branch = branch
-        if urls:
+        if not urls:
+            log.debug("The git repo at path %r has no remotes set.", path)
+        else:
             self.repo_info.git_repo_url = urls[0]
         self.repo_info.git_repo_dir = repo_dir
         return True, None
@@ -380,7 +391,10 @@ class Plan:
     def add_services_to_plan(self, services):
         """``Plan.AddServicesToPlan`` (plan.go:373-396)."""
         for service in services:
-            existing = self.services.setdefault(service.service_name, [])
+            existing = self.services.get(service.service_name)
+            if existing is None:
+                existing = self.services[service.service_name] = []
+                log.debug("Added new service to plan : %s", service.service_name)
             merged = False
             for es in existing:
                 if es.merge(service):
@@ -393,6 +407,8 @@ class Plan:
         if abs_path == "":
             return abs_path
         if not os.path.isabs(abs_path):
+            log.debug("The input path %r is not an absolute path. Cannot make it relative to the root directory.",
+                      abs_path)
             return abs_path
         if is_assets_path(abs_path):
             return common.go_rel(settings.temp_path, abs_path)
@@ -402,6 +418,7 @@ class Plan:
         if rel_path == "":
             return rel_path
         if os.path.isabs(rel_path):
+            log.debug("The input path %r is not an relative path. Cannot make it absolute.", rel_path)
             return rel_path
         if is_assets_path(rel_path):
             return common.go_join(settings.temp_path, rel_path)
@@ -449,8 +466,11 @@ def new_plan():
 
 def read_plan(path):
     """Read a plan converting relative paths to absolute (planutils.go:165-178)."""
-    data = common.read_move2kube_yaml(path)
-    plan = Plan.from_yaml(data)
+    try:
+        plan = Plan.from_yaml(common.read_move2kube_yaml(path))
+    except Exception as e:  # noqa: BLE001 - logged like ReadPlan, then returned to the caller
+        log.error("Failed to load the plan file at path %r Error %r", path, str(e))
+        raise
     plan.root_dir = common.go_abs(plan.root_dir) if plan.root_dir else os.getcwd()
     _convert_paths(plan, plan.get_absolute_path)
     return plan
