@@ -57,6 +57,14 @@ class Problem:
         self.answer = answer
         self.resolved = resolved
 
+    def go_s(self):
+        """fmt ``%s`` of the Go struct (ints and bools print as ``%!s(...)``)."""
+        def lst(xs):
+            return "[" + " ".join(xs or ()) + "]"
+        return "{%%!s(int=%d) %s %s {%s %s %s %s} %%!s(bool=%s)}" % (
+            self.id, self.desc, lst(self.context), self.type, lst(self.default), lst(self.options),
+            lst(self.answer), "true" if self.resolved else "false")
+
     def copy(self):
         return Problem(self.id, self.desc, list(self.context), self.type, list(self.default),
                        list(self.options), None if self.answer is None else list(self.answer), self.resolved)
@@ -484,7 +492,11 @@ class Cache:
 
     def load(self):
         """Load and merge the cache file (cache.go:45-60)."""
-        data = common.read_move2kube_yaml(self.file)
+        try:
+            data = common.read_move2kube_yaml(self.file)
+        except Exception as e:  # noqa: BLE001 - logged, then returned to StartEngine
+            log.error("Unable to load cache : %s", e)
+            raise
         other = Cache.from_yaml(data, self.file)
         self._merge(other)
         for p in self.problems:

@@ -7,8 +7,16 @@ from .engine import Engine
 
 
 class CacheEngine(Engine):
+    go_type = "*qaengine.CacheEngine"
+
     def __init__(self, cache_file):
         self.cache = qa.Cache(cache_file)
+
+    def go_s(self):
+        """``%s`` of ``*CacheEngine``: its Cache struct, problems and all."""
+        c = self.cache
+        return "&{{{%s %s} {%s} {%s [%s]}}}" % (qa.SCHEME_GROUP_VERSION, qa.QACACHE_KIND, "", c.file,
+                                                " ".join(p.go_s() for p in c.problems))
 
     def start_engine(self):
         self.cache.load()

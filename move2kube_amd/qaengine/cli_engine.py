@@ -20,6 +20,7 @@ from .engine import Engine
 
 
 class CliEngine(Engine):
+    go_type = "*qaengine.CliEngine"
     interactive = True  # may block on a person: the write cache is flushed first
 
     def __init__(self, stdin=None, stdout=None):

@@ -9,6 +9,7 @@ from .engine import Engine
 
 
 class DefaultEngine(Engine):
+    go_type = "*qaengine.DefaultEngine"
     def fetch_answer(self, prob):
         if prob.type == qa.PASSWORD and not prob.default:
             prob.set_answer([""])

@@ -35,6 +35,13 @@ MAX_LAST_ENGINE_RETRIES = 8
 
 
 class Engine:
+    # how the reference's log lines print the engine: %T, and %s of the
+    # pointer (``&{...}``: every field with the verb applied)
+    go_type = "*qaengine.Engine"
+
+    def go_s(self):
+        return "&{}"
+
     def start_engine(self):
         pass
 
@@ -78,7 +85,7 @@ def add_engine(e):
     try:
         e.start_engine()
     except Exception as ex:  # noqa: BLE001
-        log.error("Ignoring engine %r due to error : %s", e, ex)
+        log.error("Ignoring engine %s due to error : %s", e.go_type, ex)
         return
     with _lock:
         _engines.append(e)
@@ -92,7 +99,7 @@ def add_caches(cache_files):
         try:
             e.start_engine()
         except Exception as ex:  # noqa: BLE001
-            log.error("Ignoring engine %r due to error : %s", e, ex)
+            log.error("Ignoring engine %s due to error : %s", e.go_type, ex)
             continue
         new.append(e)
     with _lock:
@@ -116,7 +123,7 @@ def fetch_answer(prob):
             err = None
         except Exception as ex:  # noqa: BLE001
             err = ex
-            log.warning("Error while fetching answer using engine %r : %s", e, ex)
+            log.warning("Error while fetching answer using engine %s : %s", e.go_s(), ex)
             continue
         if ans.resolved:
             break

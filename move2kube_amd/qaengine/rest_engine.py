@@ -61,6 +61,7 @@ def _string_slice(v):
     return ["" if x is None else x for x in v]
 
 class HTTPRESTEngine(Engine):
+    go_type = "*qaengine.HTTPRESTEngine"
     interactive = True  # may block on a person: the write cache is flushed first
 
     def __init__(self, port=0, host=""):
@@ -74,6 +75,12 @@ class HTTPRESTEngine(Engine):
         self.answers = queue.Queue()
         self.server = None
         self.thread = None
+
+    def go_s(self):
+        """``%s`` of ``*HTTPRESTEngine`` (the two channel fields print as
+        addresses in the reference; these are placeholders)."""
+        chan = "%!s(chan qaengine.Problem=0xc000000000)"
+        return "&{%%!s(int=%d) %s %s %s}" % (self.port, self.current.go_s(), chan, chan)
 
     def start_engine(self):
         if self.port == 0:

@@ -51,11 +51,16 @@ def translate(plan):
             with trace.span(type(t).__name__, "translate", services=len(valid)):
                 cur = t.translate(valid, plan)
         except Exception as e:  # noqa: BLE001
+            # the counts are logged before the error check (translator.go:58-64)
+            log.debug("Services translated : %d", 0)
+            log.debug("Containers translated : %d", 0)
             log.warning("[%r] Failed : %s", t, e)
             continue
         log.debug("Services translated : %d", len(cur.services))
         log.debug("Containers translated : %d", len(cur.containers))
         log.info("[%r] Done", t)
         ir.merge(cur)
+        log.debug("Total Services after translation : %d", len(ir.services))
+        log.debug("Total Containers after translation : %d", len(ir.containers))
     log.info("Translation done")
     return ir

@@ -185,3 +185,31 @@ def test_pending_answers_dropped_when_output_is_removed(tmp_path):
     qaengine.fetch_answer(qa.new_input_problem("q2", [], "b"))
     qaengine.flush_write_cache()
     assert _cache_answers(cache) == ["q1", "q2"]
+
+
+def test_engines_print_like_go_values(tmp_path, capsys):
+    """engine.go logs an engine with %T ("Ignoring engine") and %s ("Error
+    while fetching answer using engine &{...}": the Cache struct with every
+    problem, ints and bools as %!s(...))."""
+    import logparse
+    from move2kube_amd.models import qa
+    from move2kube_amd.qaengine import engine as eng
+    from move2kube_amd.qaengine.cache_engine import CacheEngine
+    from move2kube_amd.qaengine.default_engine import DefaultEngine
+    from move2kube_amd.utils import log
+    log.set_verbose(False)
+    cf = tmp_path / "c.yaml"
+    cf.write_text("apiVersion: move2kube.konveyor.io/v1alpha1\nkind: QACache\nspec:\n  solutions:\n"
+                  "    - description: Pick one\n      solution:\n        type: Select\n        default:\n          - a\n"
+                  "        options:\n          - a\n          - b\n        answer:\n          - b\n")
+    ce = CacheEngine(str(cf))
+    ce.start_engine()
+    assert ce.go_s() == ("&{{{move2kube.konveyor.io/v1alpha1 QACache} {} {%s [{%%!s(int=0) Pick one [] {Select [a] "
+                         "[a b] [b]} %%!s(bool=true)}]}}}" % cf)
+    assert DefaultEngine().go_s() == "&{}"
+    eng.add_engine(CacheEngine(str(tmp_path / "missing.yaml")))
+    err = capsys.readouterr().err
+    msgs = logparse.messages(err)
+    assert msgs[0][0] == "error" and msgs[0][1].startswith("Unable to load cache : ")
+    assert msgs[1][0] == "error" and msgs[1][1].startswith("Ignoring engine *qaengine.CacheEngine due to error : ")
+    assert qa.Problem(id=3, desc="d", type="Input", answer=None).go_s() == "{%!s(int=3) d [] {Input [] [] []} %!s(bool=false)}"
