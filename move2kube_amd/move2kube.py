@@ -291,7 +291,7 @@ def _emit_artifacts(p, ir, outpath, qadisablecli):
     except Exception as e:  # noqa: BLE001
         if isinstance(e, log.FatalError):
             raise
-        log.error("Unable to write docker compose objects : %s", e)
+        log.error("Error during translate docker compose file : %s", e)
     else:
         later(write_compose)
 
@@ -317,7 +317,7 @@ def _emit_artifacts(p, ir, outpath, qadisablecli):
             except Exception as e:  # noqa: BLE001
                 if isinstance(e, log.FatalError):
                     raise
-                log.error("Unable to write the CI/CD artifacts to files. Error: %r", str(e))
+                log.error("Error while genrationg CI/CD resource fomr the IR. Error: %r", str(e))  # sic
             else:
                 later(write_cicd)
 
