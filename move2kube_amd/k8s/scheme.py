@@ -129,24 +129,68 @@ def decode(data, scheme="k8s"):
         raise DecodeError("document nested too deeply") from None
 
 
+# runtime.NewScheme() names a scheme after its call site
+# (naming.GetNameFromCallsite); the reference's schemes are created at these
+# lines.  The path prefix depends on where the binary was built (parity unpinned).
+_SCHEME_NAMES = {"k8s": "github.com/konveyor/move2kube/internal/apiresourceset/k8sapiresourceset.go:46",
+                 "knative": "github.com/konveyor/move2kube/internal/apiresourceset/knativeapiresourceset.go:39"}
+_FIND_KIND = ('struct { APIVersion string "json:\\"apiVersion,omitempty\\""; '
+              'Kind string "json:\\"kind,omitempty\\"" }')
+
+
+def _json_kind(v):
+    if isinstance(v, bool):
+        return "bool"
+    if isinstance(v, (int, float)):
+        return "number"
+    if isinstance(v, str):
+        return "string"
+    return "array" if isinstance(v, list) else "object"
+
+
+def _interpret(obj):
+    """``SimpleMetaFactory.Interpret``: apiVersion and kind through
+    json.Unmarshal into a two-field struct (the first type error in document
+    order), then ``schema.ParseGroupVersion``."""
+    pre = "couldn't get version/kind; json parse error: "
+    if obj is None:
+        return "", ""
+    if not isinstance(obj, dict):
+        raise DecodeError(pre + "json: cannot unmarshal %s into Go value of type %s" % (_json_kind(obj), _FIND_KIND))
+    for key in obj:
+        if key in ("apiVersion", "kind"):
+            v = obj[key]
+            if v is not None and not isinstance(v, str):
+                raise DecodeError(pre + "json: cannot unmarshal %s into Go struct field .%s of type string"
+                                  % (_json_kind(v), key))
+    gv = obj.get("apiVersion") or ""
+    if gv.count("/") > 1:
+        raise DecodeError("unexpected GroupVersion string: %s" % gv)
+    return gv, obj.get("kind") or ""
+
+
 def _decode(data, scheme):
+    """The YAML serializer's ``Decode`` (apimachinery v0.19.4
+    ``runtime/serializer/json``) for the reference's schemes, with its error
+    texts: a YAML error, ``Interpret``, ``Object 'Kind' is missing in
+    '<input>'``, ``Object 'apiVersion' is missing in '<input>'``, a kind the
+    scheme does not register."""
+    text = data.decode("utf-8", "surrogateescape") if isinstance(data, bytes) else data
     try:
-        text = data.decode("utf-8", "surrogateescape") if isinstance(data, bytes) else data
         # sigs.k8s.io/yaml converts YAML to JSON with go-yaml v2 scalars
         docs = yamlio.load_all_v2(text)
     except (yamlio.YAMLError, ValueError) as e:
-        raise DecodeError("yaml: %s" % e)
+        raise DecodeError("error converting YAML to JSON: %s" % e)
     obj = docs[0] if docs else None
-    if not isinstance(obj, dict):
-        raise DecodeError("Object 'Kind' is missing")
-    kind = obj.get("kind")
-    gv = obj.get("apiVersion")
-    if not kind or not isinstance(kind, str):
-        raise DecodeError("Object 'Kind' is missing in %r" % (str(obj)[:80],))
-    if not isinstance(gv, str) or not gv:
-        raise DecodeError("Object 'apiVersion' is missing")
+    gv, kind = _interpret(obj)
+    if not kind:
+        raise DecodeError("Object 'Kind' is missing in '%s'" % text)
+    version = gv.rsplit("/", 1)[-1] if gv else ""
+    if not version:
+        raise DecodeError("Object 'apiVersion' is missing in '%s'" % text)
     if not is_registered(gv, kind, scheme):
-        raise DecodeError('no kind "%s" is registered for version "%s" in scheme' % (kind, gv))
+        raise DecodeError('no kind "%s" is registered for version "%s" in scheme "%s"'
+                          % (kind, gv, _SCHEME_NAMES.get(scheme, _SCHEME_NAMES["k8s"])))
     md = obj.get("metadata")
     if md is not None and not isinstance(md, dict):
         raise DecodeError("metadata must be an object")

@@ -27,17 +27,28 @@ def get_loaders():
 
 
 def _read_cluster_metadata(path):
-    data = common.read_move2kube_yaml(path)
+    """``getClusterMetadata`` (clustermdloader.go:121-133)."""
+    try:
+        data = common.read_move2kube_yaml(path)
+    except Exception as e:  # noqa: BLE001
+        log.debug("Failed to read the cluster metadata at path %r Error: %r", path, str(e))
+        raise
     cm = collection.ClusterMetadata.from_yaml(data)
     if cm.kind != collection.CLUSTER_METADATA_KIND:
-        raise ValueError("The file at path %r is not a valid cluster metadata. Expected kind: %s Actual kind: %s"
-                         % (path, collection.CLUSTER_METADATA_KIND, cm.kind))
+        err = ValueError("The file at path %s is not a valid cluster metadata. Expected kind: %s Actual kind: %s"
+                         % (log.go_quote(path), collection.CLUSTER_METADATA_KIND, cm.kind))
+        log.debug(str(err))
+        raise err
     return cm
 
 
 class ClusterMDLoader(Loader):
     def update_plan(self, input_path, plan):
-        files = common.get_files_by_ext(input_path, [".yml", ".yaml"])
+        try:
+            files = common.get_files_by_ext(input_path, [".yml", ".yaml"])
+        except (OSError, ValueError) as e:
+            log.warning("Failed to fetch the cluster metadata yamls at path %r Error: %r", input_path, str(e))
+            raise
         for f in files:
             try:
                 cm = _read_cluster_metadata(f)
@@ -56,8 +67,10 @@ class ClusterMDLoader(Loader):
             log.warning("Neither type nor path is specified for the target cluster. Going with the default cluster type: %s",
                         DEFAULT_CLUSTER_TYPE)
             ttype = DEFAULT_CLUSTER_TYPE
+        target = "{%s %s}" % (ttype, tpath)   # %v of the TargetCluster struct
         if ttype and tpath:
-            raise ValueError("Only one of type or path should be specified for the target cluster.")
+            raise ValueError("Only one of type or path should be specified for the target cluster. Target cluster: %s"
+                             % target)
         key = tpath if tpath else ttype
         cm = clusters.get(key)
         if cm is None and tpath and settings.fixed:
@@ -68,7 +81,7 @@ class ClusterMDLoader(Loader):
             except Exception:  # noqa: BLE001
                 cm = None
         if cm is None:
-            raise ValueError("The requested target cluster %r was not found" % key)
+            raise ValueError("The requested target cluster %s was not found" % target)
         ir.target_cluster_spec = cm.spec.copy()
 
     @staticmethod
@@ -81,6 +94,7 @@ class ClusterMDLoader(Loader):
             cm.spec = collection.ClusterMetadataSpec(prof["storageClasses"], prof["apiKindVersionMap"])
             if not cm.spec.storage_classes:
                 cm.spec.storage_classes = [DEFAULT_STORAGE_CLASS_NAME]
+                log.debug("No storage class in the cluster %s, adding [default] storage class", name)
             clusters[cm.name] = cm
         for p in plan.target_info_artifacts.get(plantypes.K8S_CLUSTER_ARTIFACT) or []:
             try:
@@ -90,16 +104,27 @@ class ClusterMDLoader(Loader):
                 continue
             if not cm.spec.storage_classes:
                 cm.spec.storage_classes = [DEFAULT_STORAGE_CLASS_NAME]
+                log.debug("No storage class in the cluster %s at path %r, adding [default] storage class", cm.name, p)
             clusters[cm.name] = cm
         return clusters
 
 
 class K8sFilesLoader(Loader):
     def update_plan(self, input_path, plan):
-        for f in common.get_files_by_ext(input_path, [".yml", ".yaml"]):
+        try:
+            files = common.get_files_by_ext(input_path, [".yml", ".yaml"])
+        except (OSError, ValueError) as e:
+            log.error("Unable to fetch yaml files at path %r Error: %r", input_path, str(e))
+            raise
+        for f in files:
             try:
-                scheme.decode_file(f, "k8s")
-            except (OSError, scheme.DecodeError) as e:
+                data = common.read_bytes(f)
+            except OSError as e:
+                log.debug("Failed to read the yaml file at path %r Error: %r", f, common.go_path_error(e, "open"))
+                continue
+            try:
+                scheme.decode(data, "k8s")
+            except scheme.DecodeError as e:
                 log.debug("Failed to decode the file at path %r as a k8s file. Error: %r", f, str(e))
                 continue
             plan.k8s_files.append(f)
@@ -107,8 +132,13 @@ class K8sFilesLoader(Loader):
     def load_to_ir(self, plan, ir):
         for f in plan.k8s_files:
             try:
-                obj = scheme.decode_file(f, "k8s")
-            except (OSError, scheme.DecodeError) as e:
+                data = common.read_bytes(f)
+            except OSError as e:
+                log.error("Failed to read the k8s file at path %r Error: %r", f, common.go_path_error(e, "open"))
+                continue
+            try:
+                obj = scheme.decode(data, "k8s")
+            except scheme.DecodeError as e:
                 log.error("Failed to decode the file at path %r as a k8s file. Error: %r", f, str(e))
                 continue
             ir.cached_objects.append(obj)
@@ -116,10 +146,16 @@ class K8sFilesLoader(Loader):
 
 class QACacheLoader(Loader):
     def update_plan(self, input_path, plan):
-        for f in common.get_files_by_ext(input_path, [".yml", ".yaml"]):
+        try:
+            files = common.get_files_by_ext(input_path, [".yml", ".yaml"])
+        except (OSError, ValueError) as e:
+            log.error("Unable to fetch yaml files at path %r Error: %r", input_path, str(e))
+            raise
+        for f in files:
             try:
                 data = common.read_move2kube_yaml(f)
-            except Exception:  # noqa: BLE001
+            except Exception as e:  # noqa: BLE001
+                log.debug("Failed to read the yaml file at path %r Error: %r", f, str(e))
                 continue
             if not isinstance(data, dict) or data.get("kind") != qa.QACACHE_KIND:
                 continue

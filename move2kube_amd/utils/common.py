@@ -213,22 +213,41 @@ def read_move2kube_yaml(path, raw=True):
     Checks that ``apiVersion``'s group is ``move2kube.konveyor.io`` and warns on a
     version mismatch (``internal/common/utils.go:210-251``).  Returns the decoded
     document (scalars kept as raw strings when ``raw``)."""
-    text = read_text(path)
-    data = yamlio.load(text)
+    try:
+        text = read_text(path)
+    except OSError as e:
+        log.debug("Failed to read the yaml file at path %s Error: %r", path, go_path_error(e, "open"))
+        raise
+    try:
+        data = yamlio.load(text)
+    except yamlio.YAMLError as e:
+        log.debug("Error occurred while unmarshalling yaml file at path %s Error: %r", path, str(e))
+        raise
+    if data is None:
+        data = {}
     if not isinstance(data, dict):
-        raise Move2KubeYamlError("The file at path %s is not a yaml mapping" % path)
-    gv = data.get("apiVersion")
-    if gv is None:
-        raise Move2KubeYamlError("Did not find apiVersion in the yaml file at path %s" % path)
+        err = Move2KubeYamlError(yamlio.go_unmarshal_type_error(text, data))
+        log.debug("Error occurred while unmarshalling yaml file at path %s Error: %r", path, str(err))
+        raise err
+    if "apiVersion" not in data:
+        err = Move2KubeYamlError("Did not find apiVersion in the yaml file at path %s" % path)
+        log.debug(str(err))
+        raise err
+    gv = data["apiVersion"]
     if not isinstance(gv, str):
-        raise Move2KubeYamlError("The apiVersion is not a string in the yaml file at path %s" % path)
+        err = Move2KubeYamlError("The apiVersion is not a string in the yaml file at path %s" % path)
+        log.debug(str(err))
+        raise err
     try:
         group, version = parse_group_version(gv)
     except ValueError as e:
+        log.debug("Failed to parse the apiVersion %s Error: %r", gv, str(e))
         raise Move2KubeYamlError(str(e))
     if group != GROUP_NAME:
-        raise Move2KubeYamlError("The file at path %s doesn't have the correct group. Expected group %s Actual group %s"
+        err = Move2KubeYamlError("The file at path %s doesn't have the correct group. Expected group %s Actual group %s"
                                  % (path, GROUP_NAME, group))
+        log.debug(str(err))
+        raise err
     if version != SCHEME_VERSION:
         log.warning("The file at path %s was generated using a different version. File version is %s and move2kube version is %s",
                     path, version, SCHEME_VERSION)

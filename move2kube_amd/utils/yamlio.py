@@ -985,6 +985,30 @@ def _go_quote(s):
     return go_quote(s)
 
 
+_SHORT_TAGS = {bool: "!!bool", int: "!!int", float: "!!float", str: "!!str", list: "!!seq"}
+
+
+def go_unmarshal_type_error(text, value, into="map[string]interface {}"):
+    """go-yaml v3's ``yaml: unmarshal errors:`` text for a document whose
+    top-level node (decoded here as ``value``) cannot go into ``into``: the
+    node's line, short tag and, for a scalar, its text (``decoder.terror``)."""
+    import yaml
+    line, raw = 1, ""
+    try:
+        node = yaml.compose(text, Loader=getattr(yaml, "CSafeLoader", yaml.SafeLoader))
+    except yaml.YAMLError:
+        node = None
+    if node is not None:
+        line = node.start_mark.line + 1
+        if isinstance(node, yaml.ScalarNode):
+            raw = node.value
+    tag = _SHORT_TAGS.get(type(value), "!!str")
+    shown = ""
+    if tag != "!!seq":
+        shown = " `" + (raw[:7] + "..." if len(raw) > 10 else raw) + "`"
+    return "yaml: unmarshal errors:\n  line %d: cannot unmarshal %s%s into %s" % (line, tag, shown, into)
+
+
 def _pyyaml_load(loader_cls, text, multi):
     """``yaml.load_all``, or for a single load the first document only (go-yaml's
     ``Unmarshal`` decodes the first document of a stream and never reads the

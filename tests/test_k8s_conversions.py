@@ -210,3 +210,24 @@ def test_fixed_mode_reshapes_and_fills_selector():
     role = {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": "r"}, "rules": []}
     with pytest.raises(convert.ConversionError):
         convert.convert_fixed(role, "authorization.openshift.io/v1")
+
+
+@pytest.mark.parametrize("text,msg", [
+    ("version: 3\nservices: {}\n", "Object 'Kind' is missing in 'version: 3\nservices: {}\n'"),
+    ("", "Object 'Kind' is missing in ''"),
+    ("kind: Pod\n", "Object 'apiVersion' is missing in 'kind: Pod\n'"),
+    ("- a\n", "couldn't get version/kind; json parse error: json: cannot unmarshal array into Go value of type "
+              'struct { APIVersion string "json:\\"apiVersion,omitempty\\""; Kind string "json:\\"kind,omitempty\\"" }'),
+    ("kind: 5\n", "couldn't get version/kind; json parse error: json: cannot unmarshal number into Go struct field "
+                  ".kind of type string"),
+    ("apiVersion: a/b/c\nkind: Pod\n", "unexpected GroupVersion string: a/b/c"),
+    ("apiVersion: v1\nkind: Foo\n", 'no kind "Foo" is registered for version "v1" in scheme '
+                                    '"github.com/konveyor/move2kube/internal/apiresourceset/k8sapiresourceset.go:46"'),
+])
+def test_decode_errors_read_like_the_universal_deserializer(text, msg):
+    """The YAML serializer's Decode (apimachinery v0.19.4): what the planners
+    log at debug level for every YAML file that is not a Kubernetes object."""
+    from move2kube_amd.k8s import scheme
+    with pytest.raises(scheme.DecodeError) as ei:
+        scheme.decode(text)
+    assert str(ei.value) == msg
