@@ -40,16 +40,6 @@ def get_hash(data):
     return common.fnv64a(data.encode() if isinstance(data, str) else data)
 
 
-def check_for_dockerfile(path):
-    if not os.path.exists(path):
-        log.error("There is no file at path %s", path)
-        return False
-    if os.path.isdir(path):
-        log.error("The path %s points to a directory. Expected a Dockerfile.", path)
-        return False
-    return True
-
-
 # ---------------------------------------------------------------------------
 # Go value parsers
 # ---------------------------------------------------------------------------
@@ -234,26 +224,35 @@ def resolve_bind_source(src, working_dir):
     return src
 
 
-def command_memo(name, error_type):
+def command_memo(name, error_type, wrap):
     """Memoise a compose-file parser for the enclosing ``fsindex.scope()``
     (one command): the planner tries every YAML file as compose and the
     translator parses the same files again for each of their services.  The
     result depends only on the file, the ``.env``/OS environment and
     ``--ignoreenv``, none of which change within a command.  A parse error
-    (``error_type``) is remembered and raised again."""
+    (``error_type``) is worded with ``wrap % (path, %q of the cause)``,
+    remembered, and logged at debug level on every call as the reference's
+    parser does."""
+    from ...utils.log import go_quote
+
     def deco(fn):
         def checked(path):
             try:
                 return fn(path)
             except RecursionError:  # nested too deeply for the recursive walks: this file only
-                raise error_type("Unable to load Compose file at path %s Error: document nested too deeply"
-                                 % path) from None
+                raise error_type(wrap % (path, go_quote("document nested too deeply"))) from None
+            except error_type as e:
+                raise error_type(wrap % (path, go_quote(str(e)))) from None
 
         @functools.wraps(fn)
         def parse(path):
             cache = fsindex.scoped_cache(name)
             if cache is None:
-                return checked(path)
+                try:
+                    return checked(path)
+                except error_type as e:
+                    log.debug(str(e))
+                    raise
             key = (path, settings.ignore_environment)
             hit = cache.get(key)
             if hit is None:
@@ -264,6 +263,7 @@ def command_memo(name, error_type):
                 cache[key] = hit
             if hit[0]:
                 return hit[1]
+            log.debug(str(hit[1]))
             raise hit[1]
         return parse
     return deco

@@ -49,13 +49,16 @@ def _read_raw(path):
     """``CreateConfig``: the raw document -> (version, raw services, parsed)."""
     try:
         text = common.read_text(path)
+    except OSError as e:
+        raise ComposeError(common.go_path_error(e, "open"))
+    try:
         parsed = yamlio.load_v2(text)
-    except (OSError, yamlio.YAMLError) as e:
-        raise ComposeError("Failed to load docker compose file at path %s Error: %s" % (path, e))
+    except yamlio.YAMLError as e:
+        raise ComposeError(str(e))
     if parsed is None:
-        raise ComposeError("Failed to load docker compose file at path %s Error: empty file" % path)
+        raise ComposeError("empty file %s" % path)
     if not isinstance(parsed, dict):
-        raise ComposeError("Failed to load docker compose file at path %s Error: top-level must be a mapping" % path)
+        raise ComposeError("top-level object of %s must be a mapping" % path)
     version = parsed.get("version")
     if version is not None:
         if isinstance(version, float):
@@ -265,7 +268,7 @@ def _parse_service(svc, in_file, datas, lookup, compose_path, depth=0):
     return merged
 
 
-@cu.command_memo("compose-v1v2", ComposeError)
+@cu.command_memo("compose-v1v2", ComposeError, "Failed to load docker compose file at path %s Error: %s")
 def parse_v2(path):
     """Parse a v1/v2 compose file the way the reference's libcompose
     ``project.Parse()`` does (``v1v2.go:93-129``): interpolation (``.env`` then

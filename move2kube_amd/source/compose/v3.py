@@ -177,14 +177,19 @@ def _check_string_keys(v, prefix):
             _check_string_keys(x, "%s[%d]" % (prefix, i))
 
 
-@cu.command_memo("compose-v3", ComposeError)
+@cu.command_memo("compose-v3", ComposeError, "Unable to load Compose file at path %s Error: %s")
 def parse_v3(path):
-    """Parse and load a v3 compose file -> normalized config dict."""
+    """Parse and load a v3 compose file -> normalized config dict (``ParseV3``,
+    v3.go:93-121: every failure is ``Unable to load Compose file at path <p>
+    Error: <%q of the cause>``, logged at debug level)."""
     try:
         text = common.read_text(path)
+    except OSError as e:
+        raise ComposeError(common.go_path_error(e, "open"))
+    try:
         parsed = yamlio.load_v2(text)
-    except (OSError, yamlio.YAMLError) as e:
-        raise ComposeError("Unable to load Compose file at path %s Error: %s" % (path, e))
+    except yamlio.YAMLError as e:
+        raise ComposeError(str(e))
     if not isinstance(parsed, dict):
         raise ComposeError("Top-level object must be a mapping")
     _check_string_keys(parsed, "")
@@ -344,7 +349,13 @@ def _load_service(name, d, wd, env):
 
 class V3Loader:
     def convert_to_ir(self, composefilepath, plan, service):
-        cfg = parse_v3(composefilepath)
+        log.debug("About to load configuration from docker compose file at path %s", composefilepath)
+        try:
+            cfg = parse_v3(composefilepath)
+        except ComposeError as e:
+            log.warning("Error while loading docker compose config : %s", e)
+            raise
+        log.debug("About to start loading docker compose to intermediate rep")
         return self._convert(os.path.dirname(composefilepath), cfg, plan, service)
 
     def _convert(self, filedir, cfg, plan, service):

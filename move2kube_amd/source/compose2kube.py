@@ -104,6 +104,8 @@ class ComposeTranslator(Translator):
         ir = irtypes.new_ir(plan)
         for service in services:
             if service.translation_type != self.translation_type:
+                log.debug("Expected service to have compose2kube translation type. Got %s . Skipping.",
+                          service.translation_type)
                 continue
             for path in service.source_artifacts.get(plantypes.COMPOSE_FILE_ARTIFACT) or []:
                 log.debug("File %s being loaded from compose service : %s", path, service.service_name)
@@ -111,13 +113,17 @@ class ComposeTranslator(Translator):
                 from .compose.v3 import ComposeError, V3Loader
                 try:
                     cir = V3Loader().convert_to_ir(path, plan, service)
+                    version = "v3"
                 except ComposeError as e3:
                     try:
                         cir = V1V2Loader().convert_to_ir(path, plan, service)
+                        version = "v1v2"
                     except ComposeError as e2:
-                        log.error("Unable to parse the docker compose file at path %s Error V3: %s Error V1V2: %s", path, e3, e2)
+                        log.error("Unable to parse the docker compose file at path %s Error V3: %r Error V1V2: %r",
+                                  path, str(e3), str(e2))
                         continue
                 ir.merge(cir)
+                log.debug("compose %s translator returned %d services", version, len(ir.services))
             for path in service.source_artifacts.get(plantypes.IMAGE_INFO_ARTIFACT) or []:
                 try:
                     im = _read_image_info(path)

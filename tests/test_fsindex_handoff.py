@@ -91,7 +91,7 @@ def test_compose_files_parsed_once_per_command(tmp_path, monkeypatch):
     def counting(path):
         calls.append(path)
         return real(path)
-    monkeypatch.setattr(v3, "parse_v3", v3.cu.command_memo("compose-v3", v3.ComposeError)(counting))
+    monkeypatch.setattr(v3, "parse_v3", v3.cu.command_memo("compose-v3", v3.ComposeError, "%s %s")(counting))
     with api.Session(qaskip=True) as s:
         s.translate(str(src), str(tmp_path / "out"))
     compose_files = [c for c in calls if c.endswith("docker-compose.yaml") or c.endswith("docker-compose.yml")]
