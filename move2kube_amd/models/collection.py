@@ -157,7 +157,18 @@ class ImageInfo:
         return i
 
 
+def _go_list(xs):
+    return "[" + " ".join(str(x) for x in xs) + "]"
+
+
 class CfApplication:
+    def go_plus_v(self):
+        """fmt ``%+v`` of the Go struct."""
+        env = "map[" + " ".join("%s:%s" % (k, self.env[k]) for k in sorted(self.env)) + "]"
+        return ("{Name:%s Buildpack:%s DetectedBuildpack:%s Memory:%d Instances:%d DockerImage:%s Ports:%s Env:%s}"
+                % (self.name, self.buildpack, self.detected_buildpack, self.memory, self.instances, self.docker_image,
+                   _go_list(self.ports), env))
+
     def __init__(self, name=""):
         self.name = name
         self.buildpack = ""
@@ -219,6 +230,10 @@ class CfInstanceApps:
 
 
 class BuildpackContainerizer:
+    def go_plus_v(self):
+        return "{BuildpackName:%s ContainerBuildType:%s ContainerizationTargetOptions:%s}" % (
+            self.buildpack_name, self.container_build_type, _go_list(self.target_options))
+
     def __init__(self, buildpack_name="", container_build_type="", target_options=None):
         self.buildpack_name = buildpack_name
         self.container_build_type = container_build_type

@@ -2,6 +2,12 @@
 ``internal/source/cfmanifest2kube.go:422-489`` on top of the CF CLI
 ``util/manifest`` package and bosh ``((var))`` templates).
 
+Both the CF CLI (``ReadAndInterpolateManifest``) and the reference's own
+reader first run the file through the bosh template, which decodes it with
+go-yaml v2 (YAML 1.1 scalars: ``yes``/``on`` are booleans, ``010`` is octal;
+a repeated key keeps its last value) and marshals it again; the decode here
+is the same v2 one.
+
 ``((var))`` placeholders without a value are reported as missing variables;
 :func:`read_application_manifest` replaces them with ``{{ $var }}`` (Yamls/
 Knative) or ``{{ index  .Values "globalvariables" "var"}}`` (Helm) so the
@@ -11,7 +17,7 @@ generated manifests stay parameterised.
 import re
 
 from ..models import plan as plantypes
-from ..utils import common, yamlio
+from ..utils import common, log, yamlio
 from ..utils.gotemplate import go_sprint
 from ..utils.lazyre import lazy as _lazy_re
 
@@ -103,21 +109,26 @@ def _load(path):
     try:
         text = common.read_text(path)
     except OSError as e:
-        raise ManifestError(str(e))
+        raise ManifestError(common.go_path_error(e, "open"))
     try:
-        return yamlio.load(text)
+        return yamlio.load_v2(text)
     except yamlio.YAMLError as e:
-        raise ManifestError("yaml: %s" % e)
+        raise ManifestError(str(e))
 
 
 def get_missing_variables(path):
-    """Names of ``((vars))`` used by the manifest (all are missing: no vars files)."""
-    doc = _load(path)
-    names = set()
-    _var_names(doc, names)
-    if not names:
-        # interpolation succeeded, so the manifest itself must decode
-        _decode_manifest(doc)
+    """Names of ``((vars))`` used by the manifest (all are missing: no vars
+    files), ``getMissingVariables`` (cfmanifest2kube.go:472-489)."""
+    try:
+        doc = _load(path)
+        names = set()
+        _var_names(doc, names)
+        if not names:
+            # interpolation succeeded, so the manifest itself must decode
+            _decode_manifest(doc)
+    except ManifestError as e:
+        log.debug("Error %s", e)
+        raise
     return sorted(names)
 
 
@@ -184,16 +195,28 @@ def _decode_application(d):
     return a
 
 
+def _type_error(value, into):
+    tag = {bool: "!!bool", int: "!!int", float: "!!float", str: "!!str", list: "!!seq", dict: "!!map"}.get(type(value), "!!str")
+    shown = ""
+    if tag not in ("!!seq", "!!map"):
+        raw = _str(value)
+        shown = " `" + (raw[:7] + "..." if len(raw) > 10 else raw) + "`"
+    # the line is the node's in the bosh template's re-marshalled text, which
+    # sorts the top-level keys: "applications" (or the whole document) comes
+    # first there unless a key sorting before it exists (parity unpinned then)
+    return "yaml: unmarshal errors:\n  line 1: cannot unmarshal %s%s into %s" % (tag, shown, into)
+
+
 def _decode_manifest(doc):
     if doc is None:
         return []
     if not isinstance(doc, dict):
-        raise ManifestError("cannot unmarshal manifest")
+        raise ManifestError(_type_error(doc, "manifest.Manifest"))
     apps = doc.get("applications")
     if apps is None:
         return []
     if not isinstance(apps, list):
-        raise ManifestError("applications must be a list")
+        raise ManifestError(_type_error(apps, "[]manifest.Application"))
     return [_decode_application(x) for x in apps]
 
 
@@ -208,15 +231,27 @@ def read_application_manifest(path, service_name="", artifact_type=plantypes.YAM
 
 
 def _read_application_manifest(path, service_name, artifact_type):
-    variables = get_missing_variables(path)
-    doc = _load(path)
+    try:
+        variables = get_missing_variables(path)
+    except ManifestError as e:
+        log.debug("Unable to read as cf manifest %s : %s", path, e)
+        raise
+    try:
+        doc = _load(path)
+    except ManifestError as e:
+        log.error("Unable to read manifest file at path %r Error: %r", path, str(e))
+        raise
     values = {}
     for v in variables:
         if artifact_type == plantypes.HELM:
             values[v] = '{{ index  .Values "globalvariables" "' + v + '"}}'
         else:
             values[v] = "{{ $" + v + " }}"
-    apps = _decode_manifest(_evaluate(doc, values))
+    try:
+        apps = _decode_manifest(_evaluate(doc, values))
+    except ManifestError as e:
+        log.debug("UnMarshalling error %s", e)
+        raise
     if len(apps) == 1:
         return apps, variables
     if service_name:

@@ -62,24 +62,48 @@ class CfManifestTranslator(Translator):
         except OSError as e:
             log.warning("Unable to fetch yaml files and recognize cf manifest yamls at path %r Error: %r", input_path, str(e))
             raise
+        # The built-in map (data.Cfbuildpacks_yaml) has its list at the top
+        # level, not under spec, so the reference decodes it to an empty list
+        # (kind "cfcontainerizers"); "fixed" compat uses it.
         containerizers = []
         if settings.fixed:
             containerizers = [collection.BuildpackContainerizer(b["buildpackName"], b["containerBuildType"], b["targetOptions"])
                               for b in assets.builtin_cf_buildpacks()]
-        instance_apps = {}
-        for f in files:
+        docs = {}
+        for f in files:   # every move2kube-group YAML counts: there is no kind check (cfmanifest2kube.go:67-76)
             try:
-                data = common.read_move2kube_yaml(f)
-            except Exception:  # noqa: BLE001
+                docs[f] = data = common.read_move2kube_yaml(f)
+            except Exception as e:  # noqa: BLE001
+                log.debug("Not a valid containerizer option file at path %r Error: %r", f, str(e))
                 continue
-            kind = data.get("kind") if isinstance(data, dict) else None
             try:
-                if kind == collection.CF_CONTAINERIZERS_KIND or "spec" in (data or {}):
-                    containerizers.extend(collection.CfContainerizers.from_yaml(data).buildpack_containerizers)
-                if kind == collection.CF_INSTANCE_APPS_KIND:
-                    instance_apps.setdefault(f, []).extend(collection.CfInstanceApps.from_yaml(data).applications)
+                containerizers.extend(collection.CfContainerizers.from_yaml(data).buildpack_containerizers)
             except ValueError:
                 continue
+        if log.debug_enabled():
+            log.debug("Containerizers %s", "{TypeMeta:{APIVersion: Kind:cfcontainerizers} ObjectMeta:{Name:} "
+                      "Spec:{BuildpackContainerizers:[%s]}}" % " ".join(b.go_plus_v() for b in containerizers))
+        instance_apps = {}
+        for f in files:
+            data = docs.get(f)
+            if data is None:
+                try:
+                    data = common.read_move2kube_yaml(f)
+                except Exception as e:  # noqa: BLE001
+                    log.debug("Failed to read the yaml file at path %r Error: %r", f, str(e))
+                    continue
+            kind = data.get("kind") if isinstance(data, dict) else None
+            if kind != collection.CF_INSTANCE_APPS_KIND:
+                log.debug("%s is not a valid apps file. Expected kind: %s Actual Kind: %s", log.go_quote(f),
+                          collection.CF_INSTANCE_APPS_KIND, kind if isinstance(kind, str) else "")
+                continue
+            try:
+                instance_apps.setdefault(f, []).extend(collection.CfInstanceApps.from_yaml(data).applications)
+            except ValueError:
+                continue
+        if log.debug_enabled():
+            log.debug("Cf Instances %s", "map[" + " ".join(
+                "%s:[%s]" % (k, " ".join(a.go_plus_v() for a in instance_apps[k])) for k in sorted(instance_apps)) + "]")
         covered = []
         for f in files:
             try:
@@ -227,6 +251,7 @@ class CfManifestTranslator(Translator):
                 except (ManifestError, OSError) as e:
                     log.debug("Error while trying to parse manifest : %s", e)
                     continue
+                log.debug("Using cf manifest file at path %s to translate service %s", path, service.service_name)
                 try:
                     container = cz.get_container(plan, service)
                 except Exception as e:  # noqa: BLE001

@@ -222,3 +222,15 @@ def test_cf_manifest_variables_become_template_placeholders(tmp_path, assets_dir
     assert apps[0].environment_variables == {"MODE": "{{ $mode }}", "URL": "https://{{ $host }}/api"}
     apps, _ = cfmanifest.read_application_manifest(path, "", plantypes.HELM)
     assert apps[0].environment_variables["MODE"] == '{{ index  .Values "globalvariables" "mode"}}'
+
+
+def test_cf_manifest_scalars_follow_yaml_1_1(tmp_path):
+    """The bosh template decodes a CF manifest with go-yaml v2 before anyone
+    reads it: yes/on are booleans (env values print "true"), 010 is octal, a
+    repeated key keeps its last value."""
+    from move2kube_amd.source import cfmanifest
+    p = tmp_path / "manifest.yml"
+    p.write_text("applications:\n- name: a\n  name: app\n  instances: 010\n  env:\n    FLAG: yes\n    OTHER: off\n")
+    (app,), variables = cfmanifest.read_application_manifest(str(p))
+    assert variables == [] and app.name == "app" and app.instances.value == 8
+    assert app.environment_variables == {"FLAG": "true", "OTHER": "false"}
