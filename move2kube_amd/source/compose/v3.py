@@ -9,6 +9,7 @@ relative to the compose file's directory.
 """
 
 import os
+import stat
 
 from ...containerizer.reusedockerfile import ReuseDockerfileContainerizer
 from ...models import ir as irtypes
@@ -537,28 +538,51 @@ class V3Loader:
             st = irtypes.Storage(name=name, storage_type=irtypes.CONFIGMAP_KIND)
             if not obj["external"]:
                 f = obj["file"]
-                if not os.path.exists(f):
-                    log.warning("Could not identify the type of secret artifact [%s].", f)
-                elif not os.path.isdir(f):
-                    try:
-                        with open(f, "rb") as fh:
-                            st.content = {name: fh.read()}
-                    except OSError:
-                        log.warning("Could not read the secret file [%s].", f)
+                try:
+                    is_dir = stat.S_ISDIR(os.stat(f).st_mode)
+                except OSError as e:
+                    log.warning("Could not identify the type of secret artifact [%s]. Encountered [%s]", f,
+                                common.go_path_error(e, "stat"))
                 else:
-                    data = {}
-                    for entry in sorted(os.listdir(f)):
-                        p = os.path.join(f, entry)
-                        if os.path.isdir(p):
-                            continue
+                    if not is_dir:
                         try:
-                            with open(p, "rb") as fh:
-                                data[entry] = fh.read()
-                        except OSError:
-                            continue
-                    st.content = data
+                            with open(f, "rb") as fh:
+                                st.content = {name: fh.read()}
+                        except OSError as e:
+                            log.warning("Could not read the secret file [%s]. Encountered [%s]", f,
+                                        common.go_path_error(e, "open"))
+                    else:
+                        try:
+                            st.content = self._dir_content_as_map(f)
+                        except OSError as e:
+                            log.warning("Could not read the secret directory [%s]. Encountered [%s]", f,
+                                        common.go_path_error(e, "open"))
             out.append(st)
         return out
+
+    @staticmethod
+    def _dir_content_as_map(directory):
+        """``getAllDirContentAsMap`` (v3.go:625-651): the directory's files by
+        name (ioutil.ReadDir: sorted, lstat, so a symlink is read as a file)."""
+        data = {}
+        count = 0
+        for entry in sorted(os.listdir(directory)):
+            p = os.path.join(directory, entry)
+            try:
+                if stat.S_ISDIR(os.lstat(p).st_mode):
+                    continue
+            except OSError:
+                continue
+            log.debug("Reading file into the data map: [%s]", entry)
+            try:
+                with open(p, "rb") as fh:
+                    data[entry] = fh.read()
+            except OSError:
+                log.debug("Unable to read file data : %s", entry)
+                continue
+            count += 1
+        log.debug("Read %d files into the data map", count)
+        return data
 
     @staticmethod
     def get_ports(ports, expose):
