@@ -78,13 +78,19 @@ class Deployment(IAPIResource):
         return ps
 
     def create_deployment(self, service):
-        return self.to_deployment(self._meta(service), self._podspec(service), service.replicas)
+        m, ps = self._meta(service), self._podspec(service)
+        log.debug("Created deployment for %s", service.name)
+        return self.to_deployment(m, ps, service.replicas)
 
     def create_deployment_config(self, service):
-        return self.to_deployment_config(self._meta(service), self._podspec(service), service.replicas)
+        m, ps = self._meta(service), self._podspec(service)
+        log.debug("Created DeploymentConfig for %s", service.name)
+        return self.to_deployment_config(m, ps, service.replicas)
 
     def create_replication_controller(self, service):
-        return self.to_replication_controller(self._meta(service), self._podspec(service), service.replicas)
+        m, ps = self._meta(service), self._podspec(service)
+        log.debug("Created DeploymentConfig for %s", service.name)   # sic, deployment.go:230
+        return self.to_replication_controller(m, ps, service.replicas)
 
     def create_pod(self, service):
         ps = self._podspec(service)

@@ -41,15 +41,32 @@ class K8sAPIResourceSet:
 
     @staticmethod
     def _yaml_files(input_path):
-        return common.get_files_by_ext(input_path, [".yml", ".yaml"])
+        try:
+            return common.get_files_by_ext(input_path, [".yml", ".yaml"])
+        except (OSError, ValueError) as e:
+            log.error("Unable to fetch yaml files at path %r Error: %r", input_path, str(e))
+            raise
+
+    @staticmethod
+    def _read_and_decode(f, scheme_name):
+        """ioutil.ReadFile + UniversalDeserializer().Decode of the planners,
+        with their debug lines; None when either fails."""
+        try:
+            data = common.read_bytes(f)
+        except OSError as e:
+            log.debug("Failed to read the yaml file at path %r Error: %r", f, common.go_path_error(e, "open"))
+            return None
+        try:
+            return scheme.decode(data, scheme_name)
+        except scheme.DecodeError as e:
+            log.debug("Failed to decode the file at path %r as a %s file. Error: %r", f, scheme_name, str(e))
+            return None
 
     def get_service_options(self, input_path, plan):
         services = []
         for f in self._yaml_files(input_path):
-            try:
-                obj = scheme.decode_file(f, "k8s")
-            except (OSError, scheme.DecodeError) as e:
-                log.debug("Failed to decode the file at path %r as a k8s file. Error: %r", f, str(e))
+            obj = self._read_and_decode(f, "k8s")
+            if obj is None:
                 continue
             try:
                 name, _ = ar.Deployment.get_name_and_pod_spec(obj)
@@ -69,9 +86,18 @@ class K8sAPIResourceSet:
                 continue
             irs = irtypes.new_service_from_plan_service(service)
             try:
-                obj = scheme.decode_file(files[0], "k8s")
+                data = common.read_bytes(files[0])
+            except OSError as e:
+                log.error("Unable to read the k8s file at path %r Error: %r", files[0], common.go_path_error(e, "open"))
+                continue
+            try:
+                obj = scheme.decode(data, "k8s")
+            except scheme.DecodeError as e:
+                log.error("Failed to decode the k8s file at path %r Error: %r", files[0], str(e))
+                continue
+            try:
                 _, ps = ar.Deployment.get_name_and_pod_spec(obj)
-            except (OSError, scheme.DecodeError, ValueError) as e:
+            except ValueError as e:
                 log.error("Failed to get the pod specification for the k8s file at path %r Error: %r", files[0], str(e))
                 continue
             irs.pod_spec = ps
@@ -101,10 +127,8 @@ class KnativeAPIResourceSet(K8sAPIResourceSet):
     def get_service_options(self, input_path, plan):
         services = []
         for f in self._yaml_files(input_path):
-            try:
-                obj = scheme.decode_file(f, "knative")
-            except (OSError, scheme.DecodeError) as e:
-                log.debug("Failed to decode the file at path %r as a knative file. Error: %r", f, str(e))
+            obj = self._read_and_decode(f, "knative")
+            if obj is None:
                 continue
             is_ksvc = obj.get("kind") == "Service" and obj.get("apiVersion") == "serving.knative.dev/v1"
             # The reference inverts this check: real Knative services are skipped and
@@ -126,12 +150,20 @@ class KnativeAPIResourceSet(K8sAPIResourceSet):
                 continue
             irs = irtypes.new_service_from_plan_service(service)
             try:
-                obj = scheme.decode_file(files[0], "knative")
-            except (OSError, scheme.DecodeError) as e:
+                data = common.read_bytes(files[0])
+            except OSError as e:
+                log.error("Unable to read the knative file at path %r Error: %r", files[0], common.go_path_error(e, "open"))
+                continue
+            try:
+                obj = scheme.decode(data, "knative")
+            except scheme.DecodeError as e:
                 log.error("Failed to decode the knative file at path %r Error: %r", files[0], str(e))
                 continue
             if not (obj.get("kind") == "Service" and obj.get("apiVersion") == "serving.knative.dev/v1"):
-                log.error("The knative file at path %r does not contain the required type.", files[0])
+                # %T of the decoded object: *<version package>.<Kind>
+                actual = "*%s.%s" % (str(obj.get("apiVersion", "")).rsplit("/", 1)[-1], obj.get("kind", ""))
+                log.error("The knative file at path %r does not contain the required type. Expected: %s Actual: %s",
+                          files[0], "*v1.Service", actual)
                 continue
             spec = ((obj.get("spec") or {}).get("template") or {}).get("spec") or {}
             ps = {k: v for k, v in spec.items() if k not in ("containerConcurrency", "timeoutSeconds")}
