@@ -39,6 +39,7 @@ def _mkdir(p):
 def write_containers(containers, outpath, root_dir, registry_url, registry_namespace):
     """Write new-container files and build/push scripts; True if any new image exists."""
     cpath = os.path.join(outpath, CONTAINERS_DIR)
+    log.debug("containerspath %s", cpath)
     try:
         _mkdir(cpath)
     except OSError as e:
@@ -48,6 +49,7 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
     batch = []
     made = set()
     for c in containers:
+        log.debug("Container : %s", "true" if c.new else "false")
         if not c.new:
             continue
         if not c.new_files:
@@ -71,6 +73,7 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
             if common.go_ext(wp) == ".sh":
                 mode = DEFAULT_EXECUTABLE_PERMISSION
                 buildscripts.append(os.path.join(CONTAINERS_DIR, rel))
+            log.debug("Writing at %s", wp)
             batch.append((wp, c.new_files[rel], mode))
     for (wp, _, _), err in zip(batch, native.write_files(batch)):
         if err is not None:
@@ -78,11 +81,13 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
     if manualimages:
         wp = os.path.join(outpath, "Manualimages.md")
         if settings.fixed:
-            common.write_template_to_file(assets.template("manualimages.md.tpl"), {"Images": manualimages}, wp,
-                                          DEFAULT_FILE_PERMISSION)
+            _write_template("manualimages.md.tpl", {"Images": manualimages}, wp, DEFAULT_FILE_PERMISSION,
+                            "Unable to create manual image : %s")
         else:
             # the reference hands the template a struct without the field it ranges over,
             # so template execution fails and no file is written
+            log.warning("Unable to translate template %s to string using the data %s",
+                        log.go_quote(assets.template("manualimages.md.tpl")), "{[" + " ".join(manualimages) + "]}")
             log.error("Unable to create manual image : template: manualimages:5:17: executing \"manualimages\" at "
                       "<.Images>: can't evaluate field Images in type struct { Scripts []string }")
     if buildscripts:
@@ -90,23 +95,40 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
         for v in buildscripts:
             d, f = os.path.split(v)
             script_map[f] = d + "/" if d else ""
-        common.write_template_to_file(assets.template("buildimages.sh.tpl"), script_map,
-                                      os.path.join(outpath, "buildimages.sh"), DEFAULT_EXECUTABLE_PERMISSION)
+        if log.debug_enabled():
+            log.debug("buildscripts %s", "[" + " ".join(buildscripts) + "]")
+            log.debug("buildScriptMap %s", "map[" + " ".join("%s:%s" % (k, script_map[k]) for k in sorted(script_map)) + "]")
+        _write_template("buildimages.sh.tpl", script_map, os.path.join(outpath, "buildimages.sh"),
+                        DEFAULT_EXECUTABLE_PERMISSION, "Unable to create script to build images : %s")
         try:
             rel_root = common.go_rel(outpath, root_dir)
         except ValueError as e:
             log.error("Failed to make the root directory path %r relative to the output directory %r Error %r",
                       root_dir, outpath, str(e))
             rel_root = root_dir
-        common.write_template_to_file(assets.template("copysources.sh.tpl"), {"RelRootDir": rel_root, "Dst": CONTAINERS_DIR},
-                                      os.path.join(outpath, "copysources.sh"), DEFAULT_EXECUTABLE_PERMISSION)
+        _write_template("copysources.sh.tpl", {"RelRootDir": rel_root, "Dst": CONTAINERS_DIR},
+                        os.path.join(outpath, "copysources.sh"), DEFAULT_EXECUTABLE_PERMISSION,
+                        "Unable to create script to build images : %s")
     if dockerimages:
-        common.write_template_to_file(assets.template("pushimages.sh.tpl"),
-                                      {"Images": dockerimages, "RegistryURL": registry_url,
-                                       "RegistryNamespace": registry_namespace},
-                                      os.path.join(outpath, "pushimages.sh"), DEFAULT_EXECUTABLE_PERMISSION)
+        _write_template("pushimages.sh.tpl", {"Images": dockerimages, "RegistryURL": registry_url,
+                                              "RegistryNamespace": registry_namespace},
+                        os.path.join(outpath, "pushimages.sh"), DEFAULT_EXECUTABLE_PERMISSION,
+                        "Unable to create script to push images : %s")
         return True
     return False
+
+
+def _write_template(name, data, path, mode, error_fmt):
+    """WriteTemplateToFile of a packaged template; a failure is logged with
+    the caller's text and the run goes on, as in the reference."""
+    from ..utils.gotemplate import TemplateError
+    try:
+        common.write_template_to_file(assets.template(name), data, path, mode)
+    except TemplateError as e:
+        log.error(error_fmt, e)
+    except OSError as e:
+        log.warning("Error writing file at %s : %s", path, common.go_path_error(e, "open"))
+        log.error(error_fmt, common.go_path_error(e, "open"))
 
 
 def serialize_object(obj):
@@ -250,16 +272,51 @@ class K8sTransformer(Transformer):
                                 self.values.registry_namespace)
 
     def generate_helm_metadata(self, d):
-        _mkdir(d)
-        common.write_text(os.path.join(d, "README.md"), "This chart was created by Move2Kube\n")
+        """``generateHelmMetadata`` (k8stransformer.go:156-217): each step
+        that fails is logged and the rest still written."""
+        from ..utils.gotemplate import TemplateError
+        try:
+            _mkdir(d)
+        except OSError as e:
+            log.error("Unable to create Helm Metadata directory %s : %s", d, common.go_path_error(e, "mkdir"))
+            raise
+        try:
+            common.write_text(os.path.join(d, "README.md"), "This chart was created by Move2Kube\n")
+        except OSError as e:
+            log.error("Error while writing Readme : %s", common.go_path_error(e, "open"))
         base = common.go_base(d)
-        common.write_template_to_file(assets.template("chart.yaml.tpl"), {"Name": base}, os.path.join(d, "Chart.yaml"),
-                                      DEFAULT_FILE_PERMISSION)
-        _mkdir(os.path.join(d, HELM_TEMPLATES_REL_PATH))
-        notes = common.get_string_from_template(assets.template("notes.txt.tpl"),
-                                                {"IsHelm": True, "ExposedServicePaths": self.exposed_service_paths})
-        common.write_text(os.path.join(d, HELM_TEMPLATES_REL_PATH, "NOTES.txt"), assets.template("helmnotes.txt") + notes)
-        common.write_yaml(os.path.join(d, "values.yaml"), self.values)
+        try:
+            common.write_template_to_file(assets.template("chart.yaml.tpl"), {"Name": base},
+                                          os.path.join(d, "Chart.yaml"), DEFAULT_FILE_PERMISSION)
+        except (OSError, TemplateError) as e:
+            log.error("Error while writing Chart.yaml : %s",
+                      common.go_path_error(e, "open") if isinstance(e, OSError) else e)
+        try:
+            _mkdir(os.path.join(d, HELM_TEMPLATES_REL_PATH))
+        except OSError as e:
+            log.error("Unable to create templates directory : %s", common.go_path_error(e, "mkdir"))
+        notes = ""
+        try:
+            notes = common.get_string_from_template(assets.template("notes.txt.tpl"),
+                                                    {"IsHelm": True, "ExposedServicePaths": self.exposed_service_paths})
+        except TemplateError as e:
+            paths = self.exposed_service_paths
+            log.error("Failed to fill the NOTES.txt template %s with the service paths %s Error: %r",
+                      assets.template("notes.txt.tpl"),
+                      "map[" + " ".join("%s:%s" % (k, paths[k]) for k in sorted(paths)) + "]", str(e))
+        try:
+            common.write_text(os.path.join(d, HELM_TEMPLATES_REL_PATH, "NOTES.txt"),
+                              assets.template("helmnotes.txt") + notes)
+        except OSError as e:
+            log.error("Error while writing Helm NOTES.txt : %s", common.go_path_error(e, "open"))
+        values_path = os.path.join(d, "values.yaml")
+        try:
+            common.write_yaml(values_path, self.values)
+        except OSError as e:
+            # log.Warn("Error in writing Helm values", err): Sprint puts no space after a string operand
+            log.warning("Error in writing Helm values%s", common.go_path_error(e, "open"))
+        else:
+            log.debug("Wrote Helm values to file: %s", values_path)
         common.write_template_to_file(assets.template("helminstall.sh.tpl"), {"Project": base},
                                       os.path.join(os.path.dirname(d), "helminstall.sh"), DEFAULT_EXECUTABLE_PERMISSION)
 
@@ -328,19 +385,35 @@ class K8sTransformer(Transformer):
             out.close()
 
     def write_deploy_script(self, proj, outpath):
-        common.write_template_to_file(assets.template("deploy.sh.tpl"), {"Project": proj},
-                                      os.path.join(outpath, "deploy.sh"), DEFAULT_EXECUTABLE_PERMISSION)
-        common.write_template_to_file(assets.template("notes.txt.tpl"),
-                                      {"IsHelm": False, "IngressHost": self.target_cluster_spec.host,
-                                       "ExposedServicePaths": self.exposed_service_paths},
-                                      os.path.join(outpath, "NOTES.txt"), DEFAULT_FILE_PERMISSION)
+        deploy = os.path.join(outpath, "deploy.sh")
+        _write_or_log(assets.template("deploy.sh.tpl"), {"Project": proj}, deploy, DEFAULT_EXECUTABLE_PERMISSION,
+                      "Failed to write the deploy script at path %r Error: %r", deploy)
+        notes = os.path.join(outpath, "NOTES.txt")
+        _write_or_log(assets.template("notes.txt.tpl"),
+                      {"IsHelm": False, "IngressHost": self.target_cluster_spec.host,
+                       "ExposedServicePaths": self.exposed_service_paths},
+                      notes, DEFAULT_FILE_PERMISSION, "Failed to write the NOTES.txt file at path %r Error: %r", notes)
 
     @staticmethod
     def write_readme(project, new_images, helm, warn, outpath):
-        common.write_template_to_file(assets.template("k8sreadme.md.tpl"),
-                                      {"Project": project, "NewImages": new_images, "Helm": helm,
-                                       "AddCopySourcesWarning": warn},
-                                      os.path.join(outpath, "Readme.md"), DEFAULT_FILE_PERMISSION)
+        _write_or_log(assets.template("k8sreadme.md.tpl"),
+                      {"Project": project, "NewImages": new_images, "Helm": helm, "AddCopySourcesWarning": warn},
+                      os.path.join(outpath, "Readme.md"), DEFAULT_FILE_PERMISSION, "Unable to write readme : %s")
+
+
+def _write_or_log(tpl, data, path, mode, error_fmt, *prefix):
+    """WriteTemplateToFile whose error the caller logs (``error_fmt`` with
+    ``prefix`` arguments, then the error; %r arguments print Go-quoted)."""
+    from ..utils.gotemplate import TemplateError
+    try:
+        common.write_template_to_file(tpl, data, path, mode)
+    except (OSError, TemplateError) as e:
+        if isinstance(e, OSError):
+            text = common.go_path_error(e, "open")
+            log.warning("Error writing file at %s : %s", path, text)
+        else:
+            text = str(e)
+        log.error(error_fmt, *(prefix + (text,)))
 
 
 class KnativeTransformer(Transformer):
@@ -365,11 +438,10 @@ class KnativeTransformer(Transformer):
             write_transformed_objects(os.path.join(outpath, self.name), self.transformed_objects)
         except OSError as e:
             log.error("Error occurred while writing transformed objects %s", e)
-        common.write_template_to_file(assets.template("deploy.sh.tpl"), {"Project": self.name},
-                                      os.path.join(outpath, "deploy.sh"), DEFAULT_EXECUTABLE_PERMISSION)
-        common.write_template_to_file(assets.template("knativereadme.md.tpl"),
-                                      {"Project": self.name, "NewImages": new_images},
-                                      os.path.join(outpath, "Readme.md"), DEFAULT_FILE_PERMISSION)
+        _write_or_log(assets.template("deploy.sh.tpl"), {"Project": self.name}, os.path.join(outpath, "deploy.sh"),
+                      DEFAULT_EXECUTABLE_PERMISSION, "Unable to write deploy script : %s")
+        _write_or_log(assets.template("knativereadme.md.tpl"), {"Project": self.name, "NewImages": new_images},
+                      os.path.join(outpath, "Readme.md"), DEFAULT_FILE_PERMISSION, "Unable to write Readme : %s")
 
 
 class ComposeTransformer(Transformer):
@@ -414,8 +486,15 @@ class ComposeTransformer(Transformer):
         self.compose = {"version": "3.5", "services": yamlio.GoMap(services)} if services else {"version": "3.5"}
 
     def write_objects(self, outpath):
-        _mkdir(outpath)
-        common.write_yaml(os.path.join(outpath, "docker-compose.yaml"), self.compose)
+        try:
+            _mkdir(outpath)
+        except OSError as e:
+            log.error("Unable to create output directory %s : %s", outpath, common.go_path_error(e, "mkdir"))
+        path = os.path.join(outpath, "docker-compose.yaml")
+        try:
+            common.write_yaml(path, self.compose)
+        except OSError as e:
+            log.error("Unable to write docker compose file %s : %s", path, common.go_path_error(e, "open"))
 
 
 class CICDTransformer(Transformer):
@@ -428,4 +507,8 @@ class CICDTransformer(Transformer):
             _mkdir(p)
         except OSError as e:
             log.fatal("Failed to create the CI/CD directory at path %r. Error: %r", p, common.go_path_error(e, "mkdir"))
-        write_transformed_objects(p, self.cached_objs)
+        try:
+            write_transformed_objects(p, self.cached_objs)
+        except OSError as e:
+            log.error("Error occurred while writing transformed objects. Error: %r", common.go_path_error(e, "open"))
+            raise

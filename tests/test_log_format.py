@@ -70,3 +70,34 @@ def test_cli_picks_the_format_from_its_stderr(tmp_path):
     text = out.decode().replace("\r\n", "\n")
     assert p.returncode == 1
     assert re.search(r"\x1b\[31mFATA\x1b\[0m\[\d{4}\] \S", text), text
+
+
+def test_write_containers_debug_lines(tmp_path, capsys):
+    """writeContainers (transformer.go:59-160) at debug level."""
+    import logparse
+    from move2kube_amd import transformer
+    from move2kube_amd.models import ir as irtypes
+    log.set_verbose(True)
+    try:
+        c = irtypes.new_container("NewDockerfile", "img:latest", True)
+        c.new_files = {"svc/Dockerfile.svc": "FROM x\n", "svc/svc-docker-build.sh": "#!/bin/sh\n"}
+        assert transformer.write_containers([c], str(tmp_path), str(tmp_path), "quay.io", "ns") is True
+    finally:
+        log.set_verbose(False)
+    msgs = [m for lv, m in logparse.messages(capsys.readouterr().err) if lv == "debug"]
+    cpath = str(tmp_path / "containers")
+    assert msgs[:4] == ["containerspath %s" % cpath, "Total number of containers : 1", "Container : true",
+                        "New Container : img:latest"]
+    assert "Writing at %s/svc/Dockerfile.svc" % cpath in msgs
+    assert "buildscripts [containers/svc/svc-docker-build.sh]" in msgs
+    assert "buildScriptMap map[svc-docker-build.sh:containers/svc/]" in msgs
+
+
+def test_unwritable_readme_is_logged_and_the_run_goes_on(tmp_path, capsys):
+    import logparse
+    from move2kube_amd.transformer import K8sTransformer
+    (tmp_path / "Readme.md").mkdir()
+    log.set_verbose(False)
+    K8sTransformer.write_readme("p", False, False, False, str(tmp_path))
+    msgs = logparse.messages(capsys.readouterr().err)
+    assert msgs[-1] == ("error", "Unable to write readme : open %s: is a directory" % (tmp_path / "Readme.md"))
