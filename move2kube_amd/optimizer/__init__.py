@@ -64,7 +64,9 @@ class IngressOptimizer:
                 hints = ["Since there's only one exposed service, the default path is /"]
                 path = "/"
             prob = qa.new_input_problem(msg, hints, path)
-            path = self.normalize(qaengine.fetch_answer(prob).get_string_answer())
+            path = qaengine.fetch_answer(prob).get_string_answer()
+            log.debug("Exposing service %s on path %s", name, path)
+            path = self.normalize(path)
             svc = ir.services[name]
             svc.service_rel_path = path
             if svc.annotations is None:
@@ -150,8 +152,8 @@ class PortMergeOptimizer:
         for a in ans:
             try:
                 p = common.cast_to_int(a)
-            except ValueError:
-                log.debug("Failed to parse %r as an integer port.", a)
+            except ValueError as e:
+                log.debug("Failed to parse %r as an integer port. Error: %r", a, str(e))
                 continue
             out[p] = p2c.get(p, 0)
         return out
