@@ -293,20 +293,39 @@ def _run(cmd, timeout=600):
                               timeout=timeout)
 
 
+def _go_err(proc_or_exc, argv0):
+    """The Go error text of a finished command or of its failed start."""
+    if isinstance(proc_or_exc, BaseException):
+        if isinstance(proc_or_exc, OSError):
+            return str(common.go_exec_error(proc_or_exc, argv0))
+        return str(proc_or_exc)
+    return common.go_exit_status(proc_or_exc.returncode)
+
+
+def _out(p):
+    return p.stdout.decode("utf-8", "replace") if isinstance(getattr(p, "stdout", None), bytes) else ""
+
+
 class ContainerRuntimeProvider:
+    """``containerRuntimeProvider`` (containerruntimeprovider.go): podman with
+    the vfs storage driver."""
+
     def __init__(self):
         self.runtime = None  # "podman" | "none"
         self.available = set()
 
     def get_runtime(self):
         if self.runtime is None:
-            if shutil.which("podman") is None:
+            try:
+                p = _run(["podman", "run", "--storage-driver=vfs", "--rm", "hello-world"])
+            except (OSError, subprocess.TimeoutExpired) as e:
+                log.debug("Podman not supported : %s : %s", _go_err(e, "podman"), "")
                 self.runtime = "none"
             else:
-                try:
-                    p = _run(["podman", "run", "--storage-driver=vfs", "--rm", "hello-world"])
-                    self.runtime = "podman" if p.returncode == 0 else "none"
-                except (OSError, subprocess.TimeoutExpired):
+                if p.returncode == 0:
+                    self.runtime = "podman"
+                else:
+                    log.debug("Podman not supported : %s : %s", _go_err(p, "podman"), _out(p))
                     self.runtime = "none"
         return self.runtime if self.runtime != "none" else None
 
@@ -316,16 +335,29 @@ class ContainerRuntimeProvider:
             return False
         if builder in self.available:
             return True
+        log.debug("Checking if the image %s exists locally", builder)
         try:
-            p = _run([rt, "--storage-driver=vfs", "images", "-q", builder])
-            if p.returncode == 0 and p.stdout.strip():
-                self.available.add(builder)
-                return True
-            p = _run([rt, "pull", "--storage-driver=vfs", builder])
-        except (OSError, subprocess.TimeoutExpired):
+            p = subprocess.run([rt, "--storage-driver=vfs", "images", "-q", builder], stdout=subprocess.PIPE,
+                               stderr=subprocess.DEVNULL, stdin=subprocess.DEVNULL, timeout=600)
+        except (OSError, subprocess.TimeoutExpired) as e:
+            log.warning("Error while checking if the builder %s exists locally. Error: %r Output: %r", builder,
+                        _go_err(e, rt), "")
             return False
         if p.returncode != 0:
-            log.warning("Error while pulling builder %s : %s", builder, p.stdout[:200])
+            log.warning("Error while checking if the builder %s exists locally. Error: %r Output: %r", builder,
+                        _go_err(p, rt), _out(p))
+            return False
+        if p.stdout:
+            self.available.add(builder)
+            return True
+        log.debug("Pulling image %s", builder)
+        try:
+            p = _run([rt, "pull", "--storage-driver=vfs", builder])
+        except (OSError, subprocess.TimeoutExpired) as e:
+            log.warning("Error while pulling builder %s : %s : %s", builder, _go_err(e, rt), "")
+            return False
+        if p.returncode != 0:
+            log.warning("Error while pulling builder %s : %s : %s", builder, _go_err(p, rt), _out(p))
             return False
         self.available.add(builder)
         return True
@@ -334,29 +366,40 @@ class ContainerRuntimeProvider:
         return [self.runtime, "run", "--rm", "--storage-driver=vfs", "-v", os.path.abspath(path) + ":/workspace",
                 builder, "/cnb/lifecycle/detector"]
 
+    def _detect_result(self, builder, p):
+        if p.returncode != 0:
+            log.debug("Detect failed %s : %s : %s", builder, _go_err(p, self.runtime), _out(p))
+            return False
+        return True
+
     def is_builder_supported(self, path, builder):
         if not self.is_builder_available(builder):
             raise ProviderError("Builder image not available : %s" % builder)
-        p = _run(self._detect_cmd(path, builder))
-        return p.returncode == 0
+        log.debug("Running detect on image %s", builder)
+        return self._detect_result(builder, _run(self._detect_cmd(path, builder)))
 
     def is_builder_supported_batch(self, pairs):
         """[(path, builder)] -> [True/False, or None where this provider cannot
         answer].  Builder availability is settled once per builder (it may
         pull); the detector containers then run concurrently - the reference
-        runs one at a time, each a container start."""
+        runs one at a time, each a container start.  The log lines come out in
+        the order of the pairs."""
         out = [None] * len(pairs)
         runnable = []
         for i, (path, builder) in enumerate(pairs):
             if self.is_builder_available(builder):
                 runnable.append(i)
-        results = parallel_map(lambda i: _run(self._detect_cmd(*pairs[i])).returncode == 0, runnable,
+        for i in runnable:
+            log.debug("Running detect on image %s", pairs[i][1])
+        results = parallel_map(lambda i: _run(self._detect_cmd(*pairs[i])), runnable,
                                min(settings.workers, CONTAINER_PARALLEL))
         for i, r in zip(runnable, results):
             if isinstance(r, Exception):
                 if not isinstance(r, _chain_errors()):
                     raise r
                 r = None  # this pair goes on down the chain, as in is_builder_supported
+            else:
+                r = self._detect_result(pairs[i][1], r)
             out[i] = r
         return out
 
@@ -365,6 +408,9 @@ class ContainerRuntimeProvider:
         if rt is None:
             raise ProviderError("Container runtime not supported in this instance")
         out = {}
+        log.debug("Getting data of all builders %s", "[" + " ".join(builders) + "]")
+        for b in builders:
+            log.debug("Inspecting image %s", b)
         # one `inspect` per builder, concurrently
         procs = parallel_map(lambda b: _run([rt, "inspect", "--storage-driver=vfs", "--format",
                                              '{{ index .Config.Labels "' + ORDER_LABEL + '"}}', b]), builders)
@@ -372,6 +418,7 @@ class ContainerRuntimeProvider:
             if isinstance(p, Exception):
                 raise p
             if p.returncode != 0:
+                log.debug("Unable to inspect image %s : %s, %s", b, _go_err(p, rt), _out(p))
                 continue
             out[b] = get_builders_from_label(p.stdout.decode())
         return out
