@@ -113,12 +113,16 @@ def get_files_by_ext(input_path, exts):
 
     Raises FileNotFoundError if ``input_path`` does not exist (reference returns an error)."""
     from .fsindex import get_index
-    return get_index(input_path).files_by_ext(exts)
+    files = get_index(input_path).files_by_ext(exts)
+    log.debug("No of files with %s ext identified : %d", "[" + " ".join(exts) + "]", len(files))
+    return files
 
 
 def get_files_by_name(input_path, names):
     from .fsindex import get_index
-    return get_index(input_path).files_by_name(names)
+    files = get_index(input_path).files_by_name(names)
+    log.debug("No of files with %s names identified : %d", "[" + " ".join(names) + "]", len(files))
+    return files
 
 
 # ---------------------------------------------------------------------------

@@ -380,7 +380,7 @@ def get_index(root):
         if idx is not None:
             return idx
     if not os.path.exists(root):
-        log.warning("Error in walking through files due to : %r", "lstat %s: no such file or directory" % root)
+        log.warning("Error in walking through files due to : %r", "stat %s: no such file or directory" % root)
         raise FileNotFoundError(root)
     if not os.path.isdir(root):
         log.warning("The path %r is not a directory.", root)
