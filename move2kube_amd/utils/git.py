@@ -137,10 +137,22 @@ def head_branch(git_dir):
 
 
 def repo_details(path, remote_name):
-    """(remote_urls, branch, repo_dir) like ``GetGitRepoDetails``."""
-    root, git_dir = find_repo(path)
+    """(remote_urls, branch, repo_dir) like ``GetGitRepoDetails``
+    (utils.go:653-680), with its debug lines; go-git's errors are
+    ``reference not found`` and ``remote not found``."""
+    from . import log
+    try:
+        root, git_dir = find_repo(path)
+    except GitError as e:
+        log.debug("Unable to open the path %r as a git repo. Error: %r", path, str(e))
+        raise
     branch = head_branch(git_dir)
-    urls = _read_config(git_dir).get(remote_name, [])
+    if branch == "":
+        log.debug("Unable to get the current branch. Error: %r", "reference not found")
+    remotes = _read_config(git_dir)
+    if remote_name not in remotes:
+        log.debug("Unable to get remote named %s Error: %r", remote_name, "remote not found")
+    urls = remotes.get(remote_name, [])
     return list(urls), branch, root
 
 
@@ -212,12 +224,19 @@ def go_url_path(raw):
 def repo_name(path):
     """(name, root) of the repo's ``origin`` remote, or ('', '') (``GetGitRepoName``,
     ``internal/common/utils.go:682-718``)."""
+    from . import log
     try:
         root, git_dir = find_repo(path)
-    except GitError:
+    except GitError as e:
+        log.debug("Unable to open %s as a git repo : %s", path, e)
         return "", ""
-    urls = _read_config(git_dir).get("origin")
+    remotes = _read_config(git_dir)
+    if "origin" not in remotes:
+        log.debug("Unable to get origin remote : %s", "remote not found")
+        return "", ""
+    urls = remotes["origin"]
     if not urls:
+        log.debug("Unable to get origins")
         return "", ""
     u = urls[0]
     if u.startswith("git"):
@@ -227,7 +246,8 @@ def repo_name(path):
         u = parts[1]
     try:
         upath = go_url_path(u)
-    except ValueError:
+    except ValueError as e:
+        log.debug("Unable to get origin remote host : %s", e)
         return "", ""
     name = go_base(upath)
     ext = go_ext(name)
