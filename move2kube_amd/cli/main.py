@@ -24,8 +24,19 @@ move2kube = LazyModule("move2kube_amd.move2kube")
 qaengine = LazyModule("move2kube_amd.qaengine")
 
 
-def _abs(p):
-    return go_abs(p) if p else p
+def _abs(p, what=None):
+    """filepath.Abs of a flag value; the reference's commands stop with
+    ``Failed to make the <what> path %q absolute`` when it fails (the working
+    directory is gone)."""
+    if not p:
+        return p
+    try:
+        return go_abs(p)
+    except OSError as e:
+        if what is None:
+            raise
+        log.fatal("Failed to make the %s path %r absolute. Error: %r", what, p,
+                  "getwd: " + (e.strerror or str(e)).lower())
 
 
 def _go_stat(path):
@@ -77,9 +88,9 @@ def create_output_directory_and_cache_file(out):
 
 
 def translate_handler(a):
-    planfile = _abs(a.plan)
-    srcpath = _abs(a.source) if a.source else ""
-    outpath = _abs(a.outpath)
+    planfile = _abs(a.plan, "plan file")
+    srcpath = _abs(a.source, "source directory") if a.source else ""
+    outpath = _abs(a.outpath, "output directory")
     settings.ignore_environment = a.ignoreenv
     qaengine.start_engine(a.qaskip, a.qaport, a.qadisablecli)
     qaengine.add_caches(list(reversed(a.qacache or [])))
@@ -122,8 +133,8 @@ def translate_handler(a):
 
 
 def plan_handler(a):
-    planfile = _abs(a.plan)
-    srcpath = _abs(a.source)
+    planfile = _abs(a.plan, "plan file")
+    srcpath = _abs(a.source, "source directory")
     st, err = _go_stat(srcpath)
     if err:
         log.fatal("Unable to access source directory : %s", err[1])
@@ -153,10 +164,10 @@ def plan_handler(a):
 
 
 def collect_handler(a):
-    outpath = _abs(a.outpath) if a.outpath else a.outpath
+    outpath = _abs(a.outpath, "output directory") if a.outpath else a.outpath
     srcpath = ""
     if a.source:
-        srcpath = _abs(a.source)
+        srcpath = _abs(a.source, "source directory")
         st, err = _go_stat(srcpath)
         if err and err[0] == errno.ENOENT:
             log.fatal("Source directory does not exist: %s.", err[1])

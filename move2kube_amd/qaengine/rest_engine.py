@@ -103,7 +103,10 @@ class HTTPRESTEngine(Engine):
                 if self.path.split("?")[0] != CURRENT_PROBLEM_URL:
                     self._send(404, "404 page not found\n", "text/plain")
                     return
-                self._send(200, json.dumps(engine.next_problem().to_json()) + "\n")
+                log.debug("Looking for a problem fron HTTP REST service")  # sic (httprestengine.go:106)
+                prob = engine.next_problem()
+                log.debug("QA Engine serves problem id: %d, desc: %s", prob.id, prob.desc)
+                self._send(200, json.dumps(prob.to_json()) + "\n")
 
             def do_POST(self):  # noqa: N802
                 if self.path.split("?")[0] != CURRENT_SOLUTION_URL:
@@ -114,11 +117,16 @@ class HTTPRESTEngine(Engine):
                     body = self.rfile.read(max(0, n))
                     sol = _string_slice(fastjson.loads(body))
                 except ValueError as e:
-                    self._send(500, "Error in un-marshalling solution in QA engine: %s\n" % e, "text/plain")
+                    errstr = "Error in un-marshalling solution in QA engine: %s" % e
+                    self._send(500, errstr + "\n", "text/plain")
+                    log.error("%s", errstr)
                     return
+                log.debug("QA Engine receives solution: %s", "[" + " ".join(sol or []) + "]")
                 err = engine.submit_solution(sol or [])
                 if err:
-                    self._send(500, "Unsuitable answer : %s\n" % err, "text/plain")
+                    errstr = "Unsuitable answer : %s" % err
+                    self._send(500, errstr + "\n", "text/plain")
+                    log.error("%s", errstr)
                 else:
                     self._send(200, "")
 
