@@ -267,7 +267,12 @@ class ClusterCollector(Collector):
         return out
 
     def collect_using_cli(self):
-        out = self._run("api-resources", "-o", "name").decode("utf-8", "replace")
+        try:
+            out = self._run("api-resources", "-o", "name").decode("utf-8", "replace")
+        except (CommandError, OSError) as e:
+            log.error("Error while running kubectl api-resources: %s", e)
+            raise
+        log.debug("Got kind information for cluster")
         kinds = {}
         for name in out.split("\n"):
             parts = name.split(".")

@@ -410,6 +410,8 @@ def make_file_name_compliant(name):
     processed = _FILENAME_INVALID.sub("-", base) if base.translate(_DROP_FILENAME_OK) else base
     if len(processed) > 63:
         log.debug("Warning: The processed name %r is longer than 63 characters long.", processed)
+    if processed[0] in "-." or processed[-1] in "-.":
+        log.debug("Warning: The first and/or last characters of the name %r are not alphanumeric.", processed)
     return processed
 
 
