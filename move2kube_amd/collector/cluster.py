@@ -12,7 +12,6 @@ group.
 """
 
 import functools
-import json
 import os
 import re
 import shutil

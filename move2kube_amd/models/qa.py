@@ -201,8 +201,16 @@ def required_literals(pattern):
         if c == "\\":
             nxt = pattern[i + 1] if i + 1 < n else ""
             if nxt == "" or nxt.isalnum():
-                flush()  # class, anchor or back-reference
+                # class, anchor, back-reference or a numeric escape (\000,
+                # \x41, \x{41}, \pL, \p{Greek}): what follows it up to the
+                # next non-alphanumeric is part of it or not required
+                flush()
                 i += 2
+                while i < n and pattern[i].isalnum():
+                    i += 1
+                if i < n and pattern[i] == "{":
+                    j = pattern.find("}", i)
+                    i = n if j < 0 else j + 1
                 continue
             if i + 2 < n and pattern[i + 2] in _QUANTIFIERS:
                 flush()

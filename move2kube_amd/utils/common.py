@@ -7,7 +7,6 @@ the reference (CRC-64/ECMA, FNV-64a, SHA-256 truncation).
 """
 
 import os
-import re
 import shutil
 
 from . import log, yamlio

@@ -35,7 +35,8 @@ def _fresh(s1, s2):
 
 
 _ATOMS = st.sampled_from(list("abcAB .?*+{}[]()^$|\\-,:0123") + ["\\.", "\\d", "\\s", "[a-c]", "(ab)", "x{2}", "a{1,", "(?i)",
-                                                                  "[^]a]", "\\?", "Select", " service"])
+                                                                  "[^]a]", "\\?", "Select", " service", "\\000",
+                                                                  "\\x41", "\\x{42}", "\\pL", "\\u0041"])
 
 
 @settings(max_examples=600, deadline=None)
@@ -66,6 +67,10 @@ def test_required_literals_examples():
     assert qa.required_literals("a.b\\.c[xy]d(e)f") == ["a", "b.c", "d", "f"]
     assert qa.required_literals("a|b") is None
     assert qa.required_literals("(?i)abc") is None
+    # numeric escapes: the digits belong to the escape, not to the text
+    assert qa.required_literals("\\000?") == []
+    assert qa.required_literals("a\\x41?b") == ["a", "b"]
+    assert qa.required_literals("a\\x{41}b") == ["a", "b"]
 
 
 def test_cached_descriptions_of_the_fixtures_match_as_before():
