@@ -363,7 +363,14 @@ class ContainerRuntimeProvider:
         return True
 
     def _detect_cmd(self, path, builder):
-        return [self.runtime, "run", "--rm", "--storage-driver=vfs", "-v", os.path.abspath(path) + ":/workspace",
+        try:
+            p = common.go_abs(path)
+        except OSError as e:
+            # filepath.Abs fails only when the working directory is gone;
+            # the reference warns and mounts "" (containerruntimeprovider.go:113-116)
+            log.warning("Unable to resolve to absolute path : getwd: %s", (e.strerror or str(e)).lower())
+            p = ""
+        return [self.runtime, "run", "--rm", "--storage-driver=vfs", "-v", p + ":/workspace",
                 builder, "/cnb/lifecycle/detector"]
 
     def _detect_result(self, builder, p):
