@@ -96,6 +96,18 @@ def large_tree_check(sizes):
             "ratio_largest_vs_smallest": round(rows[-1]["ms_per_service"] / rows[0]["ms_per_service"], 3)}
 
 
+def step_spread(step_s):
+    """Rank 0's per-step wall times: min / p50 / p90 / max in ms, so that box
+    noise (a slow tail) can be told from a regression (a shifted p50)."""
+    if not step_s:
+        return None
+    ms = sorted(x * 1000.0 for x in step_s)
+
+    def q(f):
+        return round(ms[min(len(ms) - 1, int(f * (len(ms) - 1) + 0.5))], 3)
+    return {"min": round(ms[0], 3), "p50": q(0.5), "p90": q(0.9), "max": round(ms[-1], 3), "n": len(ms)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -105,7 +117,7 @@ def main():
                     choices=sorted(refconfigs.CONFIGS) + sorted(refconfigs.EXTRA_CONFIGS))
     ap.add_argument("--check-runs", type=int, default=3,
                     help="warm/cold runs per configuration in the untimed per-config check (0 = skip)")
-    ap.add_argument("--large-tree", default="100,2000",
+    ap.add_argument("--large-tree", default="100,1000,5000",
                     help="untimed: translate synthetic trees of these app counts and report ms per service "
                          "(benchmarks/translate_large_tree.py); empty = skip")
     ap.add_argument("--keep", action="store_true", help="keep the work directory")
@@ -142,6 +154,7 @@ def main():
     run = refconfigs.Run(args.config, work).prepare()
     undo = run.apply_env()
     n_services = 0
+    step_s = []
     diff_headline = None
     phase_ms = None
     try:
@@ -153,9 +166,12 @@ def main():
             for _ in range(max(0, args.warmup - 1)):
                 run.step(s)
             barrier()
+            step_s = []
             t0 = time.perf_counter()
             for _ in range(args.steps):
+                ts = time.perf_counter()
                 run.step(s)
+                step_s.append(time.perf_counter() - ts)
             barrier()
             elapsed = time.perf_counter() - t0
             if rank == 0:
@@ -198,6 +214,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
+            "step_ms": step_spread(step_s),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -89,11 +89,11 @@ def _cli_process():
     """Start-up trims for a process that is the CLI (``python -m
     move2kube_amd`` and the release launcher call it first; a program that
     imports the package as a library does not).  The cyclic garbage collector
-    is off while the CLI's modules are imported - the entry freezes what they
-    created and turns it back on before running the command, so neither the
-    ~20 collections an import sequence of this size triggers nor the one at
-    interpreter exit walk those objects (2 ms of a cold start on the MI355X
-    hosts, ``scripts/gc_ab.py``).  ``shutil`` is imported
+    is off for the whole process (the entry freezes what the imports created):
+    neither the ~20 collections an import sequence of this size triggers nor
+    the one at interpreter exit walk those objects (2 ms of a cold start on the
+    MI355X hosts), and a command's objects live until it ends, so collections
+    during it would only re-walk a growing heap (``api.gc_paused``).  ``shutil`` is imported
     without its optional ``bz2``/``lzma`` archive formats, which this tool never
     asks ``shutil`` for (0.7 ms of a cold start on the MI355X hosts; ``tarfile``
     still imports them when it needs them), and ``msvcrt`` is recorded as
@@ -134,8 +134,16 @@ def _cli_exit(rc):
     for stream in (_sys.stdout, _sys.stderr):
         try:
             stream.flush()
-        except (OSError, ValueError, AttributeError):
-            pass
+        except (OSError, ValueError, AttributeError) as e:
+            # CPython reports a failed flush of stdout at exit (EPIPE, ENOSPC
+            # on a redirect) and exits with 120 unless the command failed
+            if stream is _sys.stdout and not isinstance(e, AttributeError):
+                try:
+                    print("Exception ignored in: %r\n%s: %s" % (stream, type(e).__name__, e), file=_sys.stderr)
+                except (OSError, ValueError):
+                    pass
+                if code == 0:
+                    code = 120
     _os._exit(code & 0xFF)
 
 from .models.info import VERSION as __version__  # noqa: E402,F401

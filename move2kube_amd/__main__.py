@@ -6,5 +6,4 @@ _cli_process()
 from .cli.main import main  # noqa: E402
 
 gc.freeze()
-gc.enable()
 _cli_exit(main())

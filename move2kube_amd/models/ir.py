@@ -394,6 +394,35 @@ class IR:
         self.storages.append(st)
         idx[1] = len(self.storages)
 
+    def container_finder(self):
+        """A :meth:`get_container` over a snapshot of the containers: one pass
+        builds a folded-name index, then every lookup is a dict probe.  Valid
+        while no container or image name changes (the port-merge optimizer
+        asks once per service without touching containers, which made the
+        plain scan quadratic in the size of the tree)."""
+        first = {}
+        first_new = {}
+        for pos, c in enumerate(self.containers):
+            for n in c.image_names:
+                k = common.go_fold(n)
+                first.setdefault(k, pos)
+                if c.new:
+                    first_new.setdefault(k, pos)
+        containers = list(self.containers)
+        registry = self.kubernetes.registry_url
+
+        def find(imagename):
+            best = first.get(common.go_fold(imagename))
+            parts = imagename.split("/")
+            if len(parts) > 2 and parts[0] == registry:
+                p = first_new.get(common.go_fold(parts[-1]))
+                if p is not None and (best is None or p < best):
+                    best = p
+            if best is None:
+                return None, False
+            return containers[best], True
+        return find
+
     def get_container(self, imagename):
         for c in self.containers:
             if common.is_string_present(c.image_names, imagename):

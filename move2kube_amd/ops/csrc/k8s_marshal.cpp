@@ -61,9 +61,28 @@ struct Schema {
   PyObject* fallback = nullptr;  // (value, type) -> marshalled value
   PyObject* zero = nullptr;      // 0
   PyObject* empty_str = nullptr;  // ""
+  bool ready = false;             // set once every struct compiled
 };
 
 static Schema* g = nullptr;
+
+// Drop a schema whose compilation failed part-way, so that no marshal call can
+// see a struct without its field table and a later init starts afresh.
+static void discard_schema() {
+  if (g == nullptr) return;
+  for (Type& t : g->types) Py_XDECREF(t.name);
+  for (Struct& s : g->structs) {
+    for (Field& f : s.fields) Py_XDECREF(f.jname);
+    Py_XDECREF(s.keyed);
+    Py_XDECREF(s.base);
+    Py_XDECREF(s.empty);
+  }
+  Py_XDECREF(g->fallback);
+  Py_XDECREF(g->zero);
+  Py_XDECREF(g->empty_str);
+  delete g;
+  g = nullptr;
+}
 
 static int compile_type(const std::string& t);
 
@@ -359,17 +378,28 @@ extern "C" PyObject* m2k_schema_init(PyObject* structs, PyObject* fb) {
     PyErr_SetString(PyExc_TypeError, "structs must be a dict");
     return nullptr;
   }
-  if (g == nullptr) g = new Schema();
-  if (!g->structs.empty()) Py_RETURN_NONE;  // already compiled (the table never changes)
+  if (g != nullptr && g->ready) Py_RETURN_NONE;  // already compiled (the table never changes)
+  discard_schema();
+  g = new Schema();
   g->zero = PyLong_FromLong(0);
   g->empty_str = PyUnicode_FromString("");
+  if (g->zero == nullptr || g->empty_str == nullptr) {
+    discard_schema();
+    return nullptr;
+  }
   Py_INCREF(fb);
   g->fallback = fb;
   Py_ssize_t pos = 0;
   PyObject *name, *fields;
   while (PyDict_Next(structs, &pos, &name, &fields)) {
+    const char* nm = PyUnicode_Check(name) ? PyUnicode_AsUTF8(name) : nullptr;
+    if (nm == nullptr) {
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "struct names must be str");
+      discard_schema();
+      return nullptr;
+    }
     Struct s;
-    s.name = PyUnicode_AsUTF8(name);
+    s.name = nm;
     g->struct_index[s.name] = (int)g->structs.size();
     g->structs.push_back(std::move(s));
   }
@@ -378,15 +408,30 @@ extern "C" PyObject* m2k_schema_init(PyObject* structs, PyObject* fb) {
   while (PyDict_Next(structs, &pos, &name, &fields)) {
     Struct& s = g->structs[ix++];
     s.keyed = PyDict_New();
-    PyObject* seq = PySequence_Fast(fields, "fields must be a sequence");
-    if (!seq) return nullptr;
+    PyObject* seq = s.keyed ? PySequence_Fast(fields, "fields must be a sequence") : nullptr;
+    if (!seq) {
+      discard_schema();
+      return nullptr;
+    }
     Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
     for (Py_ssize_t i = 0; i < n; ++i) {
       PyObject* item = PySequence_Fast_GET_ITEM(seq, i);
       PyObject *jn, *ft, *om;
-      if (!PyArg_ParseTuple(item, "UUO", &jn, &ft, &om)) { Py_DECREF(seq); return nullptr; }
-      std::string jname = PyUnicode_AsUTF8(jn), ftype = PyUnicode_AsUTF8(ft);
-      bool omit = PyObject_IsTrue(om) == 1;
+      const char *jc = nullptr, *fc = nullptr;
+      if (!PyArg_ParseTuple(item, "UUO", &jn, &ft, &om) || (jc = PyUnicode_AsUTF8(jn)) == nullptr ||
+          (fc = PyUnicode_AsUTF8(ft)) == nullptr) {
+        Py_DECREF(seq);
+        discard_schema();
+        return nullptr;
+      }
+      std::string jname = jc, ftype = fc;
+      int truth = PyObject_IsTrue(om);
+      if (truth < 0) {
+        Py_DECREF(seq);
+        discard_schema();
+        return nullptr;
+      }
+      bool omit = truth == 1;
       Field f;
       Py_INCREF(jn);
       f.jname = jn;
@@ -398,26 +443,35 @@ extern "C" PyObject* m2k_schema_init(PyObject* structs, PyObject* fb) {
       if (f.inline_) {
         auto si = g->struct_index.find(ftype);
         if (si == g->struct_index.end()) {
+          Py_DECREF(jn);
           PyErr_Format(PyExc_ValueError, "inline type %s is not a struct", ftype.c_str());
           Py_DECREF(seq);
+          discard_schema();
           return nullptr;
         }
         s.inlines.push_back(si->second);
       } else {
         PyObject* idx = PyLong_FromSsize_t((Py_ssize_t)s.fields.size());
-        PyDict_SetItem(s.keyed, jn, idx);
-        Py_DECREF(idx);
+        int rc = idx ? PyDict_SetItem(s.keyed, jn, idx) : -1;
+        Py_XDECREF(idx);
+        if (rc < 0) {
+          Py_DECREF(jn);
+          Py_DECREF(seq);
+          discard_schema();
+          return nullptr;
+        }
       }
       s.fields.push_back(f);
     }
     Py_DECREF(seq);
   }
+  g->ready = true;
   Py_RETURN_NONE;
 }
 
 // schema_marshal(obj, type name) -> marshalled dict tree
 extern "C" PyObject* m2k_schema_marshal(PyObject* obj, PyObject* type_name) {
-  if (g == nullptr || g->structs.empty()) {
+  if (g == nullptr || !g->ready) {
     PyErr_SetString(PyExc_RuntimeError, "schema_init was not called");
     return nullptr;
   }

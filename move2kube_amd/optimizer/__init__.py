@@ -102,12 +102,15 @@ class ImagePullPolicyOptimizer:
 
 class PortMergeOptimizer:
     def optimize(self, ir):
+        find = None
         for name in sorted(ir.services):
             service = ir.services[name]
             if any(c.get("ports") for c in service.containers):
                 continue
             log.debug("The service %s has no ports", service.name)
-            p2c = self.gather_ports(ir, service)
+            if find is None:
+                find = ir.container_finder()  # containers do not change in this pass
+            p2c = self.gather_ports(ir, service, find)
             if not p2c:
                 continue
             selected = self.ask(service, p2c)
@@ -121,10 +124,11 @@ class PortMergeOptimizer:
         return ir
 
     @staticmethod
-    def gather_ports(ir, service):
+    def gather_ports(ir, service, find=None):
         p2c = {}
+        find = find or ir.get_container
         for idx, c in enumerate(service.containers):
-            irc, ok = ir.get_container(c.get("image", ""))
+            irc, ok = find(c.get("image", ""))
             if ok:
                 for port in irc.exposed_ports:
                     if port in p2c:

@@ -30,6 +30,8 @@ _GO_ESC = {"\a": "\\a", "\b": "\\b", "\f": "\\f", "\n": "\\n", "\r": "\\r", "\t"
 def go_quote(s):
     """``strconv.Quote``: what the reference's ``%q`` prints for a string.
     Bytes that were not UTF-8 (surrogateescape) come out as ``\\xNN``."""
+    if s.isascii() and s.isprintable() and '"' not in s and "\\" not in s:
+        return '"' + s + '"'
     out = ['"']
     for ch in s:
         e = _GO_ESC.get(ch)

@@ -92,8 +92,8 @@ def test_fastjson_invalid_utf8_in_strings_becomes_replacement_chars():
 
 def test_cli_entry_process_setup():
     """``python -m move2kube_amd`` (like the release launcher) imports the CLI
-    with the cyclic collector off, then freezes those objects and turns it back
-    on; shutil comes without bz2/lzma and msvcrt is recorded as absent; a
+    with the cyclic collector off, freezes those objects and leaves it off for
+    the command (``api.gc_paused``); shutil comes without bz2/lzma and msvcrt is recorded as absent; a
     library import of the package changes none of that."""
     probe = ("import atexit, gc, sys\n"
              "sys.argv = ['move2kube', 'version']\n"
@@ -103,7 +103,7 @@ def test_cli_entry_process_setup():
     env = dict(os.environ, PYTHONPATH=ROOT)
     p = subprocess.run([sys.executable, "-S", "-c", probe], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                        timeout=60)
-    assert p.stdout.decode().split() == ["v0.1.0", "True", "True", "False", "True"], p.stderr.decode()
+    assert p.stdout.decode().split() == ["v0.1.0", "False", "True", "False", "True"], p.stderr.decode()
     lib = ("import gc, sys\nimport move2kube_amd.cli.main\n"
            "print(gc.isenabled(), gc.get_freeze_count(), 'msvcrt' in sys.modules)\n")
     p = subprocess.run([sys.executable, "-S", "-c", lib], env=env, stdout=subprocess.PIPE, timeout=60)
@@ -146,3 +146,16 @@ def test_cli_runs_leave_no_unclosed_files(tmp_path):
                        cwd=str(tmp_path), stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=120)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     assert "ResourceWarning" not in p.stderr.decode()
+
+
+@pytest.mark.skipif(not os.path.exists("/dev/full"), reason="needs /dev/full")
+def test_cli_exit_reports_a_failed_stdout_flush():
+    """Output that cannot be written (ENOSPC on /dev/full) is an error, as with
+    ``sys.exit``: CPython's message on stderr and status 120."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    with open("/dev/full", "w") as full:
+        p = subprocess.run([sys.executable, "-m", "move2kube_amd", "version"], env=env, stdout=full,
+                           stderr=subprocess.PIPE, timeout=60)
+    assert p.returncode == 120
+    assert "Exception ignored in: <_io.TextIOWrapper name='<stdout>'" in p.stderr.decode()
+    assert "OSError: [Errno 28]" in p.stderr.decode()

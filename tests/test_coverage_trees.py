@@ -78,8 +78,9 @@ def test_no_tree_writes_an_invalid_selector():
 
 @pytest.mark.parametrize("profile", ["AWS-EKS", "Azure-AKS", "GCP-GKE"])
 def test_generated_ingress_keeps_networking_v1_where_profile_prefers_v1beta1(profile):
-    """networking.k8s.io/v1 -> v1beta1 fails the converter's field walk
-    (``Spec.Backend`` has no source field), so the original v1 object is written."""
+    """networking.k8s.io/v1 -> v1beta1 has no conversion function between the
+    two external packages ("unknown conversion" in apimachinery v0.19.4), so the
+    original v1 object is written."""
     ing = _objects("profiles/" + profile)["myproject-ingress.yaml"]
     assert ing["apiVersion"] == "networking.k8s.io/v1"
     assert ing["spec"]["rules"][0]["http"]["paths"][0]["backend"]["service"]["name"]
@@ -94,12 +95,12 @@ def test_carried_over_versions(profile):
     assert "selector" not in objs["legacy-ext-deployment.yaml"]["spec"]
     assert gv["old-agent-daemonset.yaml"] == "extensions/v1beta1"
     assert objs["old-agent-daemonset.yaml"]["spec"]["templateGeneration"] == 3
-    # same group, every destination field present: converted, source-only fields dropped
-    assert gv["legacy-beta1-deployment.yaml"] == "apps/v1"
-    assert "rollbackTo" not in objs["legacy-beta1-deployment.yaml"]["spec"]
-    assert gv["node-agent-daemonset.yaml"] == "apps/v1"
-    assert gv["nightly-cronjob.yaml"] == "batch/v1beta1"
-    # same group, a destination field without a source: original kept
+    # same group, other version: no conversion function (apimachinery v0.19.4
+    # has no reflection fallback), so every input object keeps its apiVersion
+    assert gv["legacy-beta1-deployment.yaml"] == "apps/v1beta1"
+    assert objs["legacy-beta1-deployment.yaml"]["spec"]["rollbackTo"] == {"revision": 1}
+    assert gv["node-agent-daemonset.yaml"] == "apps/v1beta2"
+    assert gv["nightly-cronjob.yaml"] == "batch/v2alpha1"
     assert gv["db-statefulset.yaml"] == "apps/v1beta1"
     assert gv["web-hpa-horizontalpodautoscaler.yaml"] == "autoscaling/v2beta2"
     assert gv["old-ing-ingress.yaml"] == "extensions/v1beta1"
@@ -108,8 +109,7 @@ def test_carried_over_versions(profile):
     assert gv["reader-role.yaml"] == "rbac.authorization.k8s.io/v1"
     assert gv["oc-reader-role.yaml"] == "authorization.openshift.io/v1"
     openshift = profile.endswith("Openshift")
-    assert gv["reader-binding-rolebinding.yaml"] == (
-        "rbac.authorization.k8s.io/v1beta1" if openshift else "rbac.authorization.k8s.io/v1")
+    assert gv["reader-binding-rolebinding.yaml"] == "rbac.authorization.k8s.io/v1beta1"
     if openshift:
         assert gv["new-ing-route.yaml"] == "route.openshift.io/v1"      # Ingress v1 -> Route
         assert objs["web-deploymentconfig.yaml"]["kind"] == "DeploymentConfig"

@@ -148,3 +148,25 @@ def test_wrong_shapes_raise_like_python():
                      ({"spec": {"ports": 7}}, "Service"), ({"data": ["x"]}, "Secret")):
         want, got = _both(obj, typ)
         assert got == want
+
+
+def test_failed_schema_init_leaves_no_half_built_table():
+    """A table that fails part-way (an inline field naming no struct) raises and
+    leaves nothing behind: marshal reports the missing init, and a later init
+    with the real table compiles from scratch (fresh process: the table of
+    this one is already published)."""
+    import subprocess
+    probe = ("from move2kube_amd.ops import native\n"
+             "from move2kube_amd.k8s import schema\n"
+             "m = native.module()\n"
+             "bad = {'A': [('x', 'string', False)], 'B': [('inline', 'Missing', False)]}\n"
+             "try:\n    m.schema_init(bad, schema._marshal_value)\nexcept ValueError as e:\n    print('init', e)\n"
+             "try:\n    m.schema_marshal({}, 'A')\nexcept RuntimeError as e:\n    print('marshal', e)\n"
+             "m.schema_init(schema._STRUCTS, schema._marshal_value)\n"
+             "print(m.schema_marshal({'name': 'c'}, 'Container'))\n")
+    p = subprocess.run([sys.executable, "-c", probe], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       timeout=60)
+    assert p.returncode == 0, p.stderr.decode()
+    assert p.stdout.decode().splitlines() == ["init inline type Missing is not a struct",
+                                              "marshal schema_init was not called",
+                                              "{'name': 'c', 'resources': {}}"]

@@ -141,3 +141,26 @@ def test_storage_index_agrees_with_linear_merge():
             ref.append(st_.copy())
     assert [(s.name, s.storage_type, s.content) for s in ir.storages] == \
            [(s.name, s.storage_type, s.content) for s in ref]
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.integers(min_value=0, max_value=10 ** 9))
+def test_container_finder_agrees_with_get_container(seed):
+    """``IR.container_finder`` (the port-merge optimizer's lookup) returns the
+    same container as the linear ``GetContainer`` scan (``ir.go:398-409``),
+    including the ``<registry>/<ns>/<name>`` form for new images."""
+    rng = random.Random(seed)
+    names = ["web", "WEB", "api", "db", "Straße", "STRASSE", "quay.io/x/web", "docker.io/ns/api"]
+    ir = irtypes.IR()
+    ir.kubernetes.registry_url = rng.choice(["quay.io", "docker.io", ""])
+    for _ in range(rng.randint(0, 12)):
+        c = irtypes.Container(rng.choice(["Reuse", "NewDockerfile", "CNB"]), rng.choice(names), rng.random() < 0.5)
+        for _ in range(rng.randint(0, 2)):
+            c.add_image_name(rng.choice(names))
+        ir.containers.append(c)
+    find = ir.container_finder()
+    for _ in range(20):
+        q = rng.choice(names + ["%s/%s/%s" % (ir.kubernetes.registry_url, "ns", rng.choice(names)), "nope"])
+        want, ok = ir.get_container(q)
+        got, ok2 = find(q)
+        assert ok == ok2 and got is want, q
