@@ -13,14 +13,15 @@ handler goroutines unsynchronised and hands each waiting GET its own problem
 off a channel.
 """
 
-import json
 import queue
 import socket
 import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from urllib.parse import unquote
 
 from ..models import qa
 from ..utils import fastjson, log
+from ..utils.constants import settings
 from .engine import Engine
 
 PROBLEMS_URL = "/problems"
@@ -48,17 +49,60 @@ def _json_kind(v):
     return "array" if isinstance(v, list) else "object"
 
 
+class _PartialSlice(ValueError):
+    """UnmarshalTypeError; ``partial`` is what Unmarshal still stored."""
+
+    def __init__(self, msg, partial):
+        ValueError.__init__(self, msg)
+        self.partial = partial
+
+
 def _string_slice(v):
     """``json.Unmarshal(body, &sol)`` into a ``[]string``: null is an empty
-    answer; another type is Go's UnmarshalTypeError (null elements stay "")."""
+    answer; another type is Go's UnmarshalTypeError for the first mismatch,
+    and Unmarshal still fills the slice, mismatched and null elements as ""."""
     if v is None:
         return None
     if not isinstance(v, list):
-        raise ValueError("json: cannot unmarshal %s into Go value of type []string" % _json_kind(v))
+        raise _PartialSlice("json: cannot unmarshal %s into Go value of type []string" % _json_kind(v), None)
+    out = ["" if not isinstance(x, str) else x for x in v]
     for x in v:
         if x is not None and not isinstance(x, str):
-            raise ValueError("json: cannot unmarshal %s into Go value of type string" % _json_kind(x))
-    return ["" if x is None else x for x in v]
+            raise _PartialSlice("json: cannot unmarshal %s into Go value of type string" % _json_kind(x), out)
+    return out
+
+
+_ROUTES = {CURRENT_PROBLEM_URL: "GET", CURRENT_SOLUTION_URL: "POST"}
+_STATUS_TEXT = {200: "OK", 301: "Moved Permanently", 404: "Not Found", 405: "Method Not Allowed",
+                500: "Internal Server Error"}
+
+
+def _clean_path(p):
+    """net/http's ``cleanPath``: ``path.Clean`` of the rooted path, keeping a
+    trailing slash."""
+    if p == "":
+        return "/"
+    if p[0] != "/":
+        p = "/" + p
+    parts = []
+    for seg in p.split("/"):
+        if seg in ("", "."):
+            continue
+        if seg == "..":
+            if parts:
+                parts.pop()
+            continue
+        parts.append(seg)
+    np = "/" + "/".join(parts)
+    if p.endswith("/") and np != "/":
+        np += "/"
+    return np
+
+
+def _html_escape(s):
+    """``htmlEscape`` of net/http (``htmlReplacer``)."""
+    return (s.replace("&", "&amp;").replace("<", "&lt;").replace(">", "&gt;")
+            .replace('"', "&#34;").replace("'", "&#39;"))
 
 class HTTPRESTEngine(Engine):
     go_type = "*qaengine.HTTPRESTEngine"
@@ -88,47 +132,102 @@ class HTTPRESTEngine(Engine):
         engine = self
 
         class Handler(BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"  # keep-alive like net/http
+
             def log_message(self, fmt, *args):
                 log.debug("qa-http: " + fmt, *args)
 
-            def _send(self, code, body, ctype="application/json"):
-                data = body.encode() if isinstance(body, str) else body
-                self.send_response(code)
-                self.send_header("Content-Type", ctype)
-                self.send_header("Content-Length", str(len(data)))
-                self.end_headers()
-                self.wfile.write(data)
+            def _go_reply(self, code, body=b"", headers=()):
+                """A response laid out as net/http's chunkWriter writes it:
+                the handler's own headers sorted by name, then Date,
+                Content-Length, a sniffed Content-Type (only for a non-empty
+                body without one) and Connection."""
+                http11 = self.request_version != "HTTP/1.0"
+                lines = ["%s %d %s\r\n" % ("HTTP/1.1" if http11 else "HTTP/1.0", code, _STATUS_TEXT[code])]
+                for k, v in sorted(headers):
+                    lines.append("%s: %s\r\n" % (k, v))
+                lines.append("Date: %s\r\n" % self.date_time_string())
+                if self.command != "HEAD" or body:
+                    lines.append("Content-Length: %d\r\n" % len(body))
+                if body and not any(k == "Content-Type" for k, _ in headers):
+                    lines.append("Content-Type: text/plain; charset=utf-8\r\n")
+                if self.close_connection and http11:
+                    lines.append("Connection: close\r\n")
+                elif not self.close_connection and not http11:
+                    lines.append("Connection: keep-alive\r\n")
+                lines.append("\r\n")
+                self.wfile.write("".join(lines).encode("latin-1") + (b"" if self.command == "HEAD" else body))
+                self.wfile.flush()
 
-            def do_GET(self):  # noqa: N802
-                if self.path.split("?")[0] != CURRENT_PROBLEM_URL:
-                    self._send(404, "404 page not found\n", "text/plain")
+            def _go_error(self, code, msgs):
+                """``http.Error`` (once per message: a second call only
+                appends its line, net/http ignores the superfluous header)."""
+                self._go_reply(code, "".join(m + "\n" for m in msgs).encode("utf-8"),
+                               [("Content-Type", "text/plain; charset=utf-8"), ("X-Content-Type-Options", "nosniff")])
+
+            def _dispatch(self):
+                """http.DefaultServeMux (clean-path redirect) in front of the
+                gorilla/mux router: a known path with another method is 405
+                with an empty body, an unknown path 404."""
+                raw_path, _, query = self.path.partition("?")
+                path = unquote(raw_path)
+                clean = _clean_path(path)
+                if clean != path and self.command != "CONNECT":
+                    url = clean + ("?" + query if query else "")
+                    hdrs = [("Location", url)]
+                    body = b""
+                    if self.command in ("GET", "HEAD"):
+                        hdrs.append(("Content-Type", "text/html; charset=utf-8"))
+                        if self.command == "GET":
+                            body = ('<a href="%s">Moved Permanently</a>.\n\n' % _html_escape(url)).encode("utf-8")
+                    self._go_reply(301, body, hdrs)
                     return
+                route = _ROUTES.get(path)
+                if route is None:
+                    self._go_error(404, ["404 page not found"])
+                elif route != self.command:
+                    self._go_reply(405)
+                elif route == "GET":
+                    self._problem()
+                else:
+                    self._solution()
+
+            do_GET = do_POST = do_PUT = do_DELETE = do_PATCH = do_OPTIONS = do_HEAD = _dispatch
+
+            def _problem(self):
                 log.debug("Looking for a problem fron HTTP REST service")  # sic (httprestengine.go:106)
                 prob = engine.next_problem()
                 log.debug("QA Engine serves problem id: %d, desc: %s", prob.id, prob.desc)
-                self._send(200, json.dumps(prob.to_json()) + "\n")
+                self._go_reply(200, fastjson.go_encode(prob.to_json()))
 
-            def do_POST(self):  # noqa: N802
-                if self.path.split("?")[0] != CURRENT_SOLUTION_URL:
-                    self._send(404, "404 page not found\n", "text/plain")
-                    return
+            def _solution(self):
+                n = int(self.headers.get("Content-Length") or 0)
+                body = self.rfile.read(max(0, n))
+                errs = []
                 try:
-                    n = int(self.headers.get("Content-Length") or 0)
-                    body = self.rfile.read(max(0, n))
                     sol = _string_slice(fastjson.loads(body))
+                except _PartialSlice as e:
+                    errs.append("Error in un-marshalling solution in QA engine: %s" % e)
+                    log.error("%s", errs[-1])
+                    sol = e.partial
                 except ValueError as e:
-                    errstr = "Error in un-marshalling solution in QA engine: %s" % e
-                    self._send(500, errstr + "\n", "text/plain")
-                    log.error("%s", errstr)
+                    errs.append("Error in un-marshalling solution in QA engine: %s" % e)
+                    log.error("%s", errs[-1])
+                    sol = None
+                if errs and settings.fixed:
+                    self._go_error(500, errs)
                     return
+                # the reference goes on with what Unmarshal left in the slice
+                # (httprestengine.go:127-140: no return after http.Error)
                 log.debug("QA Engine receives solution: %s", "[" + " ".join(sol or []) + "]")
                 err = engine.submit_solution(sol or [])
                 if err:
-                    errstr = "Unsuitable answer : %s" % err
-                    self._send(500, errstr + "\n", "text/plain")
-                    log.error("%s", errstr)
+                    errs.append("Unsuitable answer : %s" % err)
+                    log.error("%s", errs[-1])
+                if errs:
+                    self._go_error(500, errs)
                 else:
-                    self._send(200, "")
+                    self._go_reply(200)
 
         try:
             self.server = ThreadingHTTPServer((self.host, self.port), Handler)
@@ -152,16 +251,20 @@ class HTTPRESTEngine(Engine):
             return self.current.copy()
 
     def submit_solution(self, sol):
+        """``h.currentProblem.SetAnswer(sol)``: applied to the open problem
+        itself, so a rejected answer leaves what SetAnswer already changed
+        (a select's answer becomes ``[]``) for the next GET to show.  With no
+        open problem the reference's handler blocks forever on the answer
+        channel; here it is an error."""
         with self._cond:
             if self.current.id == 0 or self.current.resolved:
                 return "no open problem"
-            p = self.current.copy()
             try:
-                p.set_answer(sol)
+                self.current.set_answer(sol)
             except qa.ProblemError as e:
                 return str(e)
-            self.current = p
-        self.answers.put(p.copy())
+            p = self.current.copy()
+        self.answers.put(p)
         return None
 
     # called from the translator thread

@@ -1,7 +1,8 @@
 """JSON decoding straight on the C scanner (``_json.make_scanner``), the one
 the stdlib ``json`` package wraps, so the read paths of a command (cluster
 profiles, detector output, ``~/.docker/config.json``) do not import the
-four-module ``json`` package.  Encoding still goes through ``json``.
+four-module ``json`` package.  :func:`go_encode` writes what Go's
+``json.NewEncoder(w).Encode`` writes (the REST QA engine's responses).
 
 What is accepted and the error text follow Go's ``encoding/json`` (what the
 reference decodes detector output, ``docker inspect`` and the CLI tools' JSON
@@ -74,6 +75,78 @@ def loads(s, parse_int=int):
 
 def load(f, parse_int=int):
     return loads(f.read(), parse_int)
+
+
+# ---------------------------------------------------------------------------
+# Go's encoder (encoding/json encodeState, escapeHTML on)
+# ---------------------------------------------------------------------------
+
+_GO_ENC_ESC = {'"': '\\"', "\\": "\\\\", "\n": "\\n", "\r": "\\r", "\t": "\\t",
+               "<": "\\u003c", ">": "\\u003e", "&": "\\u0026",
+               "\u2028": "\\u2028", "\u2029": "\\u2029"}
+
+
+def _go_string(s):
+    """``encodeState.string`` (Go 1.15): compact escapes only for quote,
+    backslash, newline, carriage return and tab, ``\\u00XX`` for the other
+    control characters (``\\b`` and ``\\f`` included), ``<``, ``>``, ``&`` and
+    U+2028/U+2029 as ``\\uXXXX``, every other character raw UTF-8; a lone
+    surrogate (undecodable input) becomes U+FFFD."""
+    out = []
+    for ch in s:
+        e = _GO_ENC_ESC.get(ch)
+        if e is not None:
+            out.append(e)
+        elif ch < " ":
+            out.append("\\u%04x" % ord(ch))
+        elif "\ud800" <= ch <= "\udfff":
+            out.append("\ufffd")
+        else:
+            out.append(ch)
+    return '"' + "".join(out) + '"'
+
+
+def _go_value(v, out):
+    if v is None:
+        out.append("null")
+    elif v is True:
+        out.append("true")
+    elif v is False:
+        out.append("false")
+    elif isinstance(v, int):
+        out.append(str(v))
+    elif isinstance(v, float):
+        out.append(repr(v) if v != int(v) or abs(v) >= 1e21 else str(int(v)))
+    elif isinstance(v, str):
+        out.append(_go_string(v))
+    elif isinstance(v, dict):
+        out.append("{")
+        for i, (k, x) in enumerate(v.items()):
+            if i:
+                out.append(",")
+            out.append(_go_string(str(k)))
+            out.append(":")
+            _go_value(x, out)
+        out.append("}")
+    elif isinstance(v, (list, tuple)):
+        out.append("[")
+        for i, x in enumerate(v):
+            if i:
+                out.append(",")
+            _go_value(x, out)
+        out.append("]")
+    else:
+        raise TypeError("json: unsupported type: %s" % type(v).__name__)
+
+
+def go_encode(v):
+    """``json.NewEncoder(w).Encode(v)`` of a value whose dicts hold the Go
+    struct's fields in declaration order: compact, HTML-escaped, one trailing
+    newline; returned as UTF-8 bytes."""
+    out = []
+    _go_value(v, out)
+    out.append("\n")
+    return "".join(out).encode("utf-8")
 
 
 # ---------------------------------------------------------------------------

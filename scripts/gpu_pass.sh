@@ -1,0 +1,29 @@
+# One pass on the GPU box into gpurun_out/$RUN/:
+#   pytest -m gpu, smoke(), bench.py with its default checks (per-config diffs,
+#   warm/cold p50s, large-tree ratio), rocprofv3 kernel stats of smoke(), and,
+#   when AB names a tree under .ab_base/, the interleaved same-box A/B of the
+#   headline against it (benchmarks/ab_bench.py).
+# Every GPU step has its own time limit; the first failure ends the pass.
+#   RUN=r04_x AB=r03 gpurun --timeout 1200 -- bash scripts/gpu_pass.sh
+set -eo pipefail
+cd "$GRAFT_REPO_ROOT"
+RUN=${RUN:-pass}
+OUT=gpurun_out/$RUN
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+echo "pytest -m gpu"
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+tail -1 "$OUT/pytest_gpu.log"
+echo "smoke"
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+echo "bench"
+timeout -k 10 600 python -u bench.py > "$OUT/bench.log" 2>&1
+grep '^{' "$OUT/bench.log" > "$OUT/bench.json"
+python -c 'import json,sys; d=json.load(open(sys.argv[1])); print(d["ms_per_step"], d["step_ms"], d["manifest_diff_vs_ref"], d["per_config"]["large-tree"]["ratio_largest_vs_smallest"])' "$OUT/bench.json"
+echo "rocprof smoke"
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof" -o smoke -- python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/rocprof_smoke.log" 2>&1
+if [ -n "$AB" ]; then
+  echo "A/B vs $AB"
+  timeout -k 10 900 python -u benchmarks/ab_bench.py --base ".ab_base/$AB" --pairs "${AB_PAIRS:-4}" --out "$OUT/ab.jsonl"
+fi
+echo done

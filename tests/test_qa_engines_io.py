@@ -90,14 +90,19 @@ def test_rest_engine_concurrent_gets_and_bad_requests():
         for g in getters:
             g.join(20)
         assert seen == ["first"] * 4
-        # json.Unmarshal(body, &sol []string) errors, http.Error text (httprestengine.go)
+        # json.Unmarshal(body, &sol []string) errors, http.Error text; the
+        # handler does not return after it (httprestengine.go:127-140), so
+        # SetAnswer runs on what Unmarshal left and adds its own error line
         pre = "Error in un-marshalling solution in QA engine: "
         assert _post(e.port, "/problems/current/solution", "{not json") == \
-            (500, pre + "invalid character 'n' looking for beginning of object key string\n")
+            (500, pre + "invalid character 'n' looking for beginning of object key string\n"
+             "Unsuitable answer : The answer slice is empty\n")
         assert _post(e.port, "/problems/current/solution", '[1, 2]') == \
-            (500, pre + "json: cannot unmarshal number into Go value of type string\n")
+            (500, pre + "json: cannot unmarshal number into Go value of type string\n"
+             "Unsuitable answer : The question type is not multiselect, but there are multiple answers\n")
         assert _post(e.port, "/problems/current/solution", '{"a": "b"}') == \
-            (500, pre + "json: cannot unmarshal object into Go value of type []string\n")
+            (500, pre + "json: cannot unmarshal object into Go value of type []string\n"
+             "Unsuitable answer : The answer slice is empty\n")
         assert _post(e.port, "/problems/current/solution", '["one"]')[0] == 200
         assert json.loads(_get(e.port, "/problems/current")[1])["description"] == "second"
         assert _post(e.port, "/problems/current/solution", '["two"]')[0] == 200
@@ -105,6 +110,116 @@ def test_rest_engine_concurrent_gets_and_bad_requests():
         assert answers == ["one", "two"]
     finally:
         e.stop()
+
+
+def _raw(port, request):
+    """One request on a fresh socket; the response bytes with the Date value
+    blanked (Content-Length framing, the connection stays open)."""
+    import re
+    import socket
+    with socket.create_connection(("127.0.0.1", port), timeout=20) as c:
+        c.sendall(request)
+        data = b""
+        while b"\r\n\r\n" not in data:
+            data += c.recv(65536)
+        head, _, body = data.partition(b"\r\n\r\n")
+        m = re.search(rb"Content-Length: (\d+)", head)
+        n = int(m.group(1)) if m else 0
+        while len(body) < n:
+            body += c.recv(65536)
+    return re.sub(rb"Date: [^\r]+", b"Date: X", head) + b"\r\n\r\n" + body
+
+
+def test_rest_engine_wire_bytes_follow_net_http():
+    """What ``json.NewEncoder(w).Encode`` and net/http put on the wire
+    (httprestengine.go:67-69,113): compact JSON, raw UTF-8, ``<``/``>``/``&``
+    as ``\\u003c``/``\\u003e``/``\\u0026``, a trailing newline, a sniffed
+    ``text/plain`` type after Date and Content-Length; gorilla/mux answers a
+    known path with the wrong method 405 with an empty body, an unknown path
+    ``http.Error``'s 404; DefaultServeMux redirects an unclean path."""
+    e = HTTPRESTEngine(0, "127.0.0.1")
+    qaengine.reset()
+    qaengine.add_engine(e)
+    got = {}
+
+    def ask():
+        p = qa.new_select_problem("Expose <svc> & café?", ["a\tb"], "é", ["é", "<none>"])
+        got["ans"] = qaengine.fetch_answer(p).get_string_answer()
+
+    t = threading.Thread(target=ask, daemon=True)
+    t.start()
+    try:
+        body = ('{"id":%d,"description":"Expose \\u003csvc\\u003e \\u0026 café?","context":["a\\tb"],'
+                '"solution":{"type":"Select","default":["é"],"options":["é","\\u003cnone\\u003e"],"answer":[]}}\n')
+        resp = _raw(e.port, b"GET /problems/current HTTP/1.1\r\nHost: x\r\n\r\n")
+        pid = json.loads(resp.partition(b"\r\n\r\n")[2])["id"]
+        want = body % pid
+        assert resp == (b"HTTP/1.1 200 OK\r\nDate: X\r\nContent-Length: %d\r\n"
+                        b"Content-Type: text/plain; charset=utf-8\r\n\r\n" % len(want.encode()) + want.encode())
+        assert _raw(e.port, b"POST /problems/current HTTP/1.1\r\nHost: x\r\nContent-Length: 0\r\n\r\n") == \
+            b"HTTP/1.1 405 Method Not Allowed\r\nDate: X\r\nContent-Length: 0\r\n\r\n"
+        assert _raw(e.port, b"GET /problems/current/solution HTTP/1.1\r\nHost: x\r\n\r\n") == \
+            b"HTTP/1.1 405 Method Not Allowed\r\nDate: X\r\nContent-Length: 0\r\n\r\n"
+        assert _raw(e.port, b"GET /nope HTTP/1.1\r\nHost: x\r\n\r\n") == (
+            b"HTTP/1.1 404 Not Found\r\nContent-Type: text/plain; charset=utf-8\r\n"
+            b"X-Content-Type-Options: nosniff\r\nDate: X\r\nContent-Length: 19\r\n\r\n404 page not found\n")
+        assert _raw(e.port, b"GET /problems//current?a=1 HTTP/1.1\r\nHost: x\r\n\r\n") == (
+            b"HTTP/1.1 301 Moved Permanently\r\nContent-Type: text/html; charset=utf-8\r\n"
+            b"Location: /problems/current?a=1\r\nDate: X\r\nContent-Length: 56\r\n\r\n"
+            b'<a href="/problems/current?a=1">Moved Permanently</a>.\n\n')
+        # a rejected option, then an accepted one
+        sol = b'["<x>"]'
+        assert _raw(e.port, b"POST /problems/current/solution HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n%s"
+                    % (len(sol), sol)) == (
+            b"HTTP/1.1 500 Internal Server Error\r\nContent-Type: text/plain; charset=utf-8\r\n"
+            b"X-Content-Type-Options: nosniff\r\nDate: X\r\nContent-Length: 45\r\n\r\n"
+            b"Unsuitable answer : Unknown options selected\n")
+        sol = '["é"]'.encode()
+        assert _raw(e.port, b"POST /problems/current/solution HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n%s"
+                    % (len(sol), sol)) == b"HTTP/1.1 200 OK\r\nDate: X\r\nContent-Length: 0\r\n\r\n"
+        t.join(20)
+        assert got["ans"] == "é"
+    finally:
+        e.stop()
+
+
+def test_rest_engine_bad_body_still_answers_a_multiselect():
+    """The reference's fall-through after an unmarshal error: for a
+    multi-select, SetAnswer(nil) succeeds, so the translator goes on with no
+    selection while the client gets the 500.  ``M2K_COMPAT=fixed`` stops at the
+    error instead."""
+    from move2kube_amd.utils.constants import settings
+    for fixed in (False, True):
+        e = HTTPRESTEngine(0, "127.0.0.1")
+        qaengine.reset()
+        qaengine.add_engine(e)
+        got = {}
+
+        def ask():
+            p = qa.new_multiselect_problem("Pick", [], ["a"], ["a", "b"])
+            got["ans"] = qaengine.fetch_answer(p).get_slice_answer()
+
+        saved = settings.compat
+        settings.compat = "fixed" if fixed else "reference"
+        t = threading.Thread(target=ask, daemon=True)
+        t.start()
+        try:
+            _get(e.port, "/problems/current")
+            code, body = _post(e.port, "/problems/current/solution", "{bad")
+            assert code == 500
+            assert body == "Error in un-marshalling solution in QA engine: invalid character 'b' looking for " \
+                           "beginning of object key string\n"
+            t.join(2 if not fixed else 0.3)
+            if fixed:
+                assert t.is_alive()
+                assert _post(e.port, "/problems/current/solution", '["b"]')[0] == 200
+                t.join(20)
+                assert got["ans"] == ["b"]
+            else:
+                assert got["ans"] == []
+        finally:
+            settings.compat = saved
+            e.stop()
 
 
 def test_cli_engine_select_confirm_input_multiselect():
