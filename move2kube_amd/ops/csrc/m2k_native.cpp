@@ -60,12 +60,20 @@ struct WalkResult {
   std::vector<std::pair<std::string, std::string>> errors;
 };
 
+// Go's syscall.Errno text: strerror with a lower-case first letter
+// ("permission denied"), as filepath.Walk's errors print it.
+static std::string go_errstr(int e) {
+  std::string s = strerror(e);
+  if (!s.empty() && s[0] >= 'A' && s[0] <= 'Z') s[0] = (char)(s[0] - 'A' + 'a');
+  return s;
+}
+
 void walk_dir(const std::string &dir, WalkResult &r) {
   r.paths.push_back(dir);
   r.kinds.push_back(K_DIR);
   DIR *d = opendir(dir.c_str());
   if (!d) {
-    r.errors.emplace_back(dir, std::string("open ") + dir + ": " + strerror(errno));
+    r.errors.emplace_back(dir, std::string("open ") + dir + ": " + go_errstr(errno));
     return;
   }
   int dfd = dirfd(d);
@@ -88,7 +96,7 @@ void walk_dir(const std::string &dir, WalkResult &r) {
     if (t == DT_UNKNOWN) {
       struct stat st;
       if (fstatat(dfd, e.name.c_str(), &st, AT_SYMLINK_NOFOLLOW) != 0) {
-        r.errors.emplace_back(p, std::string("lstat ") + p + ": " + strerror(errno));
+        r.errors.emplace_back(p, std::string("lstat ") + p + ": " + go_errstr(errno));
         continue;
       }
       if (S_ISDIR(st.st_mode)) t = DT_DIR;
@@ -112,7 +120,7 @@ py::tuple walk(const std::string &root) {
     py::gil_scoped_release nogil;
     struct stat st;
     if (lstat(root.c_str(), &st) != 0) {
-      r.errors.emplace_back(root, std::string("lstat ") + root + ": " + strerror(errno));
+      r.errors.emplace_back(root, std::string("lstat ") + root + ": " + go_errstr(errno));
     } else if (S_ISDIR(st.st_mode)) {
       walk_dir(root, r);
     } else {

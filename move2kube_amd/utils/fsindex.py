@@ -291,6 +291,11 @@ class FileIndex:
         return k < len(pos) and pos[k] < hi
 
 
+def _go_errno_text(code):
+    from .common import go_errno_text
+    return go_errno_text(code)
+
+
 def _walk_py(root):
     paths, kinds, errors = [], [], []
     try:
@@ -310,7 +315,7 @@ def _walk_py(root):
             with os.scandir(d) as it:
                 entries = sorted((e.name, e) for e in it)
         except OSError as e:
-            errors.append((d, str(e)))
+            errors.append((d, "open %s: %s" % (d, _go_errno_text(e.errno))))
             return
         for name, e in entries:
             p = d + "/" + name if d != "/" else "/" + name
@@ -324,7 +329,7 @@ def _walk_py(root):
                     paths.append(p)
                     kinds.append(FILE if e.is_file(follow_symlinks=False) else OTHER)
             except OSError as ex:
-                errors.append((p, str(ex)))
+                errors.append((p, "lstat %s: %s" % (p, _go_errno_text(ex.errno))))
     rec(root)
     return paths, kinds, errors
 

@@ -13,7 +13,7 @@ import io
 import os
 import tarfile
 
-from . import log
+from . import common, log
 from .constants import DEFAULT_DIRECTORY_PERMISSION
 
 
@@ -53,11 +53,13 @@ def tar_as_string(path, ignore_files=()):
             if add(path):
                 walk(path)
         except OSError as e:
-            err = e
-            log.warning("Failed to create tar string: %s : %s", path, e)
+            # the Walk callback's os.Open (a file's contents, a directory's
+            # names) is what fails on a path without permissions
+            err = common.go_path_error(e, "open")
+            log.warning("Failed to create tar string: %s : %s", path, err)
     s = base64.b64encode(buf.getvalue()).decode()
     if err is not None:
-        raise TarError(str(err))
+        raise TarError(err)
     return s
 
 

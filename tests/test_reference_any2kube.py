@@ -67,18 +67,22 @@ def test_empty_dir(tmp_path, assets_dir):
     assert Any2KubeTranslator().get_service_options(str(tmp_path), plantypes.new_plan()) == []
 
 
-def test_unreadable_entries(tmp_path, assets_dir):
-    if os.geteuid() == 0:
-        pytest.skip("root can read chmod-0 files")
-    d = tmp_path / "locked"
-    d.mkdir()
-    (tmp_path / "f").write_text("x")
-    os.chmod(str(d), 0)
-    os.chmod(str(tmp_path / "f"), 0)
-    try:
-        assert Any2KubeTranslator().get_service_options(str(tmp_path), plantypes.new_plan()) == []
-    finally:
-        os.chmod(str(d), 0o755)
+def test_unreadable_entries(unprivileged):
+    """any2kube_test.go:72-95: a subdirectory with mode 0 and an unreadable
+    ``.m2kignore`` give no services and no error."""
+    root = unprivileged.tmp
+    os.mkdir(os.path.join(root, "nopermstoread"))
+    with open(os.path.join(root, ".m2kignore"), "w") as f:
+        f.write("foo/")
+    unprivileged.chown()
+    os.chmod(os.path.join(root, "nopermstoread"), 0)
+    os.chmod(os.path.join(root, ".m2kignore"), 0)
+
+    def check():
+        from move2kube_amd.utils import fsindex
+        fsindex.invalidate()
+        assert Any2KubeTranslator().get_service_options(root, plantypes.new_plan()) == []
+    unprivileged.run(check)
 
 
 def test_nodejs_app_empty_plan(layout):

@@ -45,17 +45,19 @@ def test_get_files(common_cwd, fn, keys, want):
     assert fn("empty", keys) == []
 
 
-@pytest.mark.skipif(_as_root, reason="root reads mode-0 directories")
-@pytest.mark.parametrize("fn,keys", [(common.get_files_by_ext, [".yaml"]), (common.get_files_by_name, ["a.yaml"])])
-def test_get_files_unreadable_directory(tmp_path, fn, keys):
-    d = tmp_path / "app1"
-    d.mkdir(mode=0)
-    try:
+@pytest.mark.parametrize("fn,keys", [(common.get_files_by_ext, [".yaml", ".yml"]), (common.get_files_by_name, ["a.yaml"])])
+def test_get_files_unreadable_directory(unprivileged, fn, keys):
+    """utils_test.go:76-87: a directory without permissions is an error."""
+    d = os.path.join(unprivileged.tmp, "app1")
+    os.mkdir(d)
+    unprivileged.chown()
+    os.chmod(d, 0)
+
+    def check():
         fsindex.invalidate()
         with pytest.raises(OSError):
-            fn(str(d), keys)
-    finally:
-        d.chmod(0o755)
+            fn(d, keys)
+    unprivileged.run(check)
 
 
 def test_write_yaml(tmp_path):

@@ -105,16 +105,28 @@ def test_qa_cache_loader(md_cwd, d, want):
     assert p.qa_caches == want
 
 
-def test_qa_cache_loader_unreadable_file(md_cwd):
-    if os.geteuid() == 0:
-        pytest.skip("root can read chmod-0 files")
-    d = md_cwd / "badperm"
-    d.mkdir()
-    shutil.copy("testdata/qa/valid/valid.yaml", str(d / "valid.yaml"))
-    os.chmod(str(d / "valid.yaml"), 0)
-    p = plantypes.new_plan()
-    metadata.QACacheLoader().update_plan(str(d), p)
-    assert p.qa_caches == []
+def test_qa_cache_loader_unreadable_file(md_cwd, unprivileged):
+    """``TestBadPerm`` (qacaches_test.go:77-89): a directory with mode 0 is an
+    error and the plan stays empty; a QA cache file with mode 0 inside a
+    readable directory is skipped."""
+    d = os.path.join(unprivileged.tmp, "badperm")
+    os.mkdir(d)
+    shutil.copy("testdata/qa/valid/valid.yaml", os.path.join(d, "valid.yml"))
+    f = os.path.join(unprivileged.tmp, "badfile")
+    os.mkdir(f)
+    shutil.copy("testdata/qa/valid/valid.yaml", os.path.join(f, "valid.yaml"))
+    unprivileged.chown()
+    os.chmod(d, 0)
+    os.chmod(os.path.join(f, "valid.yaml"), 0)
+
+    def check():
+        p = plantypes.new_plan()
+        with pytest.raises(OSError):
+            metadata.QACacheLoader().update_plan(d, p)
+        assert p.qa_caches == []
+        metadata.QACacheLoader().update_plan(f, p)
+        assert p.qa_caches == []
+    unprivileged.run(check)
 
 
 def test_qa_cache_load_to_ir_registers_engine(md_cwd):

@@ -83,13 +83,20 @@ def test_tar_while_ignoring_some_files(tmp_path):
     assert "test2.yml" not in [m[0] for m in got]
 
 
-@pytest.mark.skipif(os.geteuid() == 0, reason="root can read mode-000 files")
-def test_tar_unreadable_file_fails(tmp_path):
-    p = tmp_path / "nopermstoread"
-    p.write_text("no permission to read this file")
-    os.chmod(str(p), 0)
-    with pytest.raises(Exception):
-        tarutil.tar_as_string(str(p), [])
+def test_tar_unreadable_file_fails(unprivileged):
+    """tar_test.go:231-240: a file without read permission cannot be tarred."""
+    p = os.path.join(unprivileged.tmp, "nopermstoread")
+    with open(p, "w") as f:
+        f.write("no permission to read this file")
+    unprivileged.chown()
+    os.chmod(p, 0)
+
+    def check():
+        with pytest.raises(tarutil.TarError, match=r"^open %s: permission denied$" % p):
+            tarutil.tar_as_string(p, [])
+        with pytest.raises(tarutil.TarError, match=r"^open %s: permission denied$" % p):
+            tarutil.tar_as_string(unprivileged.tmp, [])
+    unprivileged.run(check)
 
 
 @pytest.fixture(scope="module")
@@ -113,15 +120,17 @@ def test_untar_invalid_tar(untar_data, tmp_path):
         tarutil.untar_string(untar_data["untar_an_invalid_tarstring"], str(tmp_path))
 
 
-@pytest.mark.skipif(os.geteuid() == 0, reason="root ignores directory permissions")
 @pytest.mark.parametrize("key", ["untar_into_a_directory_we_dont_have_permission_to_write_to",
                                  "untar_a_single_file_into_a_directory_we_dont_have_permission_to_write_to"])
-def test_untar_into_unwritable_dir(untar_data, tmp_path, key):
-    d = tmp_path / "nopermstowrite"
-    d.mkdir()
-    os.chmod(str(d), 0)
-    try:
-        with pytest.raises(Exception):
-            tarutil.untar_string(untar_data[key], str(d / "foobar"))
-    finally:
-        os.chmod(str(d), 0o755)
+def test_untar_into_unwritable_dir(untar_data, unprivileged, key):
+    """tar_test.go:281-305: untarring below a directory with mode 0 fails."""
+    d = os.path.join(unprivileged.tmp, "nopermstowrite")
+    os.mkdir(d)
+    unprivileged.chown()
+    os.chmod(d, 0)
+    data = untar_data[key]
+
+    def check():
+        with pytest.raises(OSError):
+            tarutil.untar_string(data, os.path.join(d, "foobar"))
+    unprivileged.run(check)
