@@ -7,7 +7,6 @@ under ``<out>/m2k_collect/<area>/``.  Collectors are selected by annotation
 """
 
 import os
-import subprocess
 import threading
 
 from ..utils import log
@@ -45,15 +44,15 @@ def run(argv, combined=False, timeout=300):
 
     Collectors run concurrently, but two ``cf`` commands never do: the cf
     CLI rewrites ``~/.cf/config.json`` when it refreshes its token."""
-    from ..utils.common import run_command
+    from ..utils import proc
+    from ..utils.common import run_tool
     lock = _SERIAL_CLIS.get(os.path.basename(argv[0])) if argv else None
-    kw = dict(stdout=subprocess.PIPE, stderr=subprocess.STDOUT if combined else subprocess.PIPE,
-              stdin=subprocess.DEVNULL, timeout=timeout)
+    kw = dict(stdout=proc.PIPE, stderr=proc.STDOUT if combined else proc.PIPE, timeout=timeout)
     if lock is not None:
         with lock:
-            p = run_command(argv, **kw)
+            p = run_tool(argv, **kw)
     else:
-        p = run_command(argv, **kw)
+        p = run_tool(argv, **kw)
     if p.returncode != 0:
         raise CommandError(argv, p.returncode, p.stdout)
     return p.stdout

@@ -15,7 +15,7 @@ import os
 import shutil
 import threading
 
-from ...utils import common, fastjson, log
+from ...utils import common, fastjson, log, proc
 from ...utils.constants import settings
 from ...utils.lazyre import LazyModule
 
@@ -289,8 +289,25 @@ def parallel_map(fn, items, workers=None):
 
 
 def _run(cmd, timeout=600):
-    return common.run_command(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
-                              timeout=timeout)
+    return common.run_tool(cmd, stdout=proc.PIPE, stderr=proc.STDOUT, timeout=timeout)
+
+
+def _run_many(cmds, parallel=None, timeout=RUN_TIMEOUT_S):
+    """:func:`_run` of every command, up to ``parallel`` at once; an error is
+    returned in its slot."""
+    return common.run_tools(cmds, parallel=parallel, stdout=proc.PIPE, stderr=proc.STDOUT, timeout=timeout)
+
+
+def _collect(children, timeout):
+    """Results of started children (or their start errors), in order."""
+    out = []
+    for c in children:
+        if isinstance(c, BaseException):
+            out.append(c)
+            continue
+        r = c.wait(timeout)
+        out.append(proc._timeout_error(r, timeout) if r.timed_out else r)
+    return out
 
 
 def _go_err(proc_or_exc, argv0):
@@ -310,14 +327,60 @@ class ContainerRuntimeProvider:
     """``containerRuntimeProvider`` (containerruntimeprovider.go): podman with
     the vfs storage driver."""
 
+    HELLO = ["podman", "run", "--storage-driver=vfs", "--rm", "hello-world"]
+
     def __init__(self):
         self.runtime = None  # "podman" | "none"
         self.available = set()
+        self._hello = None   # prefetched runtime probe (a result or its exception)
+        self._images = {}    # builder -> prefetched `images -q` (a result or its exception)
+
+    @staticmethod
+    def _images_cmd(rt, builder):
+        return [rt, "--storage-driver=vfs", "images", "-q", builder]
+
+    @staticmethod
+    def _images_run(rt, builder):
+        return proc.run(ContainerRuntimeProvider._images_cmd(rt, builder), stdout=proc.PIPE, stderr=proc.DEVNULL,
+                        timeout=600)
+
+    def prefetch(self, builders):
+        """Start the runtime probe and the local-image checks of ``builders``
+        at once.  The reference runs them one after another
+        (containerruntimeprovider.go:45-95); both are read-only, so their
+        results are taken in that order later by :meth:`get_runtime` and
+        :meth:`is_builder_available`, with the same logs and decisions.  The
+        image checks of a runtime that then fails its probe are discarded."""
+        if self.runtime == "none":
+            return
+        todo = [b for b in dict.fromkeys(builders) if b not in self.available and b not in self._images]
+        hello = self.runtime is None and self._hello is None
+        if not todo and not hello:
+            return
+        children = []
+        for b in ([None] if hello else []) + todo:
+            try:
+                if b is None:
+                    children.append(proc.spawn(self.HELLO, stdout=proc.PIPE, stderr=proc.STDOUT))
+                else:
+                    children.append(proc.spawn(self._images_cmd("podman", b), stdout=proc.PIPE, stderr=proc.DEVNULL))
+            except OSError as e:
+                children.append(e)
+        res = _collect(children, 600)
+        if hello:
+            self._hello = (res.pop(0),)
+        for b, r in zip(todo, res):
+            self._images[b] = r
 
     def get_runtime(self):
         if self.runtime is None:
             try:
-                p = _run(["podman", "run", "--storage-driver=vfs", "--rm", "hello-world"])
+                if self._hello is not None:
+                    p, self._hello = self._hello[0], None
+                    if isinstance(p, BaseException):
+                        raise p
+                else:
+                    p = _run(self.HELLO)
             except (OSError, subprocess.TimeoutExpired) as e:
                 log.debug("Podman not supported : %s : %s", _go_err(e, "podman"), "")
                 self.runtime = "none"
@@ -337,8 +400,11 @@ class ContainerRuntimeProvider:
             return True
         log.debug("Checking if the image %s exists locally", builder)
         try:
-            p = subprocess.run([rt, "--storage-driver=vfs", "images", "-q", builder], stdout=subprocess.PIPE,
-                               stderr=subprocess.DEVNULL, stdin=subprocess.DEVNULL, timeout=600)
+            p = self._images.pop(builder, None)
+            if p is None:
+                p = self._images_run(rt, builder)
+            elif isinstance(p, BaseException):
+                raise p
         except (OSError, subprocess.TimeoutExpired) as e:
             log.warning("Error while checking if the builder %s exists locally. Error: %r Output: %r", builder,
                         _go_err(e, rt), "")
@@ -393,13 +459,14 @@ class ContainerRuntimeProvider:
         the order of the pairs."""
         out = [None] * len(pairs)
         runnable = []
+        self.prefetch([b for _, b in pairs])
         for i, (path, builder) in enumerate(pairs):
             if self.is_builder_available(builder):
                 runnable.append(i)
         for i in runnable:
             log.debug("Running detect on image %s", pairs[i][1])
-        results = parallel_map(lambda i: _run(self._detect_cmd(*pairs[i])), runnable,
-                               min(settings.workers, CONTAINER_PARALLEL))
+        results = _run_many([self._detect_cmd(*pairs[i]) for i in runnable],
+                            min(settings.workers, CONTAINER_PARALLEL))
         for i, r in zip(runnable, results):
             if isinstance(r, Exception):
                 if not isinstance(r, _chain_errors()):
@@ -419,8 +486,8 @@ class ContainerRuntimeProvider:
         for b in builders:
             log.debug("Inspecting image %s", b)
         # one `inspect` per builder, concurrently
-        procs = parallel_map(lambda b: _run([rt, "inspect", "--storage-driver=vfs", "--format",
-                                             '{{ index .Config.Labels "' + ORDER_LABEL + '"}}', b]), builders)
+        procs = _run_many([[rt, "inspect", "--storage-driver=vfs", "--format",
+                            '{{ index .Config.Labels "' + ORDER_LABEL + '"}}', b] for b in builders])
         for b, p in zip(builders, procs):
             if isinstance(p, Exception):
                 raise p
@@ -442,23 +509,23 @@ class PackProvider:
     def is_builder_supported(self, path, builder):
         if not self.is_available():
             raise ProviderError("Pack not supported in this instance")
-        proc = subprocess.Popen(["pack", "build", "m2ktestcflinuxf2selector:1", "-B", builder, "-p", path],
+        child = subprocess.Popen(["pack", "build", "m2ktestcflinuxf2selector:1", "-B", builder, "-p", path],
                                 stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL)
         try:
-            for raw in proc.stdout:
+            for raw in child.stdout:
                 t = raw.decode("utf-8", "replace")
                 if "===> ANALYZING" in t:
-                    proc.kill()
+                    child.kill()
                     return True
                 if "No buildpack groups passed detection." in t:
-                    proc.kill()
+                    child.kill()
                     return False
         finally:
             try:
-                proc.kill()
+                child.kill()
             except OSError:
                 pass
-            proc.wait()
+            child.wait()
         raise ProviderError("Error while using pack")
 
     def get_all_buildpacks(self, builders):

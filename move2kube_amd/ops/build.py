@@ -43,7 +43,8 @@ def _run(cmd):
 
 
 NATIVE_SOURCES = [os.path.join(CSRC, "m2k_native.cpp"), os.path.join(CSRC, "yaml_emit.cpp"),
-                  os.path.join(CSRC, "yaml_parse.cpp"), os.path.join(CSRC, "k8s_marshal.cpp")]
+                  os.path.join(CSRC, "yaml_parse.cpp"), os.path.join(CSRC, "k8s_marshal.cpp"),
+                  os.path.join(CSRC, "proc_spawn.cpp")]
 SANITIZERS = {"address": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"],
               "thread": ["-fsanitize=thread"]}
 

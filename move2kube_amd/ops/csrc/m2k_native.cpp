@@ -10,6 +10,7 @@
 //   walk()               one lexical-order lstat walk (Go filepath.Walk order)
 //   sniff_dockerfiles()  multi-threaded "first non-ARG instruction" scan
 //   run_commands()       bounded-parallel posix_spawn pool with captured stdout
+//   proc_spawn/wait      one external tool without the subprocess module (proc_spawn.cpp)
 //   crc64_ecma/fnv64a    naming hashes (utils.go:292, compose/utils.go:121)
 //   edit_distance_batch  weighted edit distance matrix (bit-parallel LCS for 1,1,2)
 //   closest_batch        fused argmin over options for every query
@@ -918,6 +919,21 @@ static py::object schema_marshal(py::object obj, py::object type_name) {
   return py::reinterpret_steal<py::object>(r);
 }
 
+extern "C" PyObject* m2k_proc_spawn(PyObject* argv, PyObject* cwd, long out_mode, long err_mode);
+extern "C" PyObject* m2k_proc_wait(long pid, long out_fd, long err_fd, double timeout_s);
+
+static py::object proc_spawn(py::object argv, py::object cwd, long out_mode, long err_mode) {
+  PyObject* r = m2k_proc_spawn(argv.ptr(), cwd.ptr(), out_mode, err_mode);
+  if (!r) throw py::error_already_set();
+  return py::reinterpret_steal<py::object>(r);
+}
+
+static py::object proc_wait(long pid, long out_fd, long err_fd, double timeout_s) {
+  PyObject* r = m2k_proc_wait(pid, out_fd, err_fd, timeout_s);
+  if (!r) throw py::error_already_set();
+  return py::reinterpret_steal<py::object>(r);
+}
+
 PYBIND11_MODULE(_m2k_native, m) {
   m.doc() = "move2kube_amd native runtime (walk, sniff, spawn pool, hashes, edit distance)";
   m.def("walk", &walk, py::arg("root"));
@@ -939,6 +955,8 @@ PYBIND11_MODULE(_m2k_native, m) {
         py::arg("unsupported"));
   m.def("schema_init", &schema_init, py::arg("structs"), py::arg("fallback"));
   m.def("schema_marshal", &schema_marshal, py::arg("obj"), py::arg("type_name"));
+  m.def("proc_spawn", &proc_spawn, py::arg("argv"), py::arg("cwd"), py::arg("stdout"), py::arg("stderr"));
+  m.def("proc_wait", &proc_wait, py::arg("pid"), py::arg("out_fd"), py::arg("err_fd"), py::arg("timeout_s"));
   m.def("run_commands", &run_commands, py::arg("argvs"), py::arg("cwds"), py::arg("parallel") = 8,
         py::arg("timeout_s") = 0.0);
 }

@@ -334,7 +334,7 @@ class K8sTransformer(Transformer):
             log.warning("Unable to find operator-sdk. Skipping operator generation : exec: \"operator-sdk\": "
                         "executable file not found in $PATH")
             return None
-        import subprocess
+        from ..utils import proc
         opath = os.path.join(basepath, project + "-operator")
         if os.path.exists(opath):
             shutil.rmtree(opath, ignore_errors=True)
@@ -344,40 +344,32 @@ class K8sTransformer(Transformer):
         span.__enter__()
         out = common.unnamed_temp_file()  # not a pipe: nothing reads it until the tool exits
         try:
-            p = subprocess.Popen([sdk, "init", "--plugins=helm", "--helm-chart=" + chart, "--domain=io",
-                                  "--group=" + project, "--version=v1alpha1"], cwd=opath, stdout=out,
-                                 stderr=subprocess.DEVNULL, stdin=subprocess.DEVNULL)
+            child = proc.spawn([sdk, "init", "--plugins=helm", "--helm-chart=" + chart, "--domain=io",
+                                "--group=" + project, "--version=v1alpha1"], cwd=opath, stdout=out,
+                               stderr=proc.DEVNULL)
         except OSError as e:
             out.close()
             span.__exit__(None, None, None)
             log.warning("Error during operator creation : %s", e)
             return None
-        return p, out, span
+        return child, out, span
 
     @staticmethod
     def finish_operator(started):
         if started is None:
             return False
-        import threading
-        p, out, span = started
-        # a blocking waitpid wakes when the tool exits; Popen.wait(timeout=)
-        # polls with sleeps of up to 50 ms.  A timer bounds the run instead.
-        timed_out = []
-        timer = threading.Timer(OPERATOR_SDK_TIMEOUT_S, lambda: (timed_out.append(True), p.kill()))
-        timer.daemon = True
-        timer.start()
+        child, out, span = started
         try:
             try:
-                rc = p.wait()
+                r = child.wait(OPERATOR_SDK_TIMEOUT_S)  # killed when it overruns
             finally:
-                timer.cancel()
                 span.__exit__(None, None, None)
-            if timed_out:
+            if r.timed_out:
                 log.warning("Error during operator creation : timed out after %d seconds", OPERATOR_SDK_TIMEOUT_S)
                 return False
-            if rc != 0:
+            if r.returncode != 0:
                 out.seek(0)
-                log.warning("Error during operator creation : %s, %s", common.go_exit_status(rc),
+                log.warning("Error during operator creation : %s, %s", common.go_exit_status(r.returncode),
                             out.read().decode("utf-8", "replace"))
                 return False
             return True

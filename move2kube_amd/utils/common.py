@@ -570,6 +570,33 @@ def run_command(argv, **kw):
         raise
 
 
+def _go_not_found(e, argv0):
+    return isinstance(e, FileNotFoundError) and e.filename in (argv0, os.fsencode(argv0) if isinstance(argv0, str)
+                                                                else argv0)
+
+
+def run_tool(argv, **kw):
+    """:func:`utils.proc.run` (no ``subprocess`` import) whose
+    missing-executable error reads like Go's."""
+    from . import proc
+    try:
+        return proc.run(argv, **kw)
+    except FileNotFoundError as e:
+        if _go_not_found(e, argv[0]):
+            raise go_exec_error(e, os.fsdecode(argv[0])) from None
+        raise
+
+
+def run_tools(argvs, **kw):
+    """:func:`utils.proc.run_many` with Go's missing-executable errors."""
+    from . import proc
+    out = proc.run_many(argvs, **kw)
+    for i, r in enumerate(out):
+        if _go_not_found(r, argvs[i][0]):
+            out[i] = go_exec_error(r, os.fsdecode(argvs[i][0]))
+    return out
+
+
 def go_rel(base, target):
     """Go ``filepath.Rel`` (lexical; error if one is absolute and the other is not)."""
     if os.path.isabs(base) != os.path.isabs(target):

@@ -4,6 +4,8 @@
 #   when AB names a tree under .ab_base/, the interleaved same-box A/B of the
 #   headline against it (benchmarks/ab_bench.py).
 # Every GPU step has its own time limit; the first failure ends the pass.
+#   COLD_AB=<tree> adds the same A/B of cold CLI starts (ab_bench.py --cold),
+#   PHASES=1 the per-configuration cold phase split (scripts/cold_phases.py).
 #   RUN=r04_x AB=r03 gpurun --timeout 1200 -- bash scripts/gpu_pass.sh
 set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -25,5 +27,17 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 if [ -n "$AB" ]; then
   echo "A/B vs $AB"
   timeout -k 10 900 python -u benchmarks/ab_bench.py --base ".ab_base/$AB" --pairs "${AB_PAIRS:-4}" --out "$OUT/ab.jsonl"
+fi
+if [ -n "$COLD_AB" ]; then
+  echo "cold A/B vs $COLD_AB"
+  timeout -k 10 900 python -u benchmarks/ab_bench.py --base ".ab_base/$COLD_AB" --cold "${COLD_CONFIGS:-golang,java-cnb,cf,helm-openshift}" \
+    --pairs "${COLD_PAIRS:-2}" --runs 9 --timeout 400 --out "$OUT/cold_ab.jsonl"
+fi
+if [ -n "$PHASES" ]; then
+  echo "cold phases"
+  for c in golang docker-compose java-cnb cf helm-openshift; do
+    timeout -k 10 120 python -u scripts/cold_phases.py "$c" --runs 15 >> "$OUT/cold_phases.jsonl"
+  done
+  cat "$OUT/cold_phases.jsonl"
 fi
 echo done

@@ -193,14 +193,14 @@ def test_batched_probe_errors(monkeypatch):
     monkeypatch.setattr(providers.ContainerRuntimeProvider, "is_builder_available", lambda self, b: True)
     monkeypatch.setattr(providers, "providers", lambda: [p])
 
-    def bad(cmd, timeout=600):
-        raise ValueError("bad mount")
-    monkeypatch.setattr(providers, "_run", bad)
+    def bad(cmds, parallel=None, timeout=600):
+        return [ValueError("bad mount") for _ in cmds]
+    monkeypatch.setattr(providers, "_run_many", bad)
     assert providers.is_builder_supported_batch([("/a", "b1"), ("/b", "b2")]) == [False, False]
 
-    def worse(cmd, timeout=600):
-        raise RuntimeError("bug")
-    monkeypatch.setattr(providers, "_run", worse)
+    def worse(cmds, parallel=None, timeout=600):
+        return [RuntimeError("bug") for _ in cmds]
+    monkeypatch.setattr(providers, "_run_many", worse)
     with pytest.raises(RuntimeError):
         providers.is_builder_supported_batch([("/a", "b1")])
 
