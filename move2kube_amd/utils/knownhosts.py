@@ -2,16 +2,15 @@
 ``internal/common/knownhosts/knownhosts.go``).
 
 ``get_known_hosts_line`` fetches a host's public key by starting an SSH
-handshake to port 22 (as user ``git``) - done here with the ``ssh-keyscan``
-tool when available, since no SSH library ships with the runtime.  Network
-access is bounded by a short timeout and can be disabled with
-``M2K_NO_NETWORK=1``.
+handshake to port 22, as ``GetKey`` does: in process (``utils/sshwire.py``:
+the transport up to the verified key-exchange reply), with the
+``ssh-keyscan`` tool as the fallback when that fails.  Network access is
+bounded by a short timeout and can be disabled with ``M2K_NO_NETWORK=1``.
 """
 
 import base64
 import os
 import shutil
-import subprocess
 
 from . import log
 
@@ -95,13 +94,34 @@ def pick_host_key_line(lines, host):
     return best[1] if best else ""
 
 
+def fetch_line_in_process(host, timeout=5, port=22):
+    """``knownhosts.Line([host], key)`` for the key ``host`` proves it holds in
+    an SSH key exchange (``GetKey``, knownhosts.go:137-155), or '' on failure."""
+    from . import sshwire
+    try:
+        ktype, blob = sshwire.fetch_host_key(host, port=port, timeout=timeout)
+    except (OSError, sshwire.SSHError, ValueError) as e:
+        log.debug("In-process ssh handshake with %s failed : %s", host, e)
+        return ""
+    log.debug("host %s on port %d has the key of type %s", host, port, ktype)
+    return "%s %s %s" % (host, ktype, base64.b64encode(blob).decode("ascii"))
+
+
 def get_known_hosts_line(host, timeout=5):
     """``host algo base64key`` for the host, or '' when it cannot be fetched.
-    Every key type the server offers is scanned and the one a Go client would
-    negotiate is kept (:data:`GO_HOST_KEY_ORDER`)."""
-    if os.environ.get("M2K_NO_NETWORK") or shutil.which("ssh-keyscan") is None:
-        log.debug("Cannot fetch the ssh host key of %s (no ssh-keyscan or network disabled)", host)
+    The key is the one a Go client would negotiate (:data:`GO_HOST_KEY_ORDER`),
+    fetched in process; ``ssh-keyscan`` (every key type scanned, the same one
+    kept) is the fallback."""
+    if os.environ.get("M2K_NO_NETWORK"):
+        log.debug("Cannot fetch the ssh host key of %s (network disabled)", host)
         return ""
+    line = fetch_line_in_process(host, timeout)
+    if line:
+        return line
+    if shutil.which("ssh-keyscan") is None:
+        log.debug("Cannot fetch the ssh host key of %s (handshake failed, no ssh-keyscan)", host)
+        return ""
+    import subprocess
     try:
         p = subprocess.run(["ssh-keyscan", "-T", str(timeout), "-t", "rsa,ecdsa,ed25519,dsa", host],
                            stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, stdin=subprocess.DEVNULL,
