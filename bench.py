@@ -108,6 +108,38 @@ def step_spread(step_s):
     return {"min": round(ms[0], 3), "p50": q(0.5), "p90": q(0.9), "max": round(ms[-1], 3), "n": len(ms)}
 
 
+def _cpu_s():
+    """CPU seconds of this process and its reaped children (the operator-sdk
+    stand-in, detector scripts)."""
+    import resource
+    a, b = resource.getrusage(resource.RUSAGE_SELF), resource.getrusage(resource.RUSAGE_CHILDREN)
+    return a.ru_utime + a.ru_stime + b.ru_utime + b.ru_stime
+
+
+def _cgroup_throttled_us():
+    """Time the container's CPU quota held its tasks back (cgroup v2 cpu.stat);
+    None where it cannot be read."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                if line.startswith("throttled_usec"):
+                    return int(line.split()[1])
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def _host_cpus():
+    """CPUs this job may use: the affinity mask within the cgroup quota."""
+    saved = os.environ.pop("LOCAL_WORLD_SIZE", None)
+    try:
+        from move2kube_amd.utils.constants import host_threads
+        return host_threads(1 << 20)
+    finally:
+        if saved is not None:
+            os.environ["LOCAL_WORLD_SIZE"] = saved
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -167,6 +199,7 @@ def main():
                 run.step(s)
             barrier()
             step_s = []
+            thr0, cpu0 = _cgroup_throttled_us(), _cpu_s()
             t0 = time.perf_counter()
             for _ in range(args.steps):
                 ts = time.perf_counter()
@@ -174,6 +207,7 @@ def main():
                 step_s.append(time.perf_counter() - ts)
             barrier()
             elapsed = time.perf_counter() - t0
+            cpu_s, thr1 = _cpu_s() - cpu0, _cgroup_throttled_us()
             if rank == 0:
                 # untimed: one traced step for the per-phase breakdown (utils/trace.py)
                 from move2kube_amd.utils import trace
@@ -195,11 +229,16 @@ def main():
         per_config = dict(per_config or {})
         per_config["large-tree"] = large_tree_check([int(x) for x in args.large_tree.split(",")])
 
+    spread = step_spread(step_s)
+    slowest_p50 = spread["p50"] if spread else 0.0
     if dist is not None:
         dev = torch.device("cuda", torch.cuda.current_device()) if have_cuda else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, slowest_p50], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, slowest_p50 = float(t[0].item()), float(t[1].item())
+        c = torch.tensor([cpu_s], dtype=torch.float64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        cpu_s = float(c.item())
     ms = elapsed * 1000.0 / max(1, args.steps)
     value = world * n_services * args.steps / elapsed if elapsed > 0 else 0.0
     if rank == 0:
@@ -214,7 +253,14 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
-            "step_ms": step_spread(step_s),
+            "step_ms": spread,
+            # host-side accounting of the timed region, to tell a CPU-share
+            # limit from a code change when N ranks share one node's CPUs:
+            # CPU ms per step summed over ranks (children included), the
+            # slowest rank's median step, and the cgroup's quota throttling
+            "host": {"cpus": _host_cpus(), "cpu_ms_per_step_all_ranks": round(cpu_s * 1000.0 / max(1, args.steps), 3),
+                     "slowest_rank_step_p50_ms": round(slowest_p50, 3),
+                     "cgroup_throttled_ms": None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1000.0, 3)},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -117,7 +117,7 @@ def _cli_process():
 def _cli_exit(rc):
     """End the CLI process the way ``sys.exit(rc)`` would, without the
     interpreter's teardown of every module and object (3 ms and more of a cold
-    ``translate``, ``scripts/exit_ab.py``): wait for non-daemon threads, run
+    ``translate``, ``profiles/tools/exit_ab.py``): wait for non-daemon threads, run
     the ``atexit`` handlers (the QA write-cache flush, the trace file,
     multiprocessing's clean-up), flush the standard streams, then ``_exit``.
     Every file the commands write is closed by then (the runs emit no

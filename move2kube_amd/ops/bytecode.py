@@ -5,7 +5,7 @@ interpreter is importing ~80 modules of this package.  The ordinary path does,
 per module, a directory-cache lookup over the candidate suffixes, a ``stat`` of
 the source, an ``open``/``read``/``close`` of its ``__pycache__`` file and the
 header checks; served from the bundle, a cold ``translate`` on the MI355X hosts
-is 1.2-2.5 ms faster (``scripts/cold_ab.py``,
+is 1.2-2.5 ms faster (``profiles/tools/cold_ab.py``,
 ``profiles/r03_cold_bundle/cold_ab.jsonl``).  The bundle
 holds the compiled code of every module in one file that the package reads once
 (``move2kube_amd/__init__.py`` installs the finder); a module is served from it
