@@ -93,11 +93,24 @@ def concurrently(*fns, workers=8):
     return out
 
 
-def get_collectors():
-    from .cf import CfAppsCollector, CFContainerTypesCollector
-    from .cluster import ClusterCollector
-    from .images import ImagesCollector
-    return [ClusterCollector(), ImagesCollector(), CFContainerTypesCollector(), CfAppsCollector()]
+# (module, class, annotations) in the reference's order (collector.go:38-44);
+# a collector's module is only imported when the annotations select it
+# (cluster metadata pulls in the Kubernetes scheme)
+REGISTRY = (("cluster", "ClusterCollector", ("k8s",)),
+            ("images", "ImagesCollector", ("k8s", "dockerswarm", "dockercompose")),
+            ("cf", "CFContainerTypesCollector", ("cloudfoundry", "cf")),
+            ("cf", "CfAppsCollector", ("cf", "cloudfoundry")))
+
+
+def get_collectors(annotations=()):
+    """The collectors, or those whose annotations overlap ``annotations``."""
+    import importlib
+    out = []
+    for mod, cls, ann in REGISTRY:
+        if annotations and not has_overlap(annotations, ann):
+            continue
+        out.append(getattr(importlib.import_module("." + mod, __name__), cls)())
+    return out
 
 
 def has_overlap(a, b):
@@ -113,7 +126,7 @@ def collect(input_path, output_path, annotations=()):
         from ..utils.common import go_path_error
         log.fatal("Unable to create output directory at path %r Error: %r", output_path, go_path_error(e, "mkdir"))
     log.info("Begin collection")
-    selected = [c for c in get_collectors()
+    selected = [c for c in get_collectors(annotations)
                 if not annotations or has_overlap(annotations, c.get_annotations())]
     # The collectors are independent (their own CLIs and output sub-directories)
     # and wait on external tools - cluster discovery, `docker`, `cf curl`, a

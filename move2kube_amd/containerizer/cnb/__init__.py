@@ -1,5 +1,7 @@
 """CNB containerizer (reference ``internal/containerizer/cnbcontainerizer.go``)."""
 
+import os
+import sys
 import threading
 
 from ... import assets
@@ -20,6 +22,34 @@ def reset_cache():
         _cache.clear()
 
 
+# once-per-process warnings of the provider chain (cnb/provider.go)
+_warned = {"not_supported": False, "long_wait": False}
+
+
+def log_not_supported():
+    if not _warned["not_supported"]:
+        from ...utils import log
+        log.warning("No CNB containerizer method accessible")
+        _warned["not_supported"] = True
+
+
+def log_long_wait():
+    # the reference initialises its flag to true so the warning never fires
+    # (SURVEY 2.13 #14); "fixed" compat warns once.
+    from ...utils.constants import settings
+    if settings.fixed and not _warned["long_wait"]:
+        from ...utils import log
+        log.warning("This could take a few minutes to complete.")
+        _warned["long_wait"] = True
+
+
+def _chain_off():
+    """``M2K_DISABLE_CNB`` empties the provider chain: answered here without
+    loading the providers (what they would say: every probe unsupported)."""
+    return (os.environ.get("M2K_DISABLE_CNB", "") not in ("", "0")
+            and __name__ + ".providers" not in sys.modules)
+
+
 class CNBContainerizer(Containerizer):
     build_type = plantypes.CNB
 
@@ -33,8 +63,14 @@ class CNBContainerizer(Containerizer):
         with _cache_lock:
             if path in _cache:
                 return list(_cache[path])
-        from . import providers  # docker API / podman / pack / runc: only when CNB is probed
-        supported = [b for b in self.builders if providers.is_builder_supported(path, b)]
+        if _chain_off():
+            supported = []
+            for _ in self.builders:
+                log_long_wait()
+                log_not_supported()
+        else:
+            from . import providers  # docker API / podman / pack / runc: only when CNB is probed
+            supported = [b for b in self.builders if providers.is_builder_supported(path, b)]
         with _cache_lock:
             _cache[path] = supported
         return list(supported)
@@ -69,9 +105,15 @@ class CNBContainerizer(Containerizer):
                 elif p not in todo:
                     todo.append(p)
         if todo:
-            from . import providers
             pairs = [(p, b) for p in todo for b in self.builders]
-            ok = providers.is_builder_supported_batch(pairs)
+            if _chain_off():
+                log_long_wait()
+                if pairs:
+                    log_not_supported()
+                ok = [False] * len(pairs)
+            else:
+                from . import providers
+                ok = providers.is_builder_supported_batch(pairs)
             nb = len(self.builders)
             with _cache_lock:
                 for j, p in enumerate(todo):
@@ -83,5 +125,8 @@ class CNBContainerizer(Containerizer):
         return out
 
     def get_all_buildpacks(self):
+        if _chain_off():
+            log_not_supported()
+            return {}
         from . import providers
         return providers.get_all_buildpacks(self.builders)

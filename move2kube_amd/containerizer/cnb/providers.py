@@ -13,6 +13,7 @@ per process so that a missing runtime costs one probe, not one per directory.
 import io
 import os
 import shutil
+import sys
 import threading
 
 from ...utils import common, fastjson, log, proc
@@ -31,8 +32,6 @@ DOCKER_SOCK = "/var/run/docker.sock"
 # memory footprint; the reference runs one at a time)
 CONTAINER_PARALLEL = int(os.environ.get("M2K_CNB_PARALLEL", "4") or 4)
 
-_warned_not_supported = False
-_warned_long_wait = False
 _lock = threading.Lock()
 
 
@@ -247,9 +246,23 @@ class DockerAPIProvider:
 # podman CLI
 # ---------------------------------------------------------------------------
 
+def _subprocess_errors(name):
+    """``subprocess.<name>`` once that module is loaded, else nothing: until
+    then no such error can have been raised (the tools run through
+    ``utils.proc``, which loads it only to raise a timeout), and naming it in
+    an ``except`` would import it into a cold CLI process."""
+    sp = sys.modules.get("subprocess")
+    return (getattr(sp, name),) if sp is not None else ()
+
+
 def _chain_errors():
     """Errors that send a probe on to the next provider of the chain."""
-    return (ProviderError, OSError, subprocess.SubprocessError, ValueError, KeyError)
+    return (ProviderError, OSError, ValueError, KeyError) + _subprocess_errors("SubprocessError")
+
+
+def _start_errors():
+    """A tool that could not start or overran its time limit."""
+    return (OSError,) + _subprocess_errors("TimeoutExpired")
 
 
 def parallel_map(fn, items, workers=None):
@@ -381,7 +394,7 @@ class ContainerRuntimeProvider:
                         raise p
                 else:
                     p = _run(self.HELLO)
-            except (OSError, subprocess.TimeoutExpired) as e:
+            except _start_errors() as e:
                 log.debug("Podman not supported : %s : %s", _go_err(e, "podman"), "")
                 self.runtime = "none"
             else:
@@ -405,7 +418,7 @@ class ContainerRuntimeProvider:
                 p = self._images_run(rt, builder)
             elif isinstance(p, BaseException):
                 raise p
-        except (OSError, subprocess.TimeoutExpired) as e:
+        except _start_errors() as e:
             log.warning("Error while checking if the builder %s exists locally. Error: %r Output: %r", builder,
                         _go_err(e, rt), "")
             return False
@@ -419,7 +432,7 @@ class ContainerRuntimeProvider:
         log.debug("Pulling image %s", builder)
         try:
             p = _run([rt, "pull", "--storage-driver=vfs", builder])
-        except (OSError, subprocess.TimeoutExpired) as e:
+        except _start_errors() as e:
             log.warning("Error while pulling builder %s : %s : %s", builder, _go_err(e, rt), "")
             return False
         if p.returncode != 0:
@@ -535,7 +548,7 @@ class PackProvider:
         for b in builders:
             try:
                 p = _run(["pack", "inspect-builder", b])
-            except (OSError, subprocess.TimeoutExpired) as e:
+            except _start_errors() as e:
                 log.warning("Error while getting supported buildpacks for builder %s : %s", b, e)
                 continue
             if p.returncode != 0:  # cmd.Output() returns an *ExitError (packprovider.go:131-136)
@@ -650,19 +663,13 @@ def reset_providers():
 
 
 def _log_not_supported():
-    global _warned_not_supported
-    if not _warned_not_supported:
-        log.warning("No CNB containerizer method accessible")
-        _warned_not_supported = True
+    from . import log_not_supported
+    log_not_supported()
 
 
 def _log_long_wait():
-    # the reference initialises its flag to true so the warning never fires
-    # (SURVEY 2.13 #14); "fixed" compat warns once.
-    global _warned_long_wait
-    if settings.fixed and not _warned_long_wait:
-        log.warning("This could take a few minutes to complete.")
-        _warned_long_wait = True
+    from . import log_long_wait
+    log_long_wait()
 
 
 def is_builder_supported(path, builder):

@@ -65,11 +65,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("config")
     ap.add_argument("--runs", type=int, default=15)
+    ap.add_argument("--command", type=int, default=-1,
+                    help="which of the configuration's CLI commands to time (cf: 0 = collect, 1 = translate)")
     a = ap.parse_args()
     work = tempfile.mkdtemp(prefix="m2k-phases-")
     run = refconfigs.Run(a.config, work).prepare()
     env = run.env()
-    argv = run.cli_commands()[-1]
+    argv = run.cli_commands()[a.command]
     result = os.path.join(work, "phases.jsonl")
     child = os.path.join(work, "child.py")
     import time
@@ -82,7 +84,7 @@ def main():
         subprocess.run([sys.executable, "-S", child, repr(time.perf_counter())], env=env, cwd=work,
                        stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True)
     rows = [json.loads(line) for line in open(result)]
-    out = {"config": a.config, "runs": len(rows)}
+    out = {"config": a.config, "command": argv[0], "runs": len(rows)}
     for k in rows[0]:
         if k == "modules":
             out[k] = rows[0][k]

@@ -256,7 +256,7 @@ def test_collectors_run_concurrently_with_ordered_logs(monkeypatch, tmp_path):
 
     buf = io.StringIO()
     monkeypatch.setattr(log.logger, "stream", buf)
-    monkeypatch.setattr(coll, "get_collectors", lambda: [Slow("a", 0.3), Slow("b", 0.1, "error"), Slow("c", 0.2)])
+    monkeypatch.setattr(coll, "get_collectors", lambda annotations=(): [Slow("a", 0.3), Slow("b", 0.1, "error"), Slow("c", 0.2)])
     t0 = time.perf_counter()
     coll.collect("", str(tmp_path / "out"), ["x"])
     assert time.perf_counter() - t0 < 0.55
@@ -266,7 +266,7 @@ def test_collectors_run_concurrently_with_ordered_logs(monkeypatch, tmp_path):
                     "Collection done"]
     buf.truncate(0)
     buf.seek(0)
-    monkeypatch.setattr(coll, "get_collectors", lambda: [Slow("a", 0.1), Slow("f", 0.0, "fatal"), Slow("c", 0.0)])
+    monkeypatch.setattr(coll, "get_collectors", lambda annotations=(): [Slow("a", 0.1), Slow("f", 0.0, "fatal"), Slow("c", 0.0)])
     with pytest.raises(log.FatalError):
         coll.collect("", str(tmp_path / "out"), ["x"])
     msgs = [m for _lv, m in logparse.messages(buf.getvalue())]
@@ -386,3 +386,13 @@ def test_interpret_error_for_oc():
     assert c.interpret_error("error: Username or password wrong") == \
         "Please login to cluster before running collect. (e.g. oc login <cluster url> --token=<token string>)"
     assert c.interpret_error("no route to host") == ""
+
+
+def test_collector_registry_matches_the_classes():
+    """get_collectors selects by the registry's annotations without importing
+    the other collectors; they must be each class's own."""
+    got = collector.get_collectors()
+    assert [type(c).__name__ for c in got] == [r[1] for r in collector.REGISTRY]
+    for c, (_, _, ann) in zip(got, collector.REGISTRY):
+        assert tuple(c.get_annotations()) == ann
+    assert [type(c).__name__ for c in collector.get_collectors(["cf"])] == ["CFContainerTypesCollector", "CfAppsCollector"]
