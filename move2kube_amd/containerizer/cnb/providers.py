@@ -490,7 +490,25 @@ class ContainerRuntimeProvider:
             out[i] = r
         return out
 
+    @staticmethod
+    def _inspect_cmd(rt, builder):
+        return [rt, "inspect", "--storage-driver=vfs", "--format", '{{ index .Config.Labels "' + ORDER_LABEL + '"}}',
+                builder]
+
     def get_all_buildpacks(self, builders):
+        procs = None
+        if self.runtime is None and self._hello is None and builders:
+            # the runtime probe and the (read-only) inspects start together;
+            # the inspects of a runtime that then fails its probe are discarded
+            children = []
+            for cmd in [self.HELLO] + [self._inspect_cmd("podman", b) for b in builders]:
+                try:
+                    children.append(proc.spawn(cmd, stdout=proc.PIPE, stderr=proc.STDOUT))
+                except OSError as e:
+                    children.append(e)
+            res = _collect(children, RUN_TIMEOUT_S)
+            self._hello = (res[0],)
+            procs = res[1:]
         rt = self.get_runtime()
         if rt is None:
             raise ProviderError("Container runtime not supported in this instance")
@@ -498,9 +516,10 @@ class ContainerRuntimeProvider:
         log.debug("Getting data of all builders %s", "[" + " ".join(builders) + "]")
         for b in builders:
             log.debug("Inspecting image %s", b)
-        # one `inspect` per builder, concurrently
-        procs = _run_many([[rt, "inspect", "--storage-driver=vfs", "--format",
-                            '{{ index .Config.Labels "' + ORDER_LABEL + '"}}', b] for b in builders])
+        if procs is None:  # one `inspect` per builder, concurrently
+            procs = _run_many([self._inspect_cmd(rt, b) for b in builders])
+        else:
+            procs = [common.go_exec_error(p, rt) if isinstance(p, FileNotFoundError) else p for p in procs]
         for b, p in zip(builders, procs):
             if isinstance(p, Exception):
                 raise p
