@@ -109,11 +109,11 @@ def step_spread(step_s):
 
 
 def _cpu_s():
-    """CPU seconds of this process and its reaped children (the operator-sdk
-    stand-in, detector scripts)."""
+    """(user, system) CPU seconds of this process and its reaped children
+    (the operator-sdk stand-in, detector scripts)."""
     import resource
     a, b = resource.getrusage(resource.RUSAGE_SELF), resource.getrusage(resource.RUSAGE_CHILDREN)
-    return a.ru_utime + a.ru_stime + b.ru_utime + b.ru_stime
+    return a.ru_utime + b.ru_utime, a.ru_stime + b.ru_stime
 
 
 def _cgroup_throttled_us():
@@ -207,7 +207,8 @@ def main():
                 step_s.append(time.perf_counter() - ts)
             barrier()
             elapsed = time.perf_counter() - t0
-            cpu_s, thr1 = _cpu_s() - cpu0, _cgroup_throttled_us()
+            cpu1, thr1 = _cpu_s(), _cgroup_throttled_us()
+            cpu_s = (cpu1[0] - cpu0[0], cpu1[1] - cpu0[1])
             if rank == 0:
                 # untimed: one traced step for the per-phase breakdown (utils/trace.py)
                 from move2kube_amd.utils import trace
@@ -236,9 +237,9 @@ def main():
         t = torch.tensor([elapsed, slowest_p50], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, slowest_p50 = float(t[0].item()), float(t[1].item())
-        c = torch.tensor([cpu_s], dtype=torch.float64, device=dev)
+        c = torch.tensor(list(cpu_s), dtype=torch.float64, device=dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        cpu_s = float(c.item())
+        cpu_s = (float(c[0].item()), float(c[1].item()))
     ms = elapsed * 1000.0 / max(1, args.steps)
     value = world * n_services * args.steps / elapsed if elapsed > 0 else 0.0
     if rank == 0:
@@ -258,7 +259,9 @@ def main():
             # limit from a code change when N ranks share one node's CPUs:
             # CPU ms per step summed over ranks (children included), the
             # slowest rank's median step, and the cgroup's quota throttling
-            "host": {"cpus": _host_cpus(), "cpu_ms_per_step_all_ranks": round(cpu_s * 1000.0 / max(1, args.steps), 3),
+            "host": {"cpus": _host_cpus(),
+                     "cpu_ms_per_step_all_ranks": round(sum(cpu_s) * 1000.0 / max(1, args.steps), 3),
+                     "cpu_sys_ms_per_step_all_ranks": round(cpu_s[1] * 1000.0 / max(1, args.steps), 3),
                      "slowest_rank_step_p50_ms": round(slowest_p50, 3),
                      "cgroup_throttled_ms": None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1000.0, 3)},
             "higher_is_better": True,

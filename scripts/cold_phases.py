@@ -41,6 +41,11 @@ def imp(name, *a, **k):
             acc[0] += time.perf_counter() - t
 def run(argv):
     shutil.rmtree(OUT, ignore_errors=True)
+    # a CLI process starts its QA engines once (package globals, as in the
+    # reference); drop the previous run's before the next main()
+    eng = sys.modules.get("move2kube_amd.qaengine.engine")
+    if eng is not None:
+        eng.reset()
     t = time.perf_counter()
     try:
         main(argv)

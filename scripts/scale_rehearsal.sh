@@ -22,6 +22,7 @@ d = json.loads(sys.stdin.read())
 h = d["host"]
 print(json.dumps({"n": d["n_gpus"], "ms_per_step": d["ms_per_step"], "value": d["value"], "step_ms": d["step_ms"],
                   "cpus": h["cpus"], "cpu_ms_per_step_all_ranks": h["cpu_ms_per_step_all_ranks"],
+                  "cpu_sys_ms_per_step_all_ranks": h["cpu_sys_ms_per_step_all_ranks"],
                   "cpu_demand": round(h["cpu_ms_per_step_all_ranks"] / d["ms_per_step"], 2),
                   "slowest_rank_step_p50_ms": h["slowest_rank_step_p50_ms"],
                   "cgroup_throttled_ms": h["cgroup_throttled_ms"]}))' | tee -a "$OUT/scale_summary.jsonl"

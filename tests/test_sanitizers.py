@@ -58,6 +58,31 @@ DRIVER = textwrap.dedent(r'''
     assert err == 0 and not os.path.exists(out), (err, where)
     res = m.run_commands([["/bin/sh", "-c", "echo %d" % i] for i in range(24)], ["/"] * 24, 8, 30.0)
     assert len(res) == 24
+    # proc_spawn / proc_wait (proc_spawn.cpp) from 4 threads: pipes, merged
+    # stderr, a timeout kill, a missing executable
+    failures = []
+    def tools(k):
+      try:
+        for i in range(6):
+            pid, o, e = m.proc_spawn([b"/bin/sh", b"-c", b"echo out%d; echo err >&2" % i], None, -1, -1)
+            rc, out, err, to = m.proc_wait(pid, o, e, 10.0)
+            assert (rc, out, err, to) == (0, b"out%d\n" % i, b"err\n", False)
+            pid, o, e = m.proc_spawn([b"/bin/sh", b"-c", b"echo x >&2; exit 3"], b"/", -1, -4)
+            assert m.proc_wait(pid, o, e, 10.0) == (3, b"x\n", b"", False)
+        pid, o, e = m.proc_spawn([b"/bin/sh", b"-c", b"exec sleep 5"], None, -2, -2)
+        assert m.proc_wait(pid, o, e, 0.05)[3] is True
+        try:
+            m.proc_spawn([b"m2k-no-such-tool"], None, -1, -2)
+        except FileNotFoundError:
+            pass
+        else:
+            raise AssertionError("spawned a missing tool")
+      except BaseException as ex:
+        failures.append(repr(ex))
+    ts = [threading.Thread(target=tools, args=(k,)) for k in range(4)]
+    for t in ts: t.start()
+    for t in ts: t.join()
+    assert not failures, failures
     doc = {"a": [1, {"b": "x: y", "c": "multi\nline\n"}], "n": None, "f": 1.5, "u": "hé",
            "m": yamlio.GoMap({"b10": 1, "b9": 2, "k": "007"})}
     def emit():
