@@ -361,7 +361,8 @@ class K8sTransformer(Transformer):
         child, out, span = started
         try:
             try:
-                r = child.wait(OPERATOR_SDK_TIMEOUT_S)  # killed when it overruns
+                with trace.span("operator-sdk wait", "external"):  # the part no other work hid
+                    r = child.wait(OPERATOR_SDK_TIMEOUT_S)  # killed when it overruns
             finally:
                 span.__exit__(None, None, None)
             if r.timed_out:
