@@ -59,6 +59,12 @@ def test_two_ranks_gloo():
     assert d["n_gpus"] == 2
     assert d["config"]["parallelism"] == "dp2"
     assert d["scaling"] == "weak"
+    # host accounting of the timed region: CPU summed over both ranks, the
+    # slowest rank's median step
+    h = d["host"]
+    assert h["cpus"] >= 1 and h["cpu_ms_per_step_all_ranks"] > 0
+    assert 0 <= h["cpu_sys_ms_per_step_all_ranks"] <= h["cpu_ms_per_step_all_ranks"]
+    assert h["slowest_rank_step_p50_ms"] > 0
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only contract test")
@@ -88,3 +94,18 @@ def test_baseline_configs_bench_golang():
     assert len(cfg) == 1 and cfg[0]["manifest_diff_vs_ref"] == 0
     assert cfg[0]["warm_p50_ms"] > 0 and cfg[0]["cold_p50_ms"] > 0
     assert cfg[0]["python_emulation_of_reference_fork_model_p50_ms"] > 0
+
+
+def test_cold_diagnostics_scripts_run():
+    """scripts/cold_phases.py and benchmarks/cold_trace.py (the cold-start
+    breakdowns kept under profiles/) still run and report their fields."""
+    p = subprocess.run([sys.executable, os.path.join("scripts", "cold_phases.py"), "golang", "--runs", "1"],
+                       cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    d = _last_json(p.stdout.decode())
+    assert d["command"] == "translate" and d["first_main"] > 0 and d["second_main"] > 0
+    p = subprocess.run([sys.executable, os.path.join("benchmarks", "cold_trace.py"), "helm-openshift", "--runs", "1"],
+                       cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    d = _last_json(p.stdout.decode())
+    assert d["wall_p50_ms"] > 0 and "operator-sdk wait" in d["span_p50_ms"] and "plan" in d["span_p50_ms"]
