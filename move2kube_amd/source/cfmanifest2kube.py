@@ -104,13 +104,19 @@ class CfManifestTranslator(Translator):
         if log.debug_enabled():
             log.debug("Cf Instances %s", "map[" + " ".join(
                 "%s:[%s]" % (k, " ".join(a.go_plus_v() for a in instance_apps[k])) for k in sorted(instance_apps)) + "]")
-        covered = []
+        # Every manifest app that is not a docker image has its build directory
+        # probed by the containerizers (detect scripts, CNB builders); those
+        # probes run as one batch, concurrently, instead of one app after
+        # another as in the reference (only debug lines move).
+        manifests = []
+        probe = []
         for f in files:
             try:
                 apps, _ = read_application_manifest(f, "", plantypes.YAMLS)
             except (ManifestError, OSError) as e:
                 log.debug("Failed to parse the manifest file at path %r Error: %r", f, str(e))
                 continue
+            rows = []
             for app in apps:
                 if app.path:
                     base = os.path.dirname(f) if settings.fixed else f
@@ -122,6 +128,14 @@ class CfManifestTranslator(Translator):
                     b = os.path.basename(f)
                     app_name = b[:len(b) - len(common.go_ext(b))]
                 inst_path, inst = _get_cf_instance_app(instance_apps, app_name)
+                rows.append((app, build_dir, app_name, inst_path, inst))
+                if not (app.docker_image or inst.docker_image) and build_dir not in probe:
+                    probe.append(build_dir)
+            manifests.append((f, rows))
+        probed = dict(zip(probe, cz.get_containerization_options_batch(plan, probe))) if probe else {}
+        covered = []
+        for f, rows in manifests:
+            for app, build_dir, app_name, inst_path, inst in rows:
                 if app.docker_image or inst.docker_image:
                     s = self.new_service(app_name)
                     s.container_build_type = plantypes.REUSE
@@ -131,7 +145,7 @@ class CfManifestTranslator(Translator):
                     covered.append(app_name)
                     continue
                 found = False
-                for cop in cz.get_containerization_options(plan, build_dir):
+                for cop in probed[build_dir]:
                     s = self.new_service(app_name)
                     s.container_build_type = cop.containerization_type
                     s.target_options = list(cop.target_options)
