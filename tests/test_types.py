@@ -1,6 +1,8 @@
 """Model-type merge semantics, mirroring the reference's ``types/*_test.go``:
 
 * ``types/collection/cluster_test.go`` - ClusterMetadata.Merge, GetSupportedVersions
+* ``types/collection/{image,cfcontainerizers,cfinstanceapps}_test.go`` - the
+  New* constructors set kind and apiVersion
 * ``types/output/helmvaluesoutput_test.go`` - HelmValues.Merge
 * ``types/info/versioninfo_test.go`` - VersionInfo.IsSameVersion
 * ``types/plan/plan_test.go`` - KubernetesOutput.Merge, Service.Add*,
@@ -13,6 +15,14 @@ from move2kube_amd.models import collection, info, output, plan
 
 
 # -- collection ----------------------------------------------------------------
+
+@pytest.mark.parametrize("cls,kind", [(collection.ImageInfo, "ImageMetadata"),
+                                      (collection.CfContainerizers, "CfContainerizers"),
+                                      (collection.CfInstanceApps, "CfInstanceApps")])
+def test_new_collection_types(cls, kind):
+    o = cls()
+    assert o.kind == kind and o.api_version == "move2kube.konveyor.io/v1alpha1"
+
 
 def _cmeta(name="", kind=None):
     c = collection.new_cluster_metadata(name)
