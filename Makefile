@@ -4,7 +4,8 @@
 #   make test-gpu   GPU tests (needs an MI355X)
 #   make bench      headline benchmark (translate throughput on samples/)
 #   make dist       sdist/wheel-style tarballs + sha256 sums under dist/
-#   make cbuild     container image
+#   make cbuild     container image (cimage-e2e: translate samples/ inside it)
+#   make installdeps  external tools (pack, kubectl, operator-sdk) into ./bin
 
 PYTHON      ?= python3
 IMAGE       ?= quay.io/konveyor/move2kube-amd
@@ -74,3 +75,11 @@ cbuild: ## Build the container image
 .PHONY: cpush
 cpush: ## Push the container image
 	docker push $(IMAGE):$(VERSION)
+
+.PHONY: cimage-e2e
+cimage-e2e: ## Translate samples/ inside the built image and diff against the expected tree
+	bash scripts/image_e2e.sh $(IMAGE):$(VERSION)
+
+.PHONY: installdeps
+installdeps: ## Install pack, kubectl and operator-sdk into ./bin (scripts/installdeps.sh)
+	bash scripts/installdeps.sh

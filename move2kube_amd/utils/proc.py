@@ -64,8 +64,10 @@ class Child:
         if self._done is not None:
             return self._done
         if self._popen is None:
-            rc, out, err, timed_out = native.module().proc_wait(self.pid, self._out_fd, self._err_fd,
-                                                                float(timeout or 0))
+            # proc_wait closes the descriptors whatever happens (an interrupt
+            # included): hand them over once, never twice
+            ofd, efd, self._out_fd, self._err_fd = self._out_fd, self._err_fd, -1, -1
+            rc, out, err, timed_out = native.module().proc_wait(self.pid, ofd, efd, float(timeout or 0))
             self._done = Completed(self.args, rc, out if self._pipes[0] else None,
                                    err if self._pipes[1] else None, timed_out)
             return self._done
