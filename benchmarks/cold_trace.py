@@ -58,7 +58,7 @@ def main():
             for k, v in per.items():
                 spans.setdefault(k, []).append(v)
         med = {k: round(statistics.median(v + [0.0] * (len(walls) - len(v))), 3) for k, v in spans.items()}
-        top = dict(sorted(med.items(), key=lambda kv: -kv[1])[:20])
+        top = dict(sorted(med.items(), key=lambda kv: -kv[1]))
         print(json.dumps({"config": a.config, "command": cmds[-1][0], "runs": len(walls),
                           "wall_p50_ms": round(statistics.median(walls), 3), "span_p50_ms": top}), flush=True)
     finally:

@@ -11,7 +11,8 @@
 //   proc_spawn(argv, cwd, stdout, stderr) -> (pid, out_rfd, err_rfd)
 //       posix_spawnp (glibc: clone(CLONE_VM|CLONE_VFORK), so the parent's
 //       address-space size does not matter) with stdin on /dev/null and
-//       SIGPIPE/SIGXFSZ reset to default in the child, as subprocess does.
+//       SIGPIPE/SIGXFSZ reset to default and descriptors above 2 closed in
+//       the child, as subprocess does.
 //       stdout: -1 pipe, -2 /dev/null, -3 inherit, >= 0 that descriptor.
 //       stderr: the same codes, plus -4 = into stdout.
 //       Failure raises OSError(errno, strerror, argv[0]) like subprocess.
@@ -139,6 +140,11 @@ extern "C" PyObject *m2k_proc_spawn(PyObject *argv_obj, PyObject *cwd_obj, long 
   else if (err_mode >= 0)
     posix_spawn_file_actions_adddup2(&fa, (int)err_mode, 2);
   if (!cwd.empty()) posix_spawn_file_actions_addchdir_np(&fa, cwd.c_str());
+#if defined(__GLIBC__) && (__GLIBC__ > 2 || (__GLIBC__ == 2 && __GLIBC_MINOR__ >= 34))
+  // like subprocess's close_fds=True: the child keeps only 0, 1 and 2, even of
+  // descriptors someone opened without O_CLOEXEC
+  posix_spawn_file_actions_addclosefrom_np(&fa, 3);
+#endif
 
   posix_spawnattr_t attr;
   posix_spawnattr_init(&attr);

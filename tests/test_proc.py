@@ -116,3 +116,17 @@ def test_cold_tool_paths_do_not_import_subprocess(tmp_path):
             "print('subprocess' in sys.modules)\n" % root)
     p = subprocess.run([sys.executable, "-S", "-c", code], stdout=subprocess.PIPE, check=True)
     assert p.stdout.strip() == b"False"
+
+
+def test_child_gets_only_the_standard_descriptors(mode):
+    """As subprocess's close_fds: an inheritable descriptor of ours does not
+    reach the tool."""
+    r, w = os.pipe()
+    high = os.dup2(w, 77)  # dup2 makes an inheritable copy
+    try:
+        res = proc.run(["/bin/sh", "-c", "ls /proc/$$/fd"], stdout=proc.PIPE)
+        fds = {int(x) for x in res.stdout.split()}
+        assert {0, 1, 2} <= fds and high not in fds
+    finally:
+        for fd in (r, w, high):
+            os.close(fd)
