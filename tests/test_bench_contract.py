@@ -10,6 +10,13 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
+try:  # bench.py joins torch.distributed; the image's builder stage has no torch
+    import torch  # noqa: F401
+    _HAVE_TORCH = True
+except ImportError:
+    _HAVE_TORCH = False
+needs_torch = pytest.mark.skipif(not _HAVE_TORCH, reason="bench.py needs torch")
+
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
 
@@ -28,6 +35,7 @@ def _last_json(stdout):
     return json.loads(lines[0])
 
 
+@needs_torch
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only contract test")
 def test_single_rank():
     p = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--check-runs", "1",
@@ -48,6 +56,7 @@ def test_single_rank():
         assert d["config"]["model"] in json.load(f)["configs"]
 
 
+@needs_torch
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only contract test")
 def test_two_ranks_gloo():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
@@ -67,6 +76,7 @@ def test_two_ranks_gloo():
     assert h["slowest_rank_step_p50_ms"] > 0
 
 
+@needs_torch
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="CPU-only contract test")
 def test_one_rank_under_torchrun_joins_the_group():
     """Launched by torchrun with one rank, bench.py still initialises the

@@ -300,3 +300,53 @@ def test_primitives_match_published_vectors():
         assert c.on_curve(c.g) and c.mul_add(c.n, c.g, 0, c.g) is None
     assert ssh_mpint(0) == b"\x00\x00\x00\x00" and ssh_mpint(0x80) == b"\x00\x00\x00\x02\x00\x80"
     assert struct.unpack(">I", ssh_mpint(0x7f)[:4])[0] == 1
+
+
+def _serve_bytes(chunks):
+    """A one-shot server that sends ``chunks`` (after reading the client's
+    version line) and closes."""
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+
+    def serve():
+        try:
+            c, _ = srv.accept()
+        except OSError:
+            return
+        try:
+            c.settimeout(5)
+            c.recv(256)
+            for ch in chunks:
+                c.sendall(ch)
+        except OSError:
+            pass
+        finally:
+            c.close()
+    threading.Thread(target=serve, daemon=True).start()
+    return srv
+
+
+def _pkt(payload, pad=4):
+    return struct.pack(">IB", 1 + len(payload) + pad, pad) + payload + b"\x00" * pad
+
+
+@pytest.mark.parametrize("chunks", [
+    [b"SSH-2.0-x\r\n", struct.pack(">IB", 1 << 30, 4)],                      # absurd packet length
+    [b"SSH-2.0-x\r\n", struct.pack(">IB", 3, 10)],                           # padding longer than the packet
+    [b"SSH-2.0-x\r\n", _pkt(b"\x14" + b"\x00" * 16)],                        # KEXINIT cut short
+    [b"SSH-2.0-x\r\n", _pkt(bytes([20]) + bytes(16) + ssh_string(b"\xff\xfe") * 10 + b"\x00" + bytes(4))],
+    [b"SSH-1.5-old\r\n"],                                                    # SSH 1 only
+    [b"SSH-2.0-x\r\n", _pkt(sshwire._kexinit(("curve25519-sha256",), ("ssh-ed25519",))),
+     _pkt(bytes([31]) + ssh_string(b"\x00\x00\x00\x0bssh-ed25519" + ssh_string(b"k" * 32)) + ssh_string(b"short"))],
+    [b"SSH-2.0-x\r\n", _pkt(sshwire._kexinit(("curve25519-sha256",), ("ssh-ed25519",))),
+     _pkt(bytes([1]) + struct.pack(">I", 2) + ssh_string(b"go away") + ssh_string(b""))],
+    [b"x" * 9000],                                                           # no version line at all
+])
+def test_hostile_servers_fail_cleanly(chunks):
+    srv = _serve_bytes(chunks)
+    try:
+        with pytest.raises((sshwire.SSHError, OSError)):
+            sshwire.fetch_host_key("127.0.0.1", port=srv.getsockname()[1], timeout=5)
+    finally:
+        srv.close()
