@@ -443,10 +443,18 @@ class _DescIndex:
         out = set(self.fold.get(common.go_fold(desc), ()))
         out |= self.always
         grams, q = self.grams, self.Q
-        for i in range(len(desc) - q + 1):
-            b = grams.get(desc[i:i + q])
-            if b:
-                out |= b
+        windows = len(desc) - q + 1
+        if len(grams) < windows:
+            # fewer filed pieces than windows of the description (a small
+            # cache): the same set, found by substring tests of the pieces
+            for g, b in grams.items():
+                if b and g in desc:
+                    out |= b
+        else:
+            for i in range(windows):
+                b = grams.get(desc[i:i + q])
+                if b:
+                    out |= b
         return sorted(out)
 
     def first_match(self, p, pred=None):

@@ -87,3 +87,27 @@ def test_cached_descriptions_of_the_fixtures_match_as_before():
     for a in descs:
         for b in descs:
             assert _fresh(a, b) == _reference(a, b), (a, b)
+
+
+_DESCS = st.lists(st.sampled_from(["Select ", "service ", "api", "web", "[a-z]+", ".*", "port", " for ",
+                                   "Choose", "the ", "(x|y)", "registry", ":", "?"]), max_size=9).map("".join)
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(_DESCS, max_size=40), _DESCS)
+def test_desc_index_lookup_strategies_agree(listed, desc):
+    """_DescIndex.candidates finds the filed pieces of a description either
+    by probing every window of it or, for a small index, by substring tests of
+    the pieces; both give the windows' set, and the first match equals a linear
+    scan of the list (the reference's loop)."""
+    problems = [qa.Problem(0, d, [], qa.INPUT, [], [], None, True) for d in listed]
+    idx = qa._DescIndex(problems)
+    windows = set(idx.fold.get(qa.common.go_fold(desc), ())) | idx.always
+    for i in range(len(desc) - idx.Q + 1):
+        windows |= idx.grams.get(desc[i:i + idx.Q], set())
+    assert idx.candidates(desc) == sorted(windows)
+    p = qa.Problem(0, desc, [], qa.INPUT, [], [], None, False)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        linear = next((i for i, cp in enumerate(problems) if cp.matches(p)), -1)
+        assert idx.first_match(p) == linear
