@@ -775,6 +775,8 @@ static int write_one(const std::string &path, const std::string &data, int mode)
   return 0;
 }
 
+static constexpr size_t kParallelWriteMin = 512;
+
 std::vector<int> write_files(const std::vector<std::string> &paths, const std::vector<py::bytes> &datas,
                              const std::vector<int> &modes, int nthreads) {
   const size_t n = paths.size();
@@ -797,6 +799,10 @@ std::vector<int> write_files(const std::vector<std::string> &paths, const std::v
     if (!skip[i]) by_dir[paths[i].substr(0, paths[i].rfind('/') + 1)].push_back(i);
   std::vector<const std::vector<size_t> *> groups;
   for (auto &kv : by_dir) groups.push_back(&kv.second);
+  // A command's output (a hundred-odd small files) is written faster by this
+  // thread alone than by starting workers, whose first start in a process
+  // also pays for fresh thread stacks; threads only pay off on big batches.
+  if (n < kParallelWriteMin) nthreads = 1;
   {
     py::gil_scoped_release nogil;
     parallel_for(groups.size(), std::min<int>(nthreads, static_cast<int>(groups.size())), 2, [&](size_t lo, size_t hi) {
