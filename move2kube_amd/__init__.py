@@ -13,13 +13,16 @@ import sys as _sys
 
 class _BytecodeBundle:
     """Meta-path finder/loader serving this package's modules from
-    ``_bytecode.bin`` (written by ``ops/bytecode.py``): one read per process
-    instead of a lookup, stat and pyc read per module.  A module whose source
+    ``_bytecode.bin`` (written by ``ops/bytecode.py``): the index is read once
+    per process and each module's code with one ``pread``, instead of a
+    lookup, stat and pyc read per module.  A module whose source
     no longer has the recorded mtime and size is left to the normal finders."""
 
-    def __init__(self, root, mods):
+    def __init__(self, root, mods, fd, base):
         self._root = root
         self._mods = mods
+        self._fd = fd      # the bundle file, kept open: code is read per module
+        self._base = base  # where the code section starts
 
     def find_spec(self, name, path=None, target=None):
         rec = self._mods.get(name)
@@ -49,7 +52,7 @@ class _BytecodeBundle:
         import _imp
         import marshal
         rec = self._mods[name]
-        code = marshal.loads(rec[4])
+        code = marshal.loads(_os.pread(self._fd, rec[5], self._base + rec[4]))
         _imp._fix_co_filename(code, _os.path.join(self._root, rec[1]))
         return code
 
@@ -71,15 +74,23 @@ def _install_bytecode_bundle():
     from _frozen_importlib_external import MAGIC_NUMBER
     root = _os.path.dirname(_os.path.abspath(__file__))
     try:
-        with open(_os.path.join(root, "_bytecode.bin"), "rb") as f:
-            tag, optimize, mods = marshal.loads(f.read())
-    except (OSError, ValueError, EOFError, TypeError):
+        fd = _os.open(_os.path.join(root, "_bytecode.bin"), _os.O_RDONLY | _os.O_CLOEXEC)
+    except OSError:
         return
-    if tag != MAGIC_NUMBER + b"m2k1" or optimize != _sys.flags.optimize:
+    try:  # header: b"M2KB", its length, marshalled index (ops/bytecode.py)
+        head = _os.pread(fd, 8, 0)
+        if head[:4] != b"M2KB" or len(head) != 8:
+            raise ValueError
+        n = int.from_bytes(head[4:], "big")
+        tag, optimize, mods = marshal.loads(_os.pread(fd, n, 8))
+        if tag != MAGIC_NUMBER + b"m2k2" or optimize != _sys.flags.optimize:
+            raise ValueError
+    except (OSError, ValueError, EOFError, TypeError):
+        _os.close(fd)
         return
     # a re-import of the package (tests drop it from sys.modules) replaces its finder
     _sys.meta_path[:] = [f for f in _sys.meta_path if type(f).__name__ != "_BytecodeBundle"]
-    _sys.meta_path.insert(0, _BytecodeBundle(root, mods))
+    _sys.meta_path.insert(0, _BytecodeBundle(root, mods, fd, 8 + n))
 
 
 _install_bytecode_bundle()

@@ -13,10 +13,13 @@ only while its source still has the size and mtime (whole seconds, the
 ``.pyc`` rule) it was compiled from, so an edited or added file falls back to
 the normal import path by itself, exactly as a stale ``.pyc`` is recompiled.
 
-Format: ``marshal.dumps((tag, optimize, {name: (is_pkg, relpath, mtime_s,
-size, marshalled_code)}))`` with ``tag`` = the interpreter's pyc magic number
-+ ``b"m2k1"``; an interpreter with another magic number, or another ``-O``
-level, ignores the file.
+Format: ``b"M2KB"``, the header's length (4 bytes, big-endian), the header
+``marshal.dumps((tag, optimize, {name: (is_pkg, relpath, mtime_s, size,
+offset, length)}))``, then every module's marshalled code at ``offset``
+(from the end of the header).  A process reads the small header once and each
+module's code when that module is imported (``os.pread``), not the whole file.
+``tag`` = the interpreter's pyc magic number + ``b"m2k2"``; an interpreter
+with another magic number, or another ``-O`` level, ignores the file.
 
 Built with the native targets (``ops/build.py``, ``__graft_entry__.build``);
 ``M2K_BYTECODE_BUNDLE=0`` turns the finder off.
@@ -24,10 +27,12 @@ Built with the native targets (``ops/build.py``, ``__graft_entry__.build``);
 
 import marshal
 import os
+import struct
 import sys
 from importlib.util import MAGIC_NUMBER
 
-TAG = MAGIC_NUMBER + b"m2k1"
+TAG = MAGIC_NUMBER + b"m2k2"
+MAGIC = b"M2KB"
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FILENAME = "_bytecode.bin"
 
@@ -59,6 +64,8 @@ def write(pkg_dir=PKG, out=None):
     The package's own ``__init__`` is left out (it is what reads the bundle)."""
     out = out or os.path.join(pkg_dir, FILENAME)
     mods = {}
+    blobs = []
+    offset = 0
     base = os.path.basename(pkg_dir)
     for name, path, is_pkg in _modules(pkg_dir):
         if name == base:
@@ -66,20 +73,35 @@ def write(pkg_dir=PKG, out=None):
         st = os.stat(path)
         with open(path, "rb") as f:
             src = f.read()
-        code = compile(src, path, "exec", dont_inherit=True)
-        mods[name] = (is_pkg, os.path.relpath(path, pkg_dir), int(st.st_mtime), st.st_size, marshal.dumps(code))
+        blob = marshal.dumps(compile(src, path, "exec", dont_inherit=True))
+        mods[name] = (is_pkg, os.path.relpath(path, pkg_dir), int(st.st_mtime), st.st_size, offset, len(blob))
+        blobs.append(blob)
+        offset += len(blob)
+    header = marshal.dumps((TAG, sys.flags.optimize, mods))
     with open(out + ".tmp", "wb") as f:
-        f.write(marshal.dumps((TAG, sys.flags.optimize, mods)))
+        f.write(MAGIC + struct.pack(">I", len(header)) + header)
+        for blob in blobs:
+            f.write(blob)
     os.replace(out + ".tmp", out)
     return out
+
+
+def read_header(path):
+    """(tag, optimize, {name: record}) of a bundle file, and the offset its
+    code section starts at."""
+    with open(path, "rb") as f:
+        head = f.read(8)
+        if len(head) != 8 or head[:4] != MAGIC:
+            raise ValueError("not a bytecode bundle")
+        n = struct.unpack(">I", head[4:])[0]
+        return marshal.loads(f.read(n)), 8 + n
 
 
 def stale(pkg_dir=PKG, out=None):
     """True when a module is missing from the bundle or its source changed."""
     out = out or os.path.join(pkg_dir, FILENAME)
     try:
-        with open(out, "rb") as f:
-            tag, optimize, mods = marshal.loads(f.read())
+        (tag, optimize, mods), _ = read_header(out)
     except (OSError, ValueError, EOFError, TypeError):
         return True
     if tag != TAG or optimize != sys.flags.optimize:
