@@ -43,6 +43,16 @@ def log_long_wait():
         _warned["long_wait"] = True
 
 
+def prefetch_builder_probes(builders=None):
+    """Start the container runtime's read-only probes of the default builders
+    (runtime check, local images) now, so that they have run by the time the
+    planner reaches CNB containerization."""
+    if _chain_off():
+        return
+    from . import providers
+    providers.start_runtime_prefetch(list(builders or DEFAULT_BUILDERS))
+
+
 def _chain_off():
     """``M2K_DISABLE_CNB`` empties the provider chain: answered here without
     loading the providers (what they would say: every probe unsupported)."""

@@ -347,6 +347,7 @@ class ContainerRuntimeProvider:
         self.available = set()
         self._hello = None   # prefetched runtime probe (a result or its exception)
         self._images = {}    # builder -> prefetched `images -q` (a result or its exception)
+        self._pending = None  # probes started by start_prefetch, not collected yet
 
     @staticmethod
     def _images_cmd(rt, builder):
@@ -364,6 +365,13 @@ class ContainerRuntimeProvider:
         results are taken in that order later by :meth:`get_runtime` and
         :meth:`is_builder_available`, with the same logs and decisions.  The
         image checks of a runtime that then fails its probe are discarded."""
+        self.start_prefetch(builders)
+        self._finish_prefetch()
+
+    def start_prefetch(self, builders):
+        """:meth:`prefetch` without waiting: the probes run while the caller
+        goes on (the planner starts them before it walks the tree)."""
+        self._finish_prefetch()
         if self.runtime == "none":
             return
         todo = [b for b in dict.fromkeys(builders) if b not in self.available and b not in self._images]
@@ -379,6 +387,13 @@ class ContainerRuntimeProvider:
                     children.append(proc.spawn(self._images_cmd("podman", b), stdout=proc.PIPE, stderr=proc.DEVNULL))
             except OSError as e:
                 children.append(e)
+        self._pending = (hello, todo, children)
+
+    def _finish_prefetch(self):
+        pending, self._pending = self._pending, None
+        if pending is None:
+            return
+        hello, todo, children = pending
         res = _collect(children, 600)
         if hello:
             self._hello = (res.pop(0),)
@@ -386,6 +401,7 @@ class ContainerRuntimeProvider:
             self._images[b] = r
 
     def get_runtime(self):
+        self._finish_prefetch()
         if self.runtime is None:
             try:
                 if self._hello is not None:
@@ -411,6 +427,7 @@ class ContainerRuntimeProvider:
             return False
         if builder in self.available:
             return True
+        self._finish_prefetch()
         log.debug("Checking if the image %s exists locally", builder)
         try:
             p = self._images.pop(builder, None)
@@ -497,6 +514,7 @@ class ContainerRuntimeProvider:
 
     def get_all_buildpacks(self, builders):
         procs = None
+        self._finish_prefetch()
         if self.runtime is None and self._hello is None and builders:
             # the runtime probe and the (read-only) inspects start together;
             # the inspects of a runtime that then fails its probe are discarded
@@ -678,7 +696,22 @@ def providers():
 def reset_providers():
     global _providers
     with _lock:
-        _providers = None
+        old, _providers = _providers, None
+    for p in old or ():
+        if isinstance(p, ContainerRuntimeProvider):
+            p._finish_prefetch()  # reap probes nobody asked for
+
+
+def start_runtime_prefetch(builders):
+    """Start the container runtime's probes for ``builders`` in the
+    background, when that provider is the one the chain will reach (no Docker
+    socket: the Docker Engine API provider comes first)."""
+    if os.path.exists(DOCKER_SOCK):
+        return
+    for p in providers():
+        if isinstance(p, ContainerRuntimeProvider):
+            p.start_prefetch(builders)
+            return
 
 
 def _log_not_supported():

@@ -28,6 +28,9 @@ def create_plan(input_path, project_name, keep_index=False):
     p.root_dir = input_path
     with fsindex.scope(keep_for=input_path if keep_index else None), trace.span("plan", "command"):
         log.info("Planning Translation")
+        # the CNB builders' runtime probes run while the translators walk the tree
+        from .containerizer.cnb import prefetch_builder_probes
+        prefetch_builder_probes()
         for t in source_translator.get_source_loaders():
             log.info("[%r] Planning translation", t)
             try:

@@ -376,3 +376,48 @@ def test_docker_api_copies_source_as_tar_when_bind_mount_fails(nobind_dockerd, t
     copied = [names for names in nobind_dockerd.values() if "workspace/package.json" in names]
     assert copied and set(copied[0]) == {"workspace/package.json", "workspace/src", "workspace/src/lib",
                                          "workspace/src/lib/index.js", "workspace/main.js"}
+
+
+def test_runtime_probes_start_in_the_background(monkeypatch, tmp_path):
+    """start_runtime_prefetch starts `podman run hello-world` and the image
+    checks without waiting; the chain later takes their results (same answers
+    as probing on demand), and reset_providers reaps probes nobody used."""
+    log = tmp_path / "calls"
+    wrapper = tmp_path / "bin" / "podman"
+    wrapper.parent.mkdir()
+    wrapper.write_text('#!/bin/sh\necho "$*" >> %s\nexec %s "$@"\n' % (log, os.path.join(STUBS, "podman")))
+    wrapper.chmod(0o755)
+    monkeypatch.setenv("PATH", str(wrapper.parent) + os.pathsep + "/usr/bin:/bin")
+    monkeypatch.setenv("M2K_DISABLE_CNB", "0")
+    monkeypatch.setattr(providers, "DOCKER_SOCK", str(tmp_path / "no-docker.sock"))
+    providers.reset_providers()
+    providers.start_runtime_prefetch(["b"])
+    rt = [p for p in providers.providers() if isinstance(p, providers.ContainerRuntimeProvider)][0]
+    assert rt._pending is not None          # started, not collected
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "package.json").write_text("{}")
+    assert providers.is_builder_supported_batch([(str(app), "b"), (str(tmp_path), "b")]) == [True, False]
+    assert rt._pending is None and rt.runtime == "podman"
+    calls = log.read_text().splitlines()
+    assert calls[0].startswith("run --storage-driver=vfs --rm hello-world") or calls[1].startswith("run ")
+    assert sum(c.startswith("--storage-driver=vfs images -q b") for c in calls) == 1   # not probed twice
+    # started and never used: reaped by the reset
+    providers.start_runtime_prefetch(["c"])
+    pids = [c.pid for c in providers.providers()[1]._pending[2] if not isinstance(c, Exception)]
+    providers.reset_providers()
+    for pid in pids:
+        with pytest.raises(ChildProcessError):
+            os.waitpid(pid, os.WNOHANG)
+    providers.reset_providers()
+
+
+def test_no_background_probes_when_the_docker_socket_exists(monkeypatch, tmp_path):
+    sock = tmp_path / "docker.sock"
+    sock.write_text("")
+    monkeypatch.setattr(providers, "DOCKER_SOCK", str(sock))
+    monkeypatch.setenv("M2K_DISABLE_CNB", "0")
+    providers.reset_providers()
+    providers.start_runtime_prefetch(["b"])
+    assert all(getattr(p, "_pending", None) is None for p in providers.providers())
+    providers.reset_providers()
