@@ -5,7 +5,6 @@ import sys
 import threading
 
 from ... import assets
-from ...models import ir as irtypes
 from ...models import plan as plantypes
 from ...utils import common
 from ...utils.constants import DEFAULT_SERVICE_PORT
@@ -86,6 +85,7 @@ class CNBContainerizer(Containerizer):
         return list(supported)
 
     def get_container(self, plan, service):
+        from ...models import ir as irtypes
         container = irtypes.new_container(self.build_type, service.image, True)
         if service.container_build_type != self.build_type:
             raise ContainerizerError("Service %s has container build type %s . Expected %s"

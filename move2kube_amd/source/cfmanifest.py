@@ -18,7 +18,6 @@ import re
 
 from ..models import plan as plantypes
 from ..utils import common, log, yamlio
-from ..utils.gotemplate import go_sprint
 from ..utils.lazyre import lazy as _lazy_re
 
 _VAR_RE = _lazy_re(r"\(\((!?[-/\.\w]+)\)\)", re.UNICODE)
@@ -130,6 +129,13 @@ def get_missing_variables(path):
         log.debug("Error %s", e)
         raise
     return sorted(names)
+
+
+def go_sprint(v):
+    """``fmt.Sprint`` (``utils/gotemplate.py``, loaded on first use: ``collect``
+    reads manifests without the template engine)."""
+    from ..utils.gotemplate import go_sprint as sprint
+    return sprint(v)
 
 
 def _str(v):
