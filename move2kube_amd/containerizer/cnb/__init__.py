@@ -107,13 +107,14 @@ class CNBContainerizer(Containerizer):
         """Builders whose detector accepts each path; the uncached (path,
         builder) probes of the whole batch go to the providers at once."""
         out = [None] * len(paths)
-        todo = []
+        todo = {}  # insertion-ordered set: a level of a large tree has thousands of paths
         with _cache_lock:
             for k, p in enumerate(paths):
                 if p in _cache:
                     out[k] = list(_cache[p])
-                elif p not in todo:
-                    todo.append(p)
+                else:
+                    todo[p] = None
+        todo = list(todo)
         if todo:
             pairs = [(p, b) for p in todo for b in self.builders]
             if _chain_off():

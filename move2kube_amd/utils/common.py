@@ -343,9 +343,16 @@ def is_int_present(lst, value):
 
 
 def merge_string_slices(a, b):
+    """``a`` plus the items of ``b`` not already in it (``strings.EqualFold``),
+    in order; linear, where ``IsStringPresent`` per item is quadratic."""
     a = list(a or [])
-    for item in b or []:
-        if not is_string_present(a, item):
+    if not b:
+        return a
+    seen = {go_fold(x) for x in a}
+    for item in b:
+        f = go_fold(item)
+        if f not in seen:
+            seen.add(f)
             a.append(item)
     return a
 
