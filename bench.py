@@ -131,13 +131,8 @@ def _cgroup_throttled_us():
 
 def _host_cpus():
     """CPUs this job may use: the affinity mask within the cgroup quota."""
-    saved = os.environ.pop("LOCAL_WORLD_SIZE", None)
-    try:
-        from move2kube_amd.utils.constants import host_threads
-        return host_threads(1 << 20)
-    finally:
-        if saved is not None:
-            os.environ["LOCAL_WORLD_SIZE"] = saved
+    from move2kube_amd.utils.constants import host_threads
+    return host_threads(1 << 20, local=1)
 
 
 def main():

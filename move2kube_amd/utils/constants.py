@@ -60,10 +60,11 @@ def _cgroup_cpu_limit(root="/sys/fs/cgroup"):
     return None
 
 
-def host_threads(cap):
+def host_threads(cap, local=None):
     """Threads this process should use: the CPUs it may run on (affinity, not
     the whole machine, and no more than the cgroup CPU quota), shared among
-    the ranks torchrun placed on this node (LOCAL_WORLD_SIZE), capped."""
+    the ``local`` processes of this node (default: the ranks torchrun placed
+    here, LOCAL_WORLD_SIZE), capped."""
     try:
         n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -71,10 +72,11 @@ def host_threads(cap):
     limit = _cgroup_cpu_limit()
     if limit is not None:
         n = min(n, limit)
-    try:
-        local = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
-    except ValueError:
-        local = 1
+    if local is None:
+        try:
+            local = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
+        except ValueError:
+            local = 1
     return max(1, min(cap, n // max(1, local)))
 
 
