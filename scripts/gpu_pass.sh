@@ -49,6 +49,7 @@ if [ -n "$TRACE" ]; then
   echo "cold traces"
   for c in golang java-cnb cf helm-openshift; do
     timeout -k 10 180 python -u benchmarks/cold_trace.py "$c" --runs 15 | tee -a "$OUT/cold_trace.jsonl"
+    timeout -k 10 180 python -u benchmarks/cold_importtime.py "$c" --runs 9 >> "$OUT/cold_importtime.jsonl"
   done
 fi
 echo done
