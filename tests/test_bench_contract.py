@@ -119,3 +119,8 @@ def test_cold_diagnostics_scripts_run():
     assert p.returncode == 0, p.stderr.decode()[-3000:]
     d = _last_json(p.stdout.decode())
     assert d["wall_p50_ms"] > 0 and "operator-sdk wait" in d["span_p50_ms"] and "plan" in d["span_p50_ms"]
+    p = subprocess.run([sys.executable, os.path.join("benchmarks", "cold_importtime.py"), "golang", "--runs", "1"],
+                       cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    d = _last_json(p.stdout.decode())
+    assert d["self_us_ours"] > 0 and "move2kube_amd.cli.main" in d["self_cum_us"]
