@@ -22,6 +22,7 @@ import hashlib
 import os
 import socket
 import struct
+import time
 
 CLIENT_VERSION = b"SSH-2.0-Go"  # what x/crypto/ssh sends
 KEX_ALGOS = ("curve25519-sha256", "curve25519-sha256@libssh.org", "diffie-hellman-group14-sha256",
@@ -34,6 +35,8 @@ MACS = ("hmac-sha2-256-etm@openssh.com", "hmac-sha2-256", "hmac-sha1")
 MSG_DISCONNECT, MSG_IGNORE, MSG_DEBUG = 1, 2, 4
 MSG_KEXINIT, MSG_KEXDH_INIT, MSG_KEXDH_REPLY = 20, 30, 31
 MAX_PACKET = 256 * 1024
+MAX_BANNER_LINES = 1024  # lines before the version line
+MAX_SKIPPED = 1024  # IGNORE/DEBUG messages in a row
 
 # RFC 3526 group 14 (2048-bit MODP), generator 2
 GROUP14_P = int(
@@ -404,27 +407,45 @@ def verify_signature(key_blob, sig_blob, data, sig_algo_expected):
 # ---------------------------------------------------------------------------
 
 class _Conn:
-    def __init__(self, sock):
+    """Reads bounded by one deadline for the whole exchange, so a server that
+    drips bytes or chatters (banner lines, IGNORE packets) cannot hold the
+    caller longer than its timeout."""
+
+    def __init__(self, sock, deadline=None):
         self.sock = sock
         self.buf = b""
+        self.deadline = deadline  # None: only the socket's own timeout
+
+    def _recv(self, n):
+        if self.deadline is not None:
+            left = self.deadline - time.monotonic()
+            if left <= 0:
+                raise socket.timeout("timed out")
+            self.sock.settimeout(left)
+        chunk = self.sock.recv(n)
+        if not chunk:
+            raise SSHError("connection closed by the server")
+        return chunk
 
     def _fill(self, n):
         while len(self.buf) < n:
-            chunk = self.sock.recv(65536)
-            if not chunk:
-                raise SSHError("connection closed by the server")
-            self.buf += chunk
+            self.buf += self._recv(65536)
 
     def read_line(self):
         while b"\n" not in self.buf:
             if len(self.buf) > 8192:
                 raise SSHError("no SSH version line")
-            chunk = self.sock.recv(4096)
-            if not chunk:
-                raise SSHError("connection closed by the server")
-            self.buf += chunk
+            self.buf += self._recv(4096)
         line, self.buf = self.buf.split(b"\n", 1)
         return line.rstrip(b"\r")
+
+    def read_message(self):
+        """The next packet that is not IGNORE or DEBUG."""
+        for _ in range(MAX_SKIPPED):
+            payload = self.read_packet()
+            if not payload or payload[0] not in (MSG_IGNORE, MSG_DEBUG):
+                return payload
+        raise SSHError("too many IGNORE/DEBUG messages")
 
     def read_packet(self):
         self._fill(5)
@@ -460,24 +481,23 @@ def fetch_host_key(host, port=22, timeout=5.0, kex_algos=KEX_ALGOS, host_key_alg
     """(key type, key blob) of the host key that ``host`` proves it holds in a
     key exchange, negotiated from ``host_key_algos`` in order.  Raises
     :class:`SSHError` or ``OSError``."""
+    deadline = time.monotonic() + timeout
     sock = socket.create_connection((host, port), timeout=timeout)
     try:
         sock.settimeout(timeout)
-        conn = _Conn(sock)
+        conn = _Conn(sock, deadline)
         sock.sendall(CLIENT_VERSION + b"\r\n")
-        while True:  # RFC 4253 §4.2: the server may send other lines first
+        for _ in range(MAX_BANNER_LINES):  # RFC 4253 §4.2: the server may send other lines first
             v_s = conn.read_line()
             if v_s.startswith(b"SSH-"):
                 break
+        else:
+            raise SSHError("no SSH version line in the first %d lines" % MAX_BANNER_LINES)
         if not (v_s.startswith(b"SSH-2.0-") or v_s.startswith(b"SSH-1.99-")):
             raise SSHError("unsupported server version %r" % v_s)
         i_c = _kexinit(kex_algos, host_key_algos)
         conn.send_packet(i_c)
-        while True:
-            i_s = conn.read_packet()
-            if i_s and i_s[0] in (MSG_IGNORE, MSG_DEBUG):
-                continue
-            break
+        i_s = conn.read_message()
         if not i_s or i_s[0] != MSG_KEXINIT:
             raise SSHError("expected KEXINIT, got message %d" % (i_s[0] if i_s else -1))
         r = Reader(i_s)
@@ -492,11 +512,7 @@ def fetch_host_key(host, port=22, timeout=5.0, kex_algos=KEX_ALGOS, host_key_alg
             x = int.from_bytes(os.urandom(32), "big") | (1 << 255)
             e = pow(2, x, GROUP14_P)
             conn.send_packet(bytes([MSG_KEXDH_INIT]) + ssh_mpint(e))
-        while True:
-            reply = conn.read_packet()
-            if reply and reply[0] in (MSG_IGNORE, MSG_DEBUG):
-                continue
-            break
+        reply = conn.read_message()
         if not reply or reply[0] != MSG_KEXDH_REPLY:
             if reply and reply[0] == MSG_DISCONNECT:
                 rr = Reader(reply[1:])

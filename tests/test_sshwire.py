@@ -12,6 +12,7 @@ import socket
 import struct
 import subprocess
 import threading
+import time
 
 import pytest
 
@@ -349,4 +350,53 @@ def test_hostile_servers_fail_cleanly(chunks):
         with pytest.raises((sshwire.SSHError, OSError)):
             sshwire.fetch_host_key("127.0.0.1", port=srv.getsockname()[1], timeout=5)
     finally:
+        srv.close()
+
+
+def test_chatty_servers_are_cut_off():
+    # banner lines and IGNORE packets are allowed, but not without end
+    srv = _serve_bytes([b"hello\r\n" * (sshwire.MAX_BANNER_LINES + 5)])
+    try:
+        with pytest.raises(sshwire.SSHError, match="version line"):
+            sshwire.fetch_host_key("127.0.0.1", port=srv.getsockname()[1], timeout=5)
+    finally:
+        srv.close()
+    ignore = _pkt(bytes([sshwire.MSG_IGNORE]) + ssh_string(b""))
+    srv = _serve_bytes([b"SSH-2.0-x\r\n", ignore * (sshwire.MAX_SKIPPED + 5)])
+    try:
+        with pytest.raises(sshwire.SSHError, match="IGNORE"):
+            sshwire.fetch_host_key("127.0.0.1", port=srv.getsockname()[1], timeout=5)
+    finally:
+        srv.close()
+
+
+def test_dripping_server_is_bounded_by_the_timeout():
+    # one byte every 0.2 s never trips a per-recv timeout of 1 s; the deadline
+    # for the whole exchange does
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    stop = threading.Event()
+
+    def serve():
+        try:
+            c, _ = srv.accept()
+        except OSError:
+            return
+        try:
+            while not stop.is_set():
+                c.sendall(b"x")
+                stop.wait(0.2)
+        except OSError:
+            pass
+        finally:
+            c.close()
+    threading.Thread(target=serve, daemon=True).start()
+    t0 = time.monotonic()
+    try:
+        with pytest.raises((sshwire.SSHError, OSError)):
+            sshwire.fetch_host_key("127.0.0.1", port=srv.getsockname()[1], timeout=1.0)
+        assert time.monotonic() - t0 < 3
+    finally:
+        stop.set()
         srv.close()
