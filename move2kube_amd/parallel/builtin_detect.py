@@ -233,20 +233,38 @@ def lookup(script_dir, script):
     return _lookup(script_dir, script)
 
 
-def _lookup(script_dir, script):
-    assets = os.path.abspath(settings.assets_path)
+_resolved = {}  # (script_dir, script, assets_path), all absolute -> (key, path) or None
+
+
+def _resolve(script_dir, script, assets_path):
+    """(detector key, script path) when ``script_dir`` lies in the assets tree
+    and names a built-in detector, else None (pure path arithmetic)."""
+    assets = os.path.abspath(assets_path)
     d = os.path.abspath(script_dir)
     if not d.startswith(assets + os.sep):
         return None
-    rel = os.path.relpath(d, assets)
-    key = (rel, script)
-    fn = DETECTORS.get(key)
-    if fn is None:
+    key = (os.path.relpath(d, assets), script)
+    if key not in DETECTORS:
         return None
+    return key, os.path.join(d, script)
+
+
+def _lookup(script_dir, script):
+    assets_path = settings.assets_path
+    if os.path.isabs(script_dir) and os.path.isabs(assets_path):
+        mk = (script_dir, script, assets_path)
+        r = _resolved.get(mk, _MISSING)
+        if r is _MISSING:
+            r = _resolved[mk] = _resolve(script_dir, script, assets_path)
+    else:  # relative to the working directory: nothing to remember
+        r = _resolve(script_dir, script, assets_path)
+    if r is None:
+        return None
+    key, path = r
+    fn = DETECTORS[key]
     want = _packaged_bytes(key)
     if want is None:
         return None
-    path = os.path.join(d, script)
     try:
         st = os.stat(path)
     except OSError:

@@ -123,7 +123,8 @@ def fetch_answer(prob):
             err = None
         except Exception as ex:  # noqa: BLE001
             err = ex
-            log.warning("Error while fetching answer using engine %s : %s", e.go_s(), ex)
+            if log.logger.isEnabledFor(log.WARNING):  # go_s() prints the engine's whole cache
+                log.warning("Error while fetching answer using engine %s : %s", e.go_s(), ex)
             continue
         if ans.resolved:
             break
