@@ -20,13 +20,14 @@ from ..k8s import scheme
 from ..models import collection
 from ..utils import common, log, yamlio
 from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
+from ..utils.lazyre import lazy as _lazy_re
 from . import Collector, CommandError, run
 
 GLOBAL_GROUP_ORDER = [r"^.+\.openshift\.io$", r"^.+\.k8s\.io$", r"^apps$", r"^extensions$"]
 
 # Masterminds/semver v3.1.1 (go.mod:9): NewVersion's pattern and Compare
-_SEMVER_RE = re.compile(r"v?([0-9]+)(\.[0-9]+)?(\.[0-9]+)?(-([0-9A-Za-z\-]+(\.[0-9A-Za-z\-]+)*))?"
-                        r"(\+([0-9A-Za-z\-]+(\.[0-9A-Za-z\-]+)*))?\Z")
+_SEMVER_RE = _lazy_re(r"v?([0-9]+)(\.[0-9]+)?(\.[0-9]+)?(-([0-9A-Za-z\-]+(\.[0-9A-Za-z\-]+)*))?"
+                       r"(\+([0-9A-Za-z\-]+(\.[0-9A-Za-z\-]+)*))?\Z")
 
 
 def _semver(v):

@@ -19,6 +19,7 @@ import threading
 from ...utils import common, fastjson, log, proc
 from ...utils.constants import settings
 from ...utils.lazyre import LazyModule
+from ...utils.lazyre import lazy as _lazy_re
 
 subprocess = LazyModule("subprocess")
 
@@ -46,6 +47,9 @@ def get_builders_from_label(label):
         for bp in (og or {}).get("group") or []:
             out.append(bp.get("id", ""))
     return out
+
+
+_PACK_GROUP_RE = _lazy_re(r"(?s)Group\s#\d+:[\r\n\s]+[^\s]+")
 
 
 class ProviderError(RuntimeError):
@@ -579,9 +583,8 @@ class PackProvider:
         raise ProviderError("Error while using pack")
 
     def get_all_buildpacks(self, builders):
-        import re
         out = {}
-        rx = re.compile(r"(?s)Group\s#\d+:[\r\n\s]+[^\s]+")
+        rx = _PACK_GROUP_RE
         for b in builders:
             try:
                 p = _run(["pack", "inspect-builder", b])

@@ -4,6 +4,9 @@
 * ``libm2k_ed_hip.so`` - HIP library for gfx950 (``hipcc --offload-arch=gfx950``).
 * ``move2kube_amd/_bytecode.bin`` - compiled code of every package module in
   one file (``ops/bytecode.py``), read once per CLI process.
+* ``move2kube_amd/_startcache.bin`` - the packaged Go templates parsed and the
+  package's regular expressions compiled (``ops/startcache_build.py``,
+  ``utils/startcache.py``).
 
 Run ``python -m move2kube_amd.ops.build`` (or ``__graft_entry__.build()``).
 Builds are incremental: a target is rebuilt only when its sources changed.
@@ -105,10 +108,20 @@ def build_bytecode(force=False):
     return bytecode.write()
 
 
+def build_startcache(force=False):
+    """The start-up cache of parsed templates and compiled regular expressions
+    (``ops/startcache_build.py``)."""
+    from . import startcache_build
+    if not force and not startcache_build.stale():
+        return startcache_build.target()
+    return startcache_build.write()
+
+
 def build_all(force=False):
     outs = [build_native(force)]
     outs.append(build_hip(force))
     outs.append(build_bytecode(force))
+    outs.append(build_startcache(force))
     return outs
 
 
@@ -122,7 +135,9 @@ def build_report(force=True):
     for name, fn, target in (("_m2k_native (g++, C++17/pybind11)", build_native, native_target()),
                              ("libm2k_ed_hip (hipcc --offload-arch=gfx950)", build_hip, hip_target()),
                              ("_bytecode.bin (package bytecode bundle)", build_bytecode,
-                              os.path.join(os.path.dirname(HERE), "_bytecode.bin"))):
+                              os.path.join(os.path.dirname(HERE), "_bytecode.bin")),
+                             ("_startcache.bin (parsed templates, compiled regexes)", build_startcache,
+                              os.path.join(os.path.dirname(HERE), "_startcache.bin"))):
         before = os.path.getmtime(target) if os.path.exists(target) else None
         t0 = time.perf_counter()
         out = fn(force)

@@ -17,6 +17,7 @@ from ...utils.lazyre import lazy as _lazy_re
 
 _PATTERN = _lazy_re(
     r"\$(?:(?P<escaped>\$)|(?P<named>[_a-zA-Z][_a-zA-Z0-9]*)|\{(?P<braced>[_a-zA-Z][_a-zA-Z0-9]*(?::?[-?][^}]*)?)\}|(?P<invalid>))")
+_BRACED_RE = _lazy_re(r"^([_a-zA-Z][_a-zA-Z0-9]*)(?:(:?)([-?])(.*))?$", re.S)
 
 
 class InterpolationError(ValueError):
@@ -31,7 +32,7 @@ def substitute(s, mapping, warn_missing=False):
         if name is None:
             raise InterpolationError("Invalid template: %r" % s)
         if m.group("braced") is not None:
-            mm = re.match(r"^([_a-zA-Z][_a-zA-Z0-9]*)(?:(:?)([-?])(.*))?$", name, re.S)
+            mm = _BRACED_RE.match(name)
             var, colon, op, arg = mm.group(1), mm.group(2), mm.group(3), mm.group(4)
             val = mapping(var)
             if op == "-":

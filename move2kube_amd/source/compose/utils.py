@@ -4,7 +4,6 @@ specs, volume specs, Kubernetes quantity formatting)."""
 
 import functools
 import os
-import re
 
 from ...utils import common, fsindex, log
 from ...utils.constants import settings
@@ -75,6 +74,7 @@ def parse_duration(s):
     return -v if neg else v
 
 
+_BRACKETED_HOST_RE = _lazy_re(r"^\[([^\]]+)\]:(.*)$")
 _RAM_RE = _lazy_re(r"^(\d+(?:\.\d+)*) ?([kKmMgGtTpP])?[iI]?[bB]?$")
 _RAM_MULT = {"k": 1024, "m": 1024 ** 2, "g": 1024 ** 3, "t": 1024 ** 4, "p": 1024 ** 5}
 
@@ -160,7 +160,7 @@ def parse_port_spec(raw):
     parts = spec.rsplit(":", 2) if spec.count(":") <= 2 else None
     if parts is None:
         # IPv6 host ip in brackets
-        m = re.match(r"^\[([^\]]+)\]:(.*)$", spec)
+        m = _BRACKETED_HOST_RE.match(spec)
         if not m:
             raise ValueError("Invalid port spec %r" % raw)
         rest = m.group(2).split(":")

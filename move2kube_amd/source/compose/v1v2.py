@@ -13,7 +13,6 @@ them.
 """
 
 import os
-import re
 
 from ...containerizer.reusedockerfile import ReuseDockerfileContainerizer
 from ...models import ir as irtypes
@@ -42,7 +41,8 @@ SUPPORTED_V2 = {"2", "2.0", "2.1"}
 
 
 def _normalize_project_name(s):
-    return re.sub(r"[^a-z0-9]", "", common.go_lower(s))
+    # re.sub(r"[^a-z0-9]", "", strings.ToLower(s))
+    return "".join(c for c in common.go_lower(s) if "a" <= c <= "z" or "0" <= c <= "9")
 
 
 def _read_raw(path):
@@ -344,7 +344,8 @@ def _resolve(p, base):
 
 
 def _is_url(s):
-    return re.match(r"^(https?://|git://|github\.com/|git@)", s) is not None
+    # ^(https?://|git://|github\.com/|git@)
+    return s.startswith(("http://", "https://", "git://", "github.com/", "git@"))
 
 
 def _load_service(name, d, base, version):
@@ -532,11 +533,11 @@ class V1V2Loader:
     def get_envs(envars):
         out = []
         for e in envars:
-            m = re.search(r"[=:]", e)
-            if m is None:
+            i = min((j for j in (e.find("="), e.find(":")) if j >= 0), default=-1)  # [=:]
+            if i < 0:
                 out.append({"name": e, "value": "unknown"})
             else:
-                out.append({"name": e[:m.start()], "value": e[m.start() + 1:]})
+                out.append({"name": e[:i], "value": e[i + 1:]})
         return out
 
     @staticmethod

@@ -6,7 +6,6 @@ tree root, read directly from ``.git/config`` and ``.git/HEAD``.
 """
 
 import os
-import re
 
 from . import fsindex
 from .lazyre import lazy as _lazy_re
@@ -177,6 +176,7 @@ def go_ext(p):
     return ""
 
 
+_SCP_HOST_RE = _lazy_re(r"^(?:[\w.\-]+@)?([\w.\-]+):(?!//)")
 _SCHEME_RE = _lazy_re(r"^([A-Za-z][A-Za-z0-9+.\-]*):")
 _HEX = "0123456789abcdefABCDEF"
 
@@ -260,7 +260,7 @@ def url_hostname(giturl):
     """Hostname of a git URL (scp-like ``git@host:org/repo`` or URL forms); '' if none."""
     if not giturl:
         return ""
-    m = re.match(r"^(?:[\w.\-]+@)?([\w.\-]+):(?!//)", giturl)
+    m = _SCP_HOST_RE.match(giturl)
     if m and "://" not in giturl:
         return m.group(1)
     try:

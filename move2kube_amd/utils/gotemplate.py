@@ -240,6 +240,7 @@ def go_sprintf(fmt, args):
 
 # The token grammar; _scan_token implements it by hand (compiling this costs a
 # cold process ~1 ms) and tests/test_gotemplate_lexer.py checks the two agree.
+_INT_RE = _lazy_re(r"^[-+]?\d+$")
 _TOKEN_RE = _lazy_re(r"""
     (?P<ws>\s+)
   | (?P<comment>/\*.*?\*/)
@@ -485,7 +486,7 @@ def _parse_number(text):
         return sign * int(low[2:], 2)
     if low.startswith("0o"):
         return sign * int(low[2:], 8)
-    if re.match(r"^[-+]?\d+$", t):
+    if _INT_RE.match(t):
         if len(low) > 1 and low.startswith("0"):
             return sign * int(low, 8)
         return int(t)
@@ -712,12 +713,88 @@ class Template:
         body, _ = self._parse_list(("end",))
         return body
 
+    # -- the parsed form as plain data (utils/startcache.py) -----------------
+    def to_data(self):
+        """The parse tree as nested tuples, lists and constants (marshal-able)."""
+        return (_nodes_data(self.root), {k: _nodes_data(v) for k, v in self.defines.items()})
+
+    @classmethod
+    def from_data(cls, data, name=""):
+        """The template :meth:`to_data` described, without parsing."""
+        t = cls.__new__(cls)
+        t.name = name
+        root, defines = data
+        t.root = _nodes_from(root)
+        t.defines = {k: _nodes_from(v) for k, v in defines.items()}
+        return t
+
     # -- execution ---------------------------------------------------------
     def execute(self, data, funcs=None):
         out = []
         st = _State(self, data, funcs or {})
         st.walk(self.root, data, [("$", data)], out)
         return "".join(out)
+
+
+def _pipe_data(p):
+    return None if p is None else (tuple(p.decls), [[_operand_data(a) for a in c] for c in p.cmds], p.is_assign)
+
+
+def _operand_data(a):
+    return ("pipe", _pipe_data(a[1]), a[2]) if a[0] == "pipe" else a
+
+
+def _nodes_data(nodes):
+    out = []
+    for n in nodes:
+        if isinstance(n, _Text):
+            out.append(("t", n.text))
+        elif isinstance(n, _Action):
+            out.append(("a", _pipe_data(n.pipe)))
+        elif isinstance(n, _If):
+            out.append(("i", n.kind, _pipe_data(n.pipe), _nodes_data(n.body),
+                        None if n.else_body is None else _nodes_data(n.else_body)))
+        elif isinstance(n, _TemplateCall):
+            out.append(("c", n.name, _pipe_data(n.pipe)))
+        elif isinstance(n, _Break):
+            out.append(("b",))
+        elif isinstance(n, _Continue):
+            out.append(("k",))
+        else:
+            raise TypeError("unknown template node %r" % (n,))
+    return out
+
+
+def _pipe_from(d):
+    if d is None:
+        return None
+    decls, cmds, is_assign = d
+    return _Pipe(list(decls), [[_operand_from(a) for a in c] for c in cmds], is_assign)
+
+
+def _operand_from(a):
+    return ("pipe", _pipe_from(a[1]), a[2]) if a[0] == "pipe" else a
+
+
+def _nodes_from(data):
+    out = []
+    for d in data:
+        k = d[0]
+        if k == "t":
+            out.append(_Text(d[1]))
+        elif k == "a":
+            out.append(_Action(_pipe_from(d[1])))
+        elif k == "i":
+            out.append(_If(d[1], _pipe_from(d[2]), _nodes_from(d[3]), None if d[4] is None else _nodes_from(d[4])))
+        elif k == "c":
+            out.append(_TemplateCall(d[1], _pipe_from(d[2])))
+        elif k == "b":
+            out.append(_Break())
+        elif k == "k":
+            out.append(_Continue())
+        else:
+            raise ValueError("unknown template node %r" % (k,))
+    return out
 
 
 class _State:
@@ -1041,10 +1118,14 @@ _CACHE = {}
 
 
 def compiled(src):
-    """The parsed template of ``src`` (cached); a parse error raises."""
+    """The parsed template of ``src`` (cached); a parse error raises.  A
+    packaged template comes from the build's start-up cache
+    (``utils/startcache.py``) instead of being parsed in every process."""
     t = _CACHE.get(src)
     if t is None:
-        t = Template(src)
+        from . import startcache
+        data = startcache.template(src)
+        t = Template(src) if data is None else Template.from_data(data)
         if len(_CACHE) < 512:
             _CACHE[src] = t
     return t

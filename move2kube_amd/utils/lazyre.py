@@ -5,7 +5,8 @@ import time - about a fifth of a cold ``translate`` was spent there, mostly on
 patterns the run never used (YAML timestamp forms, compose durations, semver).
 :class:`LazyPattern` has the ``re.Pattern`` interface and compiles on the first
 attribute access; after that the compiled pattern's bound methods are instance
-attributes, so the hot path is a plain attribute lookup.
+attributes, so the hot path is a plain attribute lookup.  Patterns the
+build's start-up cache holds skip ``sre_compile`` altogether (:func:`compile`).
 """
 
 import re
@@ -14,17 +15,25 @@ _FORWARDED = ("match", "fullmatch", "search", "sub", "subn", "split", "findall",
               "pattern", "flags", "groups", "groupindex")
 
 
+def compile(pattern, flags=0):
+    """``re.compile``, served from the build's start-up cache when it holds
+    the pattern (``utils/startcache.py``: no ``sre_compile`` in the process)."""
+    from . import startcache
+    rx = startcache.regex(pattern, flags)
+    return rx if rx is not None else re.compile(pattern, flags)
+
+
 class LazyPattern:
     def __init__(self, pattern, flags=0):
         self._args = (pattern, flags)
 
     def compiled(self):
-        return re.compile(*self._args)
+        return compile(*self._args)
 
     def __getattr__(self, name):
         if name.startswith("__") or name == "_args":
             raise AttributeError(name)
-        rx = re.compile(*self._args)
+        rx = compile(*self._args)
         for n in _FORWARDED:
             setattr(self, n, getattr(rx, n))
         return getattr(rx, name)

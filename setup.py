@@ -28,7 +28,7 @@ def _package_data():
     for dp, dns, fns in os.walk(root):
         dns[:] = [d for d in dns if d != "__pycache__"]
         for fn in fns:
-            if fn.endswith((".py", ".pyc", ".tmp")) or fn == "_bytecode.bin":
+            if fn.endswith((".py", ".pyc", ".tmp", ".inputs")) or fn == "_bytecode.bin":
                 continue
             out.append(os.path.relpath(os.path.join(dp, fn), root))
     return sorted(out)

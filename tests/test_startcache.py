@@ -1,0 +1,146 @@
+"""The build's start-up cache (utils/startcache.py, ops/startcache_build.py):
+parsed packaged templates and compiled package regexes must be exactly what
+parsing and ``re.compile`` give, and the cache must step aside whenever it
+could be wrong (another interpreter, another template parser)."""
+
+import marshal
+import os
+import re
+
+import pytest
+
+from move2kube_amd.ops import startcache_build
+from move2kube_amd.utils import gotemplate, lazyre, startcache
+
+
+@pytest.fixture()
+def cache_file(tmp_path, monkeypatch):
+    out = str(tmp_path / "_startcache.bin")
+    startcache_build.write(out)
+    monkeypatch.setattr(startcache, "PATH", out)
+    startcache.reset()
+    yield out
+    startcache.reset()
+
+
+def _entries(path):
+    with open(path, "rb") as f:
+        return marshal.loads(f.read())
+
+
+def test_every_cached_regex_equals_re_compile(cache_file):
+    _, _, _, regexes = _entries(cache_file)
+    assert len(regexes) >= 20
+    for (pattern, flags) in regexes:
+        rx = startcache.regex(pattern, flags)
+        assert rx is not None, pattern
+        ref = re.compile(pattern, flags)
+        assert rx == ref  # Pattern.__eq__: same flags, pattern and compiled code
+        assert (rx.groups, dict(rx.groupindex), rx.flags) == (ref.groups, dict(ref.groupindex), ref.flags)
+
+
+def test_package_patterns_are_found_by_the_source_scan():
+    found = startcache_build._patterns_in(
+        "import re\n"
+        "A = _lazy_re(r'^a+$')\n"
+        "B = lazyre.lazy('b', re.I | re.M)\n"
+        "def f(s):\n"
+        "    re.match(r'(x)', s, re.S)\n"
+        "    re.sub('y', '', s, 0, re.I)\n"
+        "    re.search('z', s, flags=re.A)\n"
+        "    re.compile(s)\n"  # not a literal: skipped
+        "    re.split('w', s, 0, some_flags)\n")  # flags not a constant: skipped
+    assert found == {("^a+$", 0), ("b", re.I | re.M), ("(x)", re.S), ("y", re.I), ("z", re.A)}
+    _, regexes = startcache_build.collect()
+    from move2kube_amd.source import dockerfile_parser
+    assert (dockerfile_parser.FROM_RE._args[0], 0) in regexes
+
+
+def test_lazy_patterns_come_from_the_cache(cache_file, monkeypatch):
+    import sre_compile
+
+    def refuse(*a, **k):
+        raise AssertionError("sre_compile used for a cached pattern")
+    monkeypatch.setattr(sre_compile, "compile", refuse)
+    rx = lazyre.LazyPattern(r"^[-+]?(\.[0-9]+|[0-9]+(\.[0-9]*)?)([eE][-+]?[0-9]+)?$")
+    assert rx.match("1.5e3") and not rx.match("1.5e")
+    monkeypatch.undo()
+    assert lazyre.compile("not(in)cache[0-9]") == re.compile("not(in)cache[0-9]")
+
+
+def test_every_cached_template_is_the_parse(cache_file):
+    _, _, templates, _ = _entries(cache_file)
+    assert len(templates) >= 20
+    for src, blob in templates.items():
+        data = marshal.loads(blob)
+        assert startcache.template(src) == data
+        assert gotemplate.Template.from_data(data).to_data() == gotemplate.Template(src).to_data()
+
+
+def test_packaged_templates_render_the_same_from_the_cache(cache_file):
+    from move2kube_amd import assets
+    data = {"IsHelm": False, "IngressHost": "example.com", "ExposedServicePaths": {"api": "/api", "web": "/"},
+            "Project": "p", "NewImages": True, "Helm": True, "AddCopySourcesWarning": True,
+            "Images": ["a", "b"], "RegistryURL": "quay.io", "RegistryNamespace": "ns"}
+    for name in ("notes.txt.tpl", "k8sreadme.md.tpl", "pushimages.sh.tpl", "deploy.sh.tpl"):
+        src = assets.template(name)
+        assert startcache.template(src) is not None, name
+        cached = gotemplate.Template.from_data(startcache.template(src)).execute(data)
+        assert cached == gotemplate.Template(src).execute(data)
+
+
+def test_round_trip_of_every_node_kind():
+    src = ('{{define "row"}}{{.}}|{{end}}{{block "b" .X}}[{{.}}]{{end}}'
+           '{{range $i, $v := .L}}{{if eq $v 2}}{{continue}}{{else if eq $v 4}}{{break}}{{end}}'
+           '{{template "row" $v}}{{end}}{{with .M}}{{.k}}{{else}}none{{end}}'
+           '{{$x := (printf "%d-%s" 3 "z")}}{{$x = print $x "!"}}{{$x}} {{len .L | printf "%03d"}}'
+           '{{/* comment */}}{{- " trimmed " -}} {{nil | print}} {{true}} {{1.5}} {{0x1F}} {{.M.k}}')
+    t = gotemplate.Template(src)
+    data = t.to_data()
+    assert marshal.loads(marshal.dumps(data)) == data
+    back = gotemplate.Template.from_data(data)
+    d = {"X": "x", "L": [1, 2, 3, 4, 5], "M": {"k": "v"}}
+    assert back.execute(d) == t.execute(d) == "[x]1|3|v3-z! 005 trimmed <nil> true 1.5 31 v"
+
+
+def test_cache_steps_aside_for_another_parser(cache_file, monkeypatch, tmp_path):
+    other = tmp_path / "gotemplate.py"
+    other.write_text("# another parser\n")
+    monkeypatch.setattr(startcache, "GOTEMPLATE_SRC", str(other))
+    startcache.reset()
+    from move2kube_amd import assets
+    assert startcache.template(assets.template("notes.txt.tpl")) is None
+    assert startcache.regex("^[-+]?\\d+$") is not None  # regexes do not depend on the parser
+
+
+def test_cache_steps_aside_for_another_interpreter(cache_file, monkeypatch):
+    tag, stamp, templates, regexes = _entries(cache_file)
+    with open(cache_file, "wb") as f:
+        f.write(marshal.dumps(("3.9.0|cpython-39|0|4", stamp, templates, regexes)))
+    startcache.reset()
+    assert startcache.regex("^[-+]?\\d+$") is None
+    from move2kube_amd import assets
+    assert startcache.template(assets.template("notes.txt.tpl")) is None
+
+
+def test_switch_missing_and_corrupt_files(cache_file, monkeypatch):
+    monkeypatch.setenv("M2K_STARTCACHE", "0")
+    startcache.reset()
+    assert startcache.regex("^[-+]?\\d+$") is None
+    monkeypatch.delenv("M2K_STARTCACHE")
+    with open(cache_file, "wb") as f:
+        f.write(b"\x00garbage")
+    startcache.reset()
+    assert startcache.regex("^[-+]?\\d+$") is None
+    os.remove(cache_file)
+    startcache.reset()
+    assert startcache.regex("^[-+]?\\d+$") is None
+
+
+def test_staleness(tmp_path):
+    out = str(tmp_path / "_startcache.bin")
+    assert startcache_build.stale(out)
+    startcache_build.write(out)
+    assert not startcache_build.stale(out)
+    os.remove(out + ".inputs")
+    assert startcache_build.stale(out)
