@@ -17,18 +17,29 @@ a struct name, ``*T`` (pointer), ``[]T`` (slice), ``map:T`` (map of T) or
 ``inline:T`` (embedded struct).
 """
 
-_STRUCTS = {}
+_STRUCTS = {}  # struct name -> its field DSL string (parsed on use: _fields)
+_parsed = {}
 
 
 def _def(name, spec):
-    fields = []
-    for item in spec.split():
-        o = item.endswith(",o")
-        if o:
-            item = item[:-2]
-        jname, typ = item.split(":", 1)
-        fields.append((jname, typ, o))
-    _STRUCTS[name] = fields
+    _STRUCTS[name] = spec
+
+
+def _fields(name):
+    """[(json name, field type, omitempty)] of a struct.  Parsed when first
+    needed: a CLI run hands the strings to the native marshaller, which parses
+    them itself, and only the Python fallback and the checks need tuples."""
+    fields = _parsed.get(name)
+    if fields is None:
+        fields = []
+        for item in _STRUCTS[name].split():
+            o = item.endswith(",o")
+            if o:
+                item = item[:-2]
+            jname, typ = item.split(":", 1)
+            fields.append((jname, typ, o))
+        _parsed[name] = fields
+    return fields
 
 
 # -- meta --------------------------------------------------------------------
@@ -413,7 +424,7 @@ def _check_value(v, typ, path):
 def _check_struct(d, typ, path):
     if not isinstance(d, dict):
         _mismatch(d, typ, path)
-    for jname, ftype, _omit in _STRUCTS[typ]:
+    for jname, ftype, _omit in _fields(typ):
         if jname == "inline":
             _check_struct(d, ftype, path)
             continue
@@ -529,7 +540,7 @@ def _plan(typ):
     pl = _plans.get(typ)
     if pl is None:
         pl = []
-        for jname, ftype, omit in _STRUCTS[typ]:
+        for jname, ftype, omit in _fields(typ):
             if jname == "inline":
                 absent = None
             elif ftype in _STRUCTS:
@@ -674,7 +685,7 @@ _native_fn = None
 
 def _native_marshal():
     """``schema_marshal`` of the native extension (ops/csrc/k8s_marshal.cpp),
-    compiled from ``_STRUCTS`` on first use; False when it is unavailable or
+    compiled from the ``_STRUCTS`` field strings on first use; False when it is unavailable or
     ``M2K_NATIVE_MARSHAL=0``.  This module stays its specification."""
     global _native_fn
     if _native_fn is None:

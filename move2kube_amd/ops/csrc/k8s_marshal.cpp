@@ -5,8 +5,8 @@
 // its Go struct before the YAML encoder).
 //
 // schema.py stays the executable specification.  At first use it hands its
-// struct table (name -> [(json name, field type, omitempty)]) to
-// `schema_init`, which compiles every field type once; `schema_marshal(obj,
+// struct table (name -> its field DSL string, or [(json name, field type,
+// omitempty)]) to `schema_init`, which parses and compiles every field once; `schema_marshal(obj,
 // type)` then walks the JSON-shaped Python tree with the raw CPython API and
 // returns the same dict tree the Python code builds (same keys, same key
 // order, the same shared per-type empty-struct dicts).  Anything outside the
@@ -370,9 +370,73 @@ static PyObject* marshal_value(PyObject* v, int type) {
 
 }  // namespace m2kschema
 
+namespace m2kschema {
+
+struct FieldSpec {
+  std::string jname, ftype;
+  bool omit;
+};
+
+static bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\f' || c == '\v'; }
+
+// One struct's fields, from either form schema.py can hand over: its field
+// DSL string ("jsonName:type[,o] ...", split on whitespace as str.split()
+// does for ASCII) or a sequence of (json name, field type, omitempty).
+static bool field_specs(PyObject* fields, std::vector<FieldSpec>& out) {
+  if (PyUnicode_Check(fields)) {
+    Py_ssize_t n = 0;
+    const char* c = PyUnicode_AsUTF8AndSize(fields, &n);
+    if (!c) return false;
+    std::string src(c, (size_t)n);
+    size_t i = 0;
+    while (i < src.size()) {
+      while (i < src.size() && is_space(src[i])) ++i;
+      size_t j = i;
+      while (j < src.size() && !is_space(src[j])) ++j;
+      if (j == i) break;
+      std::string item = src.substr(i, j - i);
+      i = j;
+      FieldSpec f;
+      f.omit = item.size() >= 2 && item.compare(item.size() - 2, 2, ",o") == 0;
+      if (f.omit) item.resize(item.size() - 2);
+      size_t colon = item.find(':');
+      if (colon == std::string::npos) {
+        PyErr_Format(PyExc_ValueError, "field %s has no type", item.c_str());
+        return false;
+      }
+      f.jname = item.substr(0, colon);
+      f.ftype = item.substr(colon + 1);
+      out.push_back(std::move(f));
+    }
+    return true;
+  }
+  PyObject* seq = PySequence_Fast(fields, "fields must be a sequence or a field string");
+  if (!seq) return false;
+  Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject *jn, *ft, *om;
+    const char *jc = nullptr, *fc = nullptr;
+    if (!PyArg_ParseTuple(PySequence_Fast_GET_ITEM(seq, i), "UUO", &jn, &ft, &om) ||
+        (jc = PyUnicode_AsUTF8(jn)) == nullptr || (fc = PyUnicode_AsUTF8(ft)) == nullptr) {
+      Py_DECREF(seq);
+      return false;
+    }
+    int truth = PyObject_IsTrue(om);
+    if (truth < 0) {
+      Py_DECREF(seq);
+      return false;
+    }
+    out.push_back(FieldSpec{jc, fc, truth == 1});
+  }
+  Py_DECREF(seq);
+  return true;
+}
+
+}  // namespace m2kschema
+
 using namespace m2kschema;
 
-// schema_init(structs: {name: [(jname, ftype, omit)]}, fallback) -> None
+// schema_init(structs: {name: "field DSL" | [(jname, ftype, omit)]}, fallback) -> None
 extern "C" PyObject* m2k_schema_init(PyObject* structs, PyObject* fb) {
   if (!PyDict_Check(structs)) {
     PyErr_SetString(PyExc_TypeError, "structs must be a dict");
@@ -408,33 +472,21 @@ extern "C" PyObject* m2k_schema_init(PyObject* structs, PyObject* fb) {
   while (PyDict_Next(structs, &pos, &name, &fields)) {
     Struct& s = g->structs[ix++];
     s.keyed = PyDict_New();
-    PyObject* seq = s.keyed ? PySequence_Fast(fields, "fields must be a sequence") : nullptr;
-    if (!seq) {
+    std::vector<FieldSpec> specs;
+    if (!s.keyed || !field_specs(fields, specs)) {
       discard_schema();
       return nullptr;
     }
-    Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
-    for (Py_ssize_t i = 0; i < n; ++i) {
-      PyObject* item = PySequence_Fast_GET_ITEM(seq, i);
-      PyObject *jn, *ft, *om;
-      const char *jc = nullptr, *fc = nullptr;
-      if (!PyArg_ParseTuple(item, "UUO", &jn, &ft, &om) || (jc = PyUnicode_AsUTF8(jn)) == nullptr ||
-          (fc = PyUnicode_AsUTF8(ft)) == nullptr) {
-        Py_DECREF(seq);
+    for (FieldSpec& spec : specs) {
+      const std::string &jname = spec.jname, &ftype = spec.ftype;
+      const bool omit = spec.omit;
+      PyObject* jn = PyUnicode_FromStringAndSize(jname.data(), (Py_ssize_t)jname.size());
+      if (!jn) {
         discard_schema();
         return nullptr;
       }
-      std::string jname = jc, ftype = fc;
-      int truth = PyObject_IsTrue(om);
-      if (truth < 0) {
-        Py_DECREF(seq);
-        discard_schema();
-        return nullptr;
-      }
-      bool omit = truth == 1;
       Field f;
-      Py_INCREF(jn);
-      f.jname = jn;
+      f.jname = jn;  // owns the reference
       f.omit = omit;
       f.inline_ = jname == "inline";
       f.type = compile_type(ftype);
@@ -445,7 +497,6 @@ extern "C" PyObject* m2k_schema_init(PyObject* structs, PyObject* fb) {
         if (si == g->struct_index.end()) {
           Py_DECREF(jn);
           PyErr_Format(PyExc_ValueError, "inline type %s is not a struct", ftype.c_str());
-          Py_DECREF(seq);
           discard_schema();
           return nullptr;
         }
@@ -456,14 +507,12 @@ extern "C" PyObject* m2k_schema_init(PyObject* structs, PyObject* fb) {
         Py_XDECREF(idx);
         if (rc < 0) {
           Py_DECREF(jn);
-          Py_DECREF(seq);
           discard_schema();
           return nullptr;
         }
       }
       s.fields.push_back(f);
     }
-    Py_DECREF(seq);
   }
   g->ready = true;
   Py_RETURN_NONE;

@@ -113,7 +113,7 @@ def _random_value(rng, ftype, depth):
 
 def _random_struct(rng, typ, depth=0):
     d = {}
-    for jname, ftype, _omit in schema._STRUCTS[typ]:
+    for jname, ftype, _omit in schema._fields(typ):
         if jname == "inline":
             d.update(_random_struct(rng, ftype, depth))
             continue
@@ -170,3 +170,31 @@ def test_failed_schema_init_leaves_no_half_built_table():
     assert p.stdout.decode().splitlines() == ["init inline type Missing is not a struct",
                                               "marshal schema_init was not called",
                                               "{'name': 'c', 'resources': {}}"]
+
+
+def test_field_strings_and_tuples_compile_alike():
+    """schema_init takes each struct's field DSL string (what a CLI run hands
+    over) or its parsed tuples; both give the same marshalling, and a field
+    without a type is refused (fresh processes: a published table is kept)."""
+    import subprocess
+    probe = ("from move2kube_amd.ops import native\n"
+             "from move2kube_amd.k8s import schema\n"
+             "import sys\n"
+             "m = native.module()\n"
+             "if sys.argv[1] == 'bad':\n"
+             "    try:\n        m.schema_init({'A': 'name:string,o oops'}, schema._marshal_value)\n"
+             "    except ValueError as e:\n        print(e)\n"
+             "    raise SystemExit\n"
+             "table = {k: (v if sys.argv[1] == 'str' else schema._fields(k)) for k, v in schema._STRUCTS.items()}\n"
+             "m.schema_init(table, schema._marshal_value)\n"
+             "obj = {'metadata': {'name': 'x', 'labels': {'a': 'b'}}, 'spec': {'replicas': 2, 'template': {'spec': "
+             "{'containers': [{'name': 'c', 'ports': [{'containerPort': 80}]}]}}}}\n"
+             "print(sorted(m.schema_marshal(obj, 'Deployment').items()))\n")
+    outs = []
+    for form in ("str", "tuple", "bad"):
+        p = subprocess.run([sys.executable, "-c", probe, form], cwd=ROOT, stdout=subprocess.PIPE,
+                           stderr=subprocess.PIPE, timeout=60)
+        assert p.returncode == 0, p.stderr.decode()
+        outs.append(p.stdout.decode())
+    assert outs[0] == outs[1] and "'replicas': 2" in outs[0]
+    assert outs[2].strip() == "field oops has no type"
