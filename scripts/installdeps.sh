@@ -4,8 +4,8 @@
 #
 #   installdeps.sh [-y] [--check]
 #
-#   -y        no prompts: install everything missing and add the install
-#             directory to ~/.bash_profile (run with sudo when docker is wanted)
+#   -y        no prompts: install everything missing and put the install
+#             directory at the front of PATH in ~/.bash_profile (run with sudo when docker is wanted)
 #   --check   only report what is present / missing, install nothing
 #
 # Tools and what uses them:
@@ -157,10 +157,15 @@ fi
 
 echo "Installed the dependencies to $DEST"
 case ":$PATH:" in
-  *":$DEST:"*) echo "$DEST is already on \$PATH" ;;
+  *":$DEST:"*)
+    echo "$DEST is already on \$PATH"
+    if [ -x "$DEST/operator-sdk" ] && [ "$(command -v operator-sdk)" != "$DEST/operator-sdk" ]; then
+      echo "Warning: $(command -v operator-sdk) comes before $DEST/operator-sdk on \$PATH"
+    fi ;;
   *)
-    if confirm "Append $DEST to \$PATH in ~/.bash_profile?"; then
-      echo "PATH=\"\$PATH:$DEST\"" >> ~/.bash_profile
+    # ahead of the rest of PATH, so a replaced pre-v1 operator-sdk does not shadow the new one
+    if confirm "Put $DEST at the front of \$PATH in ~/.bash_profile?"; then
+      echo "PATH=\"$DEST:\$PATH\"" >> ~/.bash_profile
       echo "Added $DEST to \$PATH in ~/.bash_profile; open a new shell or source it."
     else
       echo "~/.bash_profile not modified; add $DEST to \$PATH yourself."

@@ -87,7 +87,7 @@ def test_installs_missing_tools_into_prefix(env, tmp_path):
         "https://github.com/operator-framework/operator-sdk/releases/download/v1.0.0/"
         "operator-sdk-v1.0.0-x86_64-linux-gnu",
     ] if os.uname().machine == "x86_64" else urls
-    assert ('PATH="$PATH:%s"' % deps) in (tmp_path / "home" / ".bash_profile").read_text()
+    assert ('PATH="%s:$PATH"' % deps) in (tmp_path / "home" / ".bash_profile").read_text()
     # a second run finds everything on PATH and downloads nothing
     env2 = dict(env, PATH="%s:%s" % (deps, env["PATH"]))
     os.remove(str(tmp_path / "urls.log"))
