@@ -7,8 +7,11 @@ detector-process pool, plus a gfx950 HIP kernel for large all-pairs fuzzy
 matching.  See SURVEY.md for the component map.
 """
 
+import _imp
+import marshal as _marshal
 import os as _os
 import sys as _sys
+from _frozen_importlib import ModuleSpec as _ModuleSpec
 
 
 class _BytecodeBundle:
@@ -35,8 +38,7 @@ class _BytecodeBundle:
             return None
         if int(st.st_mtime) != rec[2] or st.st_size != rec[3]:
             return None
-        from _frozen_importlib import ModuleSpec
-        spec = ModuleSpec(name, self, origin=origin, is_package=rec[0])
+        spec = _ModuleSpec(name, self, origin=origin, is_package=rec[0])
         spec.has_location = True
         if rec[0]:
             spec.submodule_search_locations = [_os.path.dirname(origin)]
@@ -49,10 +51,8 @@ class _BytecodeBundle:
         exec(self.get_code(module.__spec__.name), module.__dict__)
 
     def get_code(self, name):
-        import _imp
-        import marshal
         rec = self._mods[name]
-        code = marshal.loads(_os.pread(self._fd, rec[5], self._base + rec[4]))
+        code = _marshal.loads(_os.pread(self._fd, rec[5], self._base + rec[4]))
         _imp._fix_co_filename(code, _os.path.join(self._root, rec[1]))
         return code
 
@@ -70,7 +70,6 @@ class _BytecodeBundle:
 def _install_bytecode_bundle():
     if _os.environ.get("M2K_BYTECODE_BUNDLE", "1") == "0":
         return
-    import marshal
     from _frozen_importlib_external import MAGIC_NUMBER
     root = _os.path.dirname(_os.path.abspath(__file__))
     try:
@@ -82,7 +81,7 @@ def _install_bytecode_bundle():
         if head[:4] != b"M2KB" or len(head) != 8:
             raise ValueError
         n = int.from_bytes(head[4:], "big")
-        tag, optimize, mods = marshal.loads(_os.pread(fd, n, 8))
+        tag, optimize, mods = _marshal.loads(_os.pread(fd, n, 8))
         if tag != MAGIC_NUMBER + b"m2k2" or optimize != _sys.flags.optimize:
             raise ValueError
     except (OSError, ValueError, EOFError, TypeError):
