@@ -7,6 +7,7 @@
 #   COLD_AB=<tree> adds the same A/B of cold CLI starts (ab_bench.py --cold),
 #   PHASES=1 the per-configuration cold phase split (scripts/cold_phases.py),
 #   TRACE=1 the traced spans of cold CLI runs (benchmarks/cold_trace.py),
+#   BUDGET=1 the whole-process cold budget split (benchmarks/cold_budget.py),
 #   SKIP_BENCH=1 leaves out the GPU tests, smoke, bench and rocprof steps.
 #   RUN=r04_x AB=r03 gpurun --timeout 1200 -- bash scripts/gpu_pass.sh
 set -eo pipefail
@@ -51,5 +52,9 @@ if [ -n "$TRACE" ]; then
     timeout -k 10 180 python -u benchmarks/cold_trace.py "$c" --runs 15 | tee -a "$OUT/cold_trace.jsonl"
     timeout -k 10 180 python -u benchmarks/cold_importtime.py "$c" --runs 9 >> "$OUT/cold_importtime.jsonl"
   done
+fi
+if [ -n "$BUDGET" ]; then
+  echo "cold budget"
+  timeout -k 10 600 python -u benchmarks/cold_budget.py "${BUDGET_CONFIGS:-golang,java-cnb,cf,helm-openshift}" --runs "${BUDGET_RUNS:-30}" | tee "$OUT/cold_budget.jsonl"
 fi
 echo done

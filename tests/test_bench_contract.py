@@ -124,3 +124,14 @@ def test_cold_diagnostics_scripts_run():
     assert p.returncode == 0, p.stderr.decode()[-3000:]
     d = _last_json(p.stdout.decode())
     assert d["self_us_ours"] > 0 and "move2kube_amd.cli.main" in d["self_cum_us"]
+    p = subprocess.run([sys.executable, os.path.join("benchmarks", "cold_budget.py"), "golang", "--runs", "1"],
+                       cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    d = _last_json(p.stdout.decode())
+    assert d["modules"] > 20 and set(d["median_ms"]) == {"floor", "imports", "version", "command"}
+    p = subprocess.run([sys.executable, os.path.join("benchmarks", "switch_ab.py"), "M2K_STARTCACHE", "0", "1",
+                        "golang", "--pairs", "1"],
+                       cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    d = _last_json(p.stdout.decode())
+    assert set(d["median_ms"]) == {"0", "1"}
