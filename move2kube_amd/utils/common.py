@@ -331,9 +331,11 @@ def is_string_present(lst, value):
     """Case-insensitive membership (Go ``strings.EqualFold``)."""
     if not lst:
         return False
+    if value in lst:  # an exact match: the common case, no folding
+        return True
     v = go_fold(value)
     for x in lst:
-        if x == value or go_fold(x) == v:
+        if go_fold(x) == v:
             return True
     return False
 
