@@ -2,18 +2,22 @@
 """Where a configuration's cold CLI time above the bare interpreter goes,
 from the wall clock of whole processes only (no instrumentation inside them):
 
-* ``floor``     - ``python -c pass`` (the interpreter, ``site``, teardown);
-* ``imports``   - ``python -c "import ..."`` of exactly the package modules
-  the configuration's command imports (recorded once beforehand);
-* ``version``   - ``python -m move2kube_amd version``: the ``-m`` entry
+* ``floor``      - ``python -c pass`` (the interpreter, ``site``, teardown):
+  the driver's floor;
+* ``bare_exit``  - ``python -c "import os; os._exit(0)"``: the same without
+  the interpreter's teardown, which the CLI skips too (``_cli_exit``);
+* ``imports``    - ``python -c "import ...; os._exit(0)"`` of exactly the
+  package modules the configuration's command imports (recorded beforehand);
+* ``version``    - ``python -m move2kube_amd version``: the ``-m`` entry
   (``runpy``), the package and CLI start-up and a command that does nothing;
-* ``command``   - the configuration's last command (``translate ...``).
+* ``command``    - the configuration's last command (``translate ...``).
 
 The variants run round-robin, ``--runs`` rounds, so a drifting host hits all
-alike; medians are reported, and the differences: ``imports - floor`` (module
-loading), ``version - floor`` (the entry and CLI start-up, which includes the
-CLI's own imports) and ``command - imports`` (the command's work, the ``-m``
-entry and the exit).  One JSON line per configuration.
+alike; medians are reported, and the differences: ``floor - bare_exit`` (the
+teardown the CLI does not pay), ``imports - bare_exit`` (module loading),
+``version - bare_exit`` (the entry and CLI start-up, which includes the CLI's
+own imports) and ``command - imports`` (the command's work plus the ``-m``
+entry).  One JSON line per configuration.
 
     python benchmarks/cold_budget.py helm-openshift,golang --runs 40
 """
@@ -66,7 +70,8 @@ def budget(cfg, runs):
     py = sys.executable
     variants = {
         "floor": [py, "-c", "pass"],
-        "imports": [py, "-c", "import " + ", ".join(mods)],
+        "bare_exit": [py, "-c", "import os; os._exit(0)"],
+        "imports": [py, "-c", "import os, " + ", ".join(mods) + "; os._exit(0)"],
         "version": [py, "-m", "move2kube_amd", "version"],
         "command": [py, "-m", "move2kube_amd"] + argv,
     }
@@ -76,14 +81,17 @@ def budget(cfg, runs):
         names = names[i % len(names):] + names[:i % len(names)]  # rotate the order each round
         for k in names:
             t = time.perf_counter()
+            # no timeout=: with one, Popen.wait polls with sleeps of up to 50 ms
+            # and the measured walls come out in steps of that schedule
             subprocess.run(variants[k], env=env, cwd=work, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                           check=True, timeout=300)
+                           check=True)
             if i:  # round 0 primes the caches
                 times[k].append((time.perf_counter() - t) * 1e3)
     med = {k: round(statistics.median(v), 3) for k, v in times.items()}
     return {"config": cfg, "runs": runs, "modules": len(mods), "median_ms": med,
-            "imports_over_floor_ms": round(med["imports"] - med["floor"], 3),
-            "entry_and_cli_over_floor_ms": round(med["version"] - med["floor"], 3),
+            "teardown_skipped_ms": round(med["floor"] - med["bare_exit"], 3),
+            "imports_ms": round(med["imports"] - med["bare_exit"], 3),
+            "entry_and_cli_ms": round(med["version"] - med["bare_exit"], 3),
             "command_over_imports_ms": round(med["command"] - med["imports"], 3),
             "command_over_floor_ms": round(med["command"] - med["floor"], 3)}
 
