@@ -42,7 +42,9 @@ COPY --from=builder /opt/m2k-deps/operator-sdk /opt/m2k-deps/pack /opt/m2k-deps/
 COPY --from=builder /src/move2kube_amd /opt/move2kube-amd/move2kube_amd
 COPY --from=builder /src/samples /opt/move2kube-amd/samples
 # version stamp (the reference's -ldflags -X) and a launcher that runs the
-# package by file, so a move2kube_amd directory in /wksps cannot shadow it
+# package by file, so a move2kube_amd directory in /wksps cannot shadow it; the
+# start-up cache is rebuilt for this stage's interpreter (its compiled regexes
+# are only used by the interpreter build that made them)
 RUN printf 'VERSION = "%s"\nBUILD_METADATA = ""\nGIT_COMMIT = "%s"\nGIT_TREE_STATE = "%s"\n' \
       "${VERSION}" "${GIT_COMMIT}" "${GIT_TREE_STATE}" > /opt/move2kube-amd/move2kube_amd/_buildinfo.py \
  && if [ "${WITH_HIP}" != 1 ]; then rm -f /opt/move2kube-amd/move2kube_amd/ops/libm2k_ed_hip.so; fi \
@@ -51,6 +53,7 @@ RUN printf 'VERSION = "%s"\nBUILD_METADATA = ""\nGIT_COMMIT = "%s"\nGIT_TREE_STA
  && printf '#!/bin/sh\nexec python3 /opt/move2kube-amd/m2k_main.py "$@"\n' > /usr/local/bin/move2kube \
  && chmod +x /usr/local/bin/move2kube \
  && python3 -m compileall -q /opt/move2kube-amd/move2kube_amd \
+ && (cd /opt/move2kube-amd && python3 -m move2kube_amd.ops.startcache_build >/dev/null) \
  && operator-sdk version && move2kube version
 VOLUME /wksps
 WORKDIR /wksps

@@ -64,3 +64,11 @@ def test_ci_builds_the_image_and_runs_e2e():
     runs = " ".join(s.get("run", "") for s in job["steps"])
     assert "make cbuild" in runs and "scripts/image_e2e.sh" in runs and "docker push" in runs
     assert job["needs"] == ["cpu"]
+
+
+def test_runtime_stage_rebuilds_the_startcache_for_its_interpreter():
+    # the builder's python3 and the slim runtime's differ: the cache built in
+    # the builder would be ignored (utils/startcache.py interpreter tag)
+    text = open(os.path.join(ROOT, "Dockerfile")).read()
+    runtime = text[text.index("FROM ${RUNTIME_IMAGE}"):]
+    assert "move2kube_amd.ops.startcache_build" in runtime
