@@ -144,3 +144,21 @@ def test_staleness(tmp_path):
     assert not startcache_build.stale(out)
     os.remove(out + ".inputs")
     assert startcache_build.stale(out)
+
+
+def test_every_lazy_pattern_of_the_package_is_cached():
+    """The source scan finds every module-level lazy pattern: none of them
+    pays sre_compile in a CLI process."""
+    import gc
+    import importlib
+    import pkgutil
+
+    import move2kube_amd
+    for m in pkgutil.walk_packages(move2kube_amd.__path__, "move2kube_amd."):
+        if m.name.endswith("__main__") or m.name.endswith("libm2k_ed_hip"):
+            continue
+        importlib.import_module(m.name)
+    _, regexes = startcache_build.collect()
+    lazies = [o for o in gc.get_objects() if isinstance(o, lazyre.LazyPattern)]
+    assert len(lazies) >= 20
+    assert [o._args for o in lazies if (o._args[0], int(o._args[1])) not in regexes] == []
