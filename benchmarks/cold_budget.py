@@ -8,6 +8,8 @@ from the wall clock of whole processes only (no instrumentation inside them):
   the interpreter's teardown, which the CLI skips too (``_cli_exit``);
 * ``imports``    - ``python -c "import ...; os._exit(0)"`` of exactly the
   package modules the configuration's command imports (recorded beforehand);
+* ``version_c``  - the same ``version`` command run from ``-c`` (what
+  ``__main__`` does, without ``runpy``);
 * ``version``    - ``python -m move2kube_amd version``: the ``-m`` entry
   (``runpy``), the package and CLI start-up and a command that does nothing;
 * ``command``    - the configuration's last command (``translate ...``).
@@ -16,8 +18,9 @@ The variants run round-robin, ``--runs`` rounds, so a drifting host hits all
 alike; medians are reported, and the differences: ``floor - bare_exit`` (the
 teardown the CLI does not pay), ``imports - bare_exit`` (module loading),
 ``version - bare_exit`` (the entry and CLI start-up, which includes the CLI's
-own imports) and ``command - imports`` (the command's work plus the ``-m``
-entry).  One JSON line per configuration.
+own imports), ``version - version_c`` (the ``-m`` entry: ``runpy``) and
+``command - imports`` (the command's work plus the ``-m`` entry).  One JSON
+line per configuration.
 
     python benchmarks/cold_budget.py helm-openshift,golang --runs 40
 """
@@ -72,6 +75,8 @@ def budget(cfg, runs):
         "floor": [py, "-c", "pass"],
         "bare_exit": [py, "-c", "import os; os._exit(0)"],
         "imports": [py, "-c", "import os, " + ", ".join(mods) + "; os._exit(0)"],
+        "version_c": [py, "-c", "from move2kube_amd import _cli_exit, _cli_process\n_cli_process()\n"
+                      "from move2kube_amd.cli.main import main\nimport gc\ngc.freeze()\n_cli_exit(main(['version']))"],
         "version": [py, "-m", "move2kube_amd", "version"],
         "command": [py, "-m", "move2kube_amd"] + argv,
     }
@@ -92,6 +97,7 @@ def budget(cfg, runs):
             "teardown_skipped_ms": round(med["floor"] - med["bare_exit"], 3),
             "imports_ms": round(med["imports"] - med["bare_exit"], 3),
             "entry_and_cli_ms": round(med["version"] - med["bare_exit"], 3),
+            "runpy_entry_ms": round(med["version"] - med["version_c"], 3),
             "command_over_imports_ms": round(med["command"] - med["imports"], 3),
             "command_over_floor_ms": round(med["command"] - med["floor"], 3)}
 

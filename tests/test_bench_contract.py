@@ -128,7 +128,7 @@ def test_cold_diagnostics_scripts_run():
                        cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
     assert p.returncode == 0, p.stderr.decode()[-3000:]
     d = _last_json(p.stdout.decode())
-    assert d["modules"] > 20 and set(d["median_ms"]) == {"floor", "bare_exit", "imports", "version", "command"}
+    assert d["modules"] > 20 and set(d["median_ms"]) == {"floor", "bare_exit", "imports", "version_c", "version", "command"}
     p = subprocess.run([sys.executable, os.path.join("benchmarks", "switch_ab.py"), "M2K_STARTCACHE", "0", "1",
                         "golang", "--pairs", "1"],
                        cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
