@@ -19,11 +19,16 @@ call).  Values print with Go ``fmt`` ``%v`` semantics.
 """
 
 import math
+import os
 import re
 
 from . import fastjson
 from .lazyre import lazy as _lazy_re
 from .yamlio import go_format_float
+
+
+INTERPRET = os.environ.get("M2K_TEMPLATE_INTERPRET", "") == "1"  # the tree walker instead of closures
+COMPILE_AFTER = 1  # executions of a template interpreted before it is compiled to closures
 
 
 class TemplateError(Exception):
@@ -638,6 +643,7 @@ class Template:
         items = _split_template(src)
         self._items = items
         self._i = 0
+        self._range_depth = 0  # {{break}} / {{continue}} only inside a range body (Go's parse.Tree.rangeDepth)
         body, term = self._parse_list(())
         if term is not None:
             raise TemplateError("unexpected {{%s}}" % term)
@@ -666,7 +672,10 @@ class Template:
             if k == "ident" and t in ("if", "with", "range"):
                 p = _Parser(toks[1:])
                 pipe = p.pipeline(allow_decl=True)
+                depth = 1 if t == "range" else 0
+                self._range_depth += depth
                 body, term = self._parse_list(("end", "else"))
+                self._range_depth -= depth
                 nodes.append(_If(t, pipe, body, self._parse_else(t, term)))
                 continue
             if k == "ident" and t in ("define", "block"):
@@ -684,11 +693,10 @@ class Template:
                 pipe = _Parser(toks[2:]).pipeline(allow_decl=False) if len(toks) > 2 else None
                 nodes.append(_TemplateCall(name, pipe))
                 continue
-            if k == "ident" and t == "break":
-                nodes.append(_Break())
-                continue
-            if k == "ident" and t == "continue":
-                nodes.append(_Continue())
+            if k == "ident" and t in ("break", "continue"):
+                if not self._range_depth:
+                    raise TemplateError("{{%s}} outside {{range}}" % t)
+                nodes.append(_Break() if t == "break" else _Continue())
                 continue
             p = _Parser(toks)
             pipe = p.pipeline(allow_decl=True)
@@ -732,8 +740,29 @@ class Template:
     def execute(self, data, funcs=None):
         out = []
         st = _State(self, data, funcs or {})
-        st.walk(self.root, data, [("$", data)], out)
+        run = self.__dict__.get("_run")
+        if run is None:
+            # compiling costs about three executions: a template a process
+            # executes once (most of them, in a cold CLI run) is interpreted
+            runs = self.__dict__.get("_runs", 0)
+            if INTERPRET or runs < COMPILE_AFTER:
+                self._runs = runs + 1
+                st.walk(self.root, data, [("$", data)], out)
+                return "".join(out)
+            run = self._run = _c_nodes(self.root)
+        run(st, data, [("$", data)], out)
         return "".join(out)
+
+    def compiled_define(self, name):
+        """The compiled body of ``{{define name}}``, or None."""
+        cache = self.__dict__.setdefault("_defines_run", {})
+        run = cache.get(name)
+        if run is None:
+            body = self.defines.get(name)
+            if body is None:
+                return None
+            run = cache[name] = _c_nodes(body)
+        return run
 
 
 def _pipe_data(p):
@@ -819,7 +848,7 @@ class _State:
                 elif isinstance(node, _TemplateCall):
                     body = self.tmpl.defines.get(node.name)
                     if body is None:
-                        raise TemplateError("no such template %q" % node.name)
+                        raise TemplateError(go_sprintf("template %q not defined", [node.name]))
                     newdot = self.eval_pipe(node.pipe, dot, scope) if node.pipe else None
                     self.walk(body, newdot, [("$", newdot)], out)
                 elif isinstance(node, _Break):
@@ -966,6 +995,250 @@ class _State:
             else:
                 raise TemplateError("can't evaluate field %s in type %s" % (name, _go_type_name(val)))
         return val
+
+
+# ---------------------------------------------------------------------------
+# Compilation to closures
+# ---------------------------------------------------------------------------
+# Each node becomes a Python closure once per parsed template, so executing it
+# does no per-node dispatch on node and operand kinds.  The closures follow
+# _State.walk / walk_control / eval_pipe / eval_cmd / eval_arg step for step
+# (same evaluation order, same errors).  A template is compiled on its second
+# execution (COMPILE_AFTER); M2K_TEMPLATE_INTERPRET=1 keeps the interpreter,
+# and tests/test_gotemplate_compiled.py checks the two agree on every packaged
+# template and the template test corpus.
+
+def _c_nodes(nodes):
+    fns = tuple(_c_node(n) for n in nodes)
+    declares = any(isinstance(n, _Action) and n.pipe.decls for n in nodes)
+
+    if not declares:  # nothing at this level adds to the scope
+        def run(st, dot, scope, out):
+            for f in fns:
+                f(st, dot, scope, out)
+        return run
+
+    def run_scoped(st, dot, scope, out):
+        mark = len(scope)
+        try:
+            for f in fns:
+                f(st, dot, scope, out)
+        finally:
+            del scope[mark:]
+    return run_scoped
+
+
+def _c_node(n):
+    if isinstance(n, _Text):
+        text = n.text
+
+        def text_node(st, dot, scope, out):
+            out.append(text)
+        return text_node
+    if isinstance(n, _Action):
+        pipe = _c_pipe(n.pipe, True)
+        if n.pipe.decls:
+            def declare_node(st, dot, scope, out):
+                pipe(st, dot, scope)
+            return declare_node
+
+        def action_node(st, dot, scope, out):
+            out.append(go_sprint(pipe(st, dot, scope)))
+        return action_node
+    if isinstance(n, _If):
+        return _c_control(n)
+    if isinstance(n, _TemplateCall):
+        name = n.name
+        pipe = _c_pipe(n.pipe, True) if n.pipe else None
+
+        def call_node(st, dot, scope, out):
+            body = st.tmpl.compiled_define(name)
+            if body is None:
+                raise TemplateError(go_sprintf("template %q not defined", [name]))
+            newdot = pipe(st, dot, scope) if pipe is not None else None
+            body(st, newdot, [("$", newdot)], out)
+        return call_node
+    if isinstance(n, _Break):
+        def break_node(st, dot, scope, out):
+            raise _BreakSignal()
+        return break_node
+    if isinstance(n, _Continue):
+        def continue_node(st, dot, scope, out):
+            raise _ContinueSignal()
+        return continue_node
+    raise TypeError("unknown template node %r" % (n,))
+
+
+def _c_control(node):
+    body = _c_nodes(node.body)
+    else_body = None if node.else_body is None else _c_nodes(node.else_body)
+    if node.kind == "range":
+        pipe = _c_pipe(node.pipe, False)
+        decls = tuple(node.pipe.decls)
+
+        def range_node(st, dot, scope, out):
+            mark = len(scope)
+            try:
+                val = pipe(st, dot, scope)
+                items = []
+                if isinstance(val, dict):
+                    items = [(k, val[k]) for k in sorted(val.keys(), key=_sort_key)]
+                elif isinstance(val, (list, tuple, str, bytes)):
+                    if isinstance(val, str):
+                        raise TemplateError("range can't iterate over %s" % val)
+                    items = list(enumerate(val))
+                elif isinstance(val, int) and not isinstance(val, bool):
+                    items = [(i, i) for i in range(val)]
+                elif val is None or val is NO_VALUE:
+                    items = []
+                else:
+                    raise TemplateError("range can't iterate over %s" % go_sprint(val))
+                if not items:
+                    if else_body is not None:
+                        else_body(st, dot, scope, out)
+                    return
+                for k, v in items:
+                    inner = len(scope)
+                    if len(decls) == 1:
+                        scope.append((decls[0], v))
+                    elif len(decls) == 2:
+                        scope.append((decls[0], k))
+                        scope.append((decls[1], v))
+                    try:
+                        body(st, v, scope, out)
+                    except _BreakSignal:
+                        break
+                    except _ContinueSignal:
+                        pass
+                    finally:
+                        del scope[inner:]
+            finally:
+                del scope[mark:]
+        return range_node
+    pipe = _c_pipe(node.pipe, True)
+    is_with = node.kind == "with"
+
+    def cond_node(st, dot, scope, out):
+        mark = len(scope)
+        try:
+            val = pipe(st, dot, scope)
+            if _truth(val):
+                body(st, val if is_with else dot, scope, out)
+            elif else_body is not None:
+                else_body(st, dot, scope, out)
+        finally:
+            del scope[mark:]
+    return cond_node
+
+
+def _c_pipe(pipe, declare):
+    """fn(st, dot, scope) -> value of the pipeline (declaring or assigning its
+    variables when ``declare``, as eval_pipe does)."""
+    cmds = [_c_cmd(c, i > 0) for i, c in enumerate(pipe.cmds)]
+    decls = tuple(pipe.decls) if declare else ()
+    if not decls and len(cmds) == 1:
+        only = cmds[0]
+
+        def single(st, dot, scope):
+            return only(st, dot, scope, None)
+        return single
+    is_assign = pipe.is_assign
+
+    def run(st, dot, scope):
+        val = None
+        for c in cmds:
+            val = c(st, dot, scope, val)
+        if decls:
+            if is_assign:
+                for name in decls:
+                    for idx in range(len(scope) - 1, -1, -1):
+                        if scope[idx][0] == name:
+                            scope[idx] = (name, val)
+                            break
+                    else:
+                        raise TemplateError("undefined variable: %s" % name)
+            else:
+                scope.append((decls[0], val))
+        return val
+    return run
+
+
+def _c_cmd(cmd, has_final):
+    """fn(st, dot, scope, final) of one command of a pipeline."""
+    first = cmd[0]
+    if first[0] == "ident":
+        name = first[1]
+        args = tuple(_c_arg(a) for a in cmd[1:])
+        wrap = name not in ("and", "or")
+
+        def call(st, dot, scope, final):
+            fn = st.funcs.get(name)
+            if fn is None:
+                raise TemplateError('function "%s" not defined' % name)
+            vals = [a(st, dot, scope) for a in args]
+            if has_final:
+                vals.append(final)
+            if not wrap:
+                return fn(*vals)
+            try:
+                return fn(*vals)
+            except TemplateError:
+                raise
+            except Exception as e:  # noqa: BLE001
+                raise TemplateError("error calling %s: %s" % (name, e))
+        return call
+    arg = _c_arg(first)
+    if first[0] == "field" and (len(cmd) > 1 or has_final):
+        message = "can't give argument to non-function %s" % ".".join(first[1])
+
+        def refuse(st, dot, scope, final):
+            raise TemplateError(message)
+        return refuse
+
+    def value(st, dot, scope, final):
+        return arg(st, dot, scope)
+    return value
+
+
+def _c_arg(a):
+    kind = a[0]
+    fields = _State.fields
+    if kind == "lit":
+        v = a[1]
+        return lambda st, dot, scope: v
+    if kind == "nil":
+        return lambda st, dot, scope: None
+    if kind == "dot":
+        return lambda st, dot, scope: dot
+    if kind == "field":
+        names = a[1]
+        return lambda st, dot, scope: fields(dot, names)
+    if kind == "var":
+        name, names = a[1], a[2]
+
+        def var(st, dot, scope):
+            for idx in range(len(scope) - 1, -1, -1):
+                if scope[idx][0] == name:
+                    return fields(scope[idx][1], names)
+            raise TemplateError("undefined variable: %s" % name)
+        return var
+    if kind == "pipe":
+        sub = _c_pipe(a[1], False)
+        names = a[2]
+        return lambda st, dot, scope: fields(sub(st, dot, scope), names)
+    if kind == "ident":
+        name = a[1]
+
+        def ident(st, dot, scope):
+            fn = st.funcs.get(name)
+            if fn is None:
+                raise TemplateError('function "%s" not defined' % name)
+            return fn()
+        return ident
+
+    def bad(st, dot, scope):
+        raise TemplateError("bad operand")
+    return bad
 
 
 # ---------------------------------------------------------------------------

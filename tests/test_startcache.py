@@ -159,6 +159,6 @@ def test_every_lazy_pattern_of_the_package_is_cached():
             continue
         importlib.import_module(m.name)
     _, regexes = startcache_build.collect()
-    lazies = [o for o in gc.get_objects() if isinstance(o, lazyre.LazyPattern)]
+    lazies = [o for o in gc.get_objects() if type(o) is lazyre.LazyPattern]
     assert len(lazies) >= 20
     assert [o._args for o in lazies if (o._args[0], int(o._args[1])) not in regexes] == []
