@@ -189,6 +189,34 @@ def required_literals(pattern):
     prose; almost none of them match each other)."""
     if "|" in pattern or "(?" in pattern:
         return None
+    if _SIMPLE_PATTERN_OUT.isdisjoint(pattern):
+        return _simple_required_literals(pattern)
+    return _required_literals_scan(pattern)
+
+
+# patterns made only of literal characters, "." "^" "$" "+" and the "*" / "?"
+# quantifiers (most question texts) are split with str methods
+_SIMPLE_PATTERN_OUT = frozenset("\\[](){}|\x00\x01")
+_TO_FLUSH = str.maketrans(".^$+", "\x00\x00\x00\x00")
+_TO_QUANT = str.maketrans("*?", "\x01\x01")
+
+
+def _simple_required_literals(pattern):
+    """:func:`required_literals` of a pattern without escapes, classes,
+    groups, repeat counts or alternation: runs between "." "^" "$" "+", with a
+    character followed by "*" or "?" dropped (it is optional)."""
+    out = []
+    for seg in pattern.translate(_TO_FLUSH).split("\x00"):
+        parts = seg.translate(_TO_QUANT).split("\x01")
+        for p in parts[:-1]:
+            if len(p) > 1:
+                out.append(p[:-1])
+        if parts[-1]:
+            out.append(parts[-1])
+    return out
+
+
+def _required_literals_scan(pattern):
     out, seg, depth, i, n = [], [], 0, 0, len(pattern)
 
     def flush():

@@ -111,3 +111,12 @@ def test_desc_index_lookup_strategies_agree(listed, desc):
         warnings.simplefilter("ignore")
         linear = next((i for i, cp in enumerate(problems) if cp.matches(p)), -1)
         assert idx.first_match(p) == linear
+
+
+@settings(max_examples=500, deadline=None)
+@given(st.text(alphabet="ab .^$+*?:é\n", max_size=20))
+def test_simple_pattern_fast_path_equals_the_scan(pattern):
+    """Patterns of literals, "." "^" "$" "+" and "*" / "?" take the str-method
+    split; it gives what the character scan gives."""
+    assert qa._simple_required_literals(pattern) == qa._required_literals_scan(pattern)
+    assert qa.required_literals(pattern) == qa._required_literals_scan(pattern)
