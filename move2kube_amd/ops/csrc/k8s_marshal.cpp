@@ -45,6 +45,8 @@ struct Field {
 
 struct Struct {
   std::string name;
+  PyObject* spec = nullptr;   // its fields as schema.py handed them (compiled on first use)
+  bool compiled = false;
   std::vector<Field> fields;
   PyObject* keyed = nullptr;  // json name -> field index (PyLong)
   std::vector<int> inlines;   // struct indices
@@ -73,6 +75,7 @@ static void discard_schema() {
   for (Type& t : g->types) Py_XDECREF(t.name);
   for (Struct& s : g->structs) {
     for (Field& f : s.fields) Py_XDECREF(f.jname);
+    Py_XDECREF(s.spec);
     Py_XDECREF(s.keyed);
     Py_XDECREF(s.base);
     Py_XDECREF(s.empty);
@@ -138,9 +141,13 @@ static PyObject* marshal_struct(PyObject* d, int strct);
 // the marshalled empty struct of `strct` (borrowed; cached)
 static PyObject* empty_struct(int strct);
 
+// compiles a struct's field table on its first use (false + exception on error)
+static bool ensure(int strct);
+
 static PyObject* base_of(int strct) {
   Struct& s = g->structs[strct];
   if (s.base) return s.base;
+  if (!ensure(strct)) return nullptr;
   PyObject* base = PyDict_New();
   if (!base) return nullptr;
   for (const Field& f : s.fields) {
@@ -217,7 +224,7 @@ static PyObject* fallback(PyObject* v, int type) {
 
 static PyObject* marshal_fields(PyObject* d, int strct) {
   Struct& s = g->structs[strct];
-  PyObject* base = base_of(strct);
+  PyObject* base = base_of(strct);  // compiles the struct on first use
   if (!base) return nullptr;
   PyObject* out = PyDict_Copy(base);
   if (!out) return nullptr;
@@ -277,7 +284,7 @@ static PyObject* marshal_struct(PyObject* d, int strct) {
 }
 
 static PyObject* marshal_value(PyObject* v, int type) {
-  const Type& t = g->types[type];
+  const Type t = g->types[type];  // a copy: compiling a struct on first use may grow g->types
   switch (t.kind) {
     case K_IDENT:
       Py_INCREF(v);
@@ -432,6 +439,92 @@ static bool field_specs(PyObject* fields, std::vector<FieldSpec>& out) {
   return true;
 }
 
+static bool check_inline(const std::string& ftype) {
+  if (g->struct_index.count(ftype)) return true;
+  PyErr_Format(PyExc_ValueError, "inline type %s is not a struct", ftype.c_str());
+  return false;
+}
+
+// What compiling ``fields`` would refuse, without compiling it.
+static bool check_spec(PyObject* fields) {
+  if (PyUnicode_Check(fields)) {
+    Py_ssize_t n = 0;
+    const char* c = PyUnicode_AsUTF8AndSize(fields, &n);
+    if (!c) return false;
+    size_t i = 0, len = (size_t)n;
+    while (i < len) {
+      while (i < len && is_space(c[i])) ++i;
+      size_t j = i;
+      while (j < len && !is_space(c[j])) ++j;
+      if (j == i) break;
+      std::string item(c + i, j - i);
+      i = j;
+      if (item.size() >= 2 && item.compare(item.size() - 2, 2, ",o") == 0) item.resize(item.size() - 2);
+      size_t colon = item.find(':');
+      if (colon == std::string::npos) {
+        PyErr_Format(PyExc_ValueError, "field %s has no type", item.c_str());
+        return false;
+      }
+      if (item.compare(0, colon, "inline") == 0 && colon == 6 && !check_inline(item.substr(colon + 1))) return false;
+    }
+    return true;
+  }
+  std::vector<FieldSpec> specs;
+  if (!field_specs(fields, specs)) return false;
+  for (const FieldSpec& f : specs)
+    if (f.jname == "inline" && !check_inline(f.ftype)) return false;
+  return true;
+}
+
+static bool ensure(int strct) {
+  Struct& s = g->structs[strct];
+  if (s.compiled) return true;
+  // a compile that fails part-way leaves the struct as it was: uncompiled
+  auto fail = [&s]() {
+    for (Field& f : s.fields) Py_XDECREF(f.jname);
+    s.fields.clear();
+    s.inlines.clear();
+    if (s.keyed) PyDict_Clear(s.keyed);
+    return false;
+  };
+  std::vector<FieldSpec> specs;
+  s.keyed = s.keyed ? s.keyed : PyDict_New();
+  if (!s.keyed || !field_specs(s.spec, specs)) return fail();
+  for (FieldSpec& spec : specs) {
+    const std::string &jname = spec.jname, &ftype = spec.ftype;
+    const bool omit = spec.omit;
+    PyObject* jn = PyUnicode_FromStringAndSize(jname.data(), (Py_ssize_t)jname.size());
+    if (!jn) return fail();
+    Field f;
+    f.jname = jn;  // owns the reference
+    f.omit = omit;
+    f.inline_ = jname == "inline";
+    f.type = compile_type(ftype);
+    f.empty = omit ? empty_kind(ftype) : E_NEVER;
+    f.absent = f.inline_ ? A_SKIP : absent_kind(ftype, omit);
+    if (f.inline_) {
+      auto si = g->struct_index.find(ftype);
+      if (si == g->struct_index.end()) {  // check_spec refused this at init
+        Py_DECREF(jn);
+        PyErr_Format(PyExc_ValueError, "inline type %s is not a struct", ftype.c_str());
+        return fail();
+      }
+      s.inlines.push_back(si->second);
+    } else {
+      PyObject* idx = PyLong_FromSsize_t((Py_ssize_t)s.fields.size());
+      int rc = idx ? PyDict_SetItem(s.keyed, jn, idx) : -1;
+      Py_XDECREF(idx);
+      if (rc < 0) {
+        Py_DECREF(jn);
+        return fail();
+      }
+    }
+    s.fields.push_back(f);
+  }
+  s.compiled = true;
+  return true;
+}
+
 }  // namespace m2kschema
 
 using namespace m2kschema;
@@ -467,51 +560,19 @@ extern "C" PyObject* m2k_schema_init(PyObject* structs, PyObject* fb) {
     g->struct_index[s.name] = (int)g->structs.size();
     g->structs.push_back(std::move(s));
   }
+  // keep each struct's spec and check what a compile would refuse: a field
+  // without a type, an inline field naming no struct.  The field tables are
+  // compiled per struct on first use (ensure): a run marshals a few dozen of
+  // the table's structs.
   pos = 0;
   int ix = 0;
   while (PyDict_Next(structs, &pos, &name, &fields)) {
     Struct& s = g->structs[ix++];
-    s.keyed = PyDict_New();
-    std::vector<FieldSpec> specs;
-    if (!s.keyed || !field_specs(fields, specs)) {
+    Py_INCREF(fields);
+    s.spec = fields;
+    if (!check_spec(fields)) {
       discard_schema();
       return nullptr;
-    }
-    for (FieldSpec& spec : specs) {
-      const std::string &jname = spec.jname, &ftype = spec.ftype;
-      const bool omit = spec.omit;
-      PyObject* jn = PyUnicode_FromStringAndSize(jname.data(), (Py_ssize_t)jname.size());
-      if (!jn) {
-        discard_schema();
-        return nullptr;
-      }
-      Field f;
-      f.jname = jn;  // owns the reference
-      f.omit = omit;
-      f.inline_ = jname == "inline";
-      f.type = compile_type(ftype);
-      f.empty = omit ? empty_kind(ftype) : E_NEVER;
-      f.absent = f.inline_ ? A_SKIP : absent_kind(ftype, omit);
-      if (f.inline_) {
-        auto si = g->struct_index.find(ftype);
-        if (si == g->struct_index.end()) {
-          Py_DECREF(jn);
-          PyErr_Format(PyExc_ValueError, "inline type %s is not a struct", ftype.c_str());
-          discard_schema();
-          return nullptr;
-        }
-        s.inlines.push_back(si->second);
-      } else {
-        PyObject* idx = PyLong_FromSsize_t((Py_ssize_t)s.fields.size());
-        int rc = idx ? PyDict_SetItem(s.keyed, jn, idx) : -1;
-        Py_XDECREF(idx);
-        if (rc < 0) {
-          Py_DECREF(jn);
-          discard_schema();
-          return nullptr;
-        }
-      }
-      s.fields.push_back(f);
     }
   }
   g->ready = true;
