@@ -341,7 +341,10 @@ def test_template_execution_failure_is_reported_with_its_data(capsys):
     log.set_verbose(False)
     with pytest.raises(TemplateError) as ei:
         common.get_string_from_template("FROM {{.port.x}}", {"port": 8080.0, "app": "a b", "n": None})
-    assert str(ei.value) == "can't evaluate field x in type float64"
+    # exec.go evalField: the receiver is a map element, of type interface {};
+    # the error carries Go's location (the chain's second field) and context
+    assert str(ei.value) == ('template: :1:12: executing "" at <.port.x>: '
+                             "can't evaluate field x in type interface {}")
     assert logparse.logged(capsys.readouterr().err, 'Unable to translate template "FROM {{.port.x}}" to string '
                            "using the data map[app:a b n:<nil> port:8080]", "warning")
 
