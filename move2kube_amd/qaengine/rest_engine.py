@@ -104,6 +104,29 @@ def _html_escape(s):
     return (s.replace("&", "&amp;").replace("<", "&lt;").replace(">", "&gt;")
             .replace('"', "&#34;").replace("'", "&#39;"))
 
+
+MAX_POST_HANDLER_READ_BYTES = 256 << 10   # net/http server.go: maxPostHandlerReadBytes
+_ERROR_HEADERS = "\r\nContent-Type: text/plain; charset=utf-8\r\nConnection: close\r\n\r\n"
+
+
+class _BadBody(Exception):
+    """A request body net/http cannot read (corrupt chunked encoding, EOF)."""
+
+
+def _parse_content_length(values):
+    """net/http transfer.go fixLength / parseContentLength: the length, or
+    None when Go answers 400 (differing duplicates, not a non-negative int)."""
+    first = values[0].strip(" \t")
+    if any(v.strip(" \t") != first for v in values[1:]):
+        return None
+    if first == "":
+        return 0
+    digits = first[1:] if first[:1] in "+-" else first
+    if not digits.isdigit() or not digits.isascii():
+        return None
+    n = int(first)
+    return n if 0 <= n < 1 << 63 else None
+
 class HTTPRESTEngine(Engine):
     go_type = "*qaengine.HTTPRESTEngine"
     interactive = True  # may block on a person: the write cache is flushed first
@@ -137,11 +160,96 @@ class HTTPRESTEngine(Engine):
             def log_message(self, fmt, *args):
                 log.debug("qa-http: " + fmt, *args)
 
+            # -- the request body, as net/http reads and discards it ------------
+            def _body_setup(self):
+                """transfer.go readTransfer: chunked (one Transfer-Encoding,
+                "chunked", HTTP/1.1 only) or a Content-Length; False after
+                answering a request net/http refuses before any handler runs."""
+                self._chunked = False
+                self._remaining = 0
+                self._body_done = False
+                te = self.headers.get_all("Transfer-Encoding") or []
+                if te and self.request_version != "HTTP/1.0":
+                    if len(te) != 1 or te[0].strip(" \t").lower() != "chunked":
+                        self._refuse("501 Not Implemented", "Unsupported transfer encoding")
+                        return False
+                    self._chunked = True
+                    return True
+                cls = self.headers.get_all("Content-Length") or []
+                if cls:
+                    n = _parse_content_length(cls)
+                    if n is None:
+                        self._refuse("400 Bad Request", "400 Bad Request")
+                        return False
+                    self._remaining = n
+                self._body_done = self._remaining == 0
+                return True
+
+            def _refuse(self, status, body):
+                """server.go: the reply to a request readRequest rejected."""
+                self.close_connection = True
+                self.wfile.write(("HTTP/1.1 " + status + _ERROR_HEADERS + body).encode("latin-1"))
+                self.wfile.flush()
+
+            def _read_chunk_line(self):
+                line = self.rfile.readline(4097)
+                if not line.endswith(b"\n"):
+                    raise _BadBody("unexpected EOF" if not line else "header line too long")
+                return line.rstrip(b"\r\n")
+
+            def _read_body(self, limit=None):
+                """The body's bytes (at most ``limit``+1 of them when a limit
+                is given); raises _BadBody when it cannot be read."""
+                out = bytearray()
+                if not self._chunked:
+                    n = self._remaining if limit is None else min(self._remaining, limit + 1)
+                    data = self.rfile.read(n) if n else b""
+                    self._remaining -= len(data)
+                    if len(data) < n:
+                        raise _BadBody("unexpected EOF")
+                    self._body_done = self._remaining == 0
+                    return bytes(data)
+                while True:
+                    if limit is not None and len(out) > limit:
+                        return bytes(out)
+                    size_line = self._read_chunk_line().split(b";", 1)[0].strip()
+                    try:
+                        size = int(size_line, 16)
+                    except ValueError:
+                        raise _BadBody("invalid byte in chunk length")
+                    if size == 0:
+                        while self._read_chunk_line():
+                            pass   # trailers
+                        self._body_done = True
+                        return bytes(out)
+                    chunk = self.rfile.read(size)
+                    if len(chunk) < size or self.rfile.read(2) != b"\r\n":
+                        raise _BadBody("malformed chunked encoding")
+                    out += chunk
+
+            def _discard_body(self):
+                """server.go chunkWriter.writeHeader: an unread body is read
+                and thrown away (up to maxPostHandlerReadBytes) so the
+                connection can be reused; a bigger or unreadable one closes it."""
+                if self._body_done:
+                    return
+                if not self._chunked and self._remaining >= MAX_POST_HANDLER_READ_BYTES:
+                    self.close_connection = True
+                    return
+                try:
+                    self._read_body(MAX_POST_HANDLER_READ_BYTES)
+                except (_BadBody, OSError):
+                    self.close_connection = True
+                    return
+                if not self._body_done:
+                    self.close_connection = True
+
             def _go_reply(self, code, body=b"", headers=()):
                 """A response laid out as net/http's chunkWriter writes it:
                 the handler's own headers sorted by name, then Date,
                 Content-Length, a sniffed Content-Type (only for a non-empty
                 body without one) and Connection."""
+                self._discard_body()
                 http11 = self.request_version != "HTTP/1.0"
                 lines = ["%s %d %s\r\n" % ("HTTP/1.1" if http11 else "HTTP/1.0", code, _STATUS_TEXT[code])]
                 for k, v in sorted(headers):
@@ -169,6 +277,8 @@ class HTTPRESTEngine(Engine):
                 """http.DefaultServeMux (clean-path redirect) in front of the
                 gorilla/mux router: a known path with another method is 405
                 with an empty body, an unknown path 404."""
+                if not self._body_setup():
+                    return
                 raw_path, _, query = self.path.partition("?")
                 path = unquote(raw_path)
                 clean = _clean_path(path)
@@ -201,9 +311,13 @@ class HTTPRESTEngine(Engine):
                 self._go_reply(200, fastjson.go_encode(prob.to_json()))
 
             def _solution(self):
-                n = int(self.headers.get("Content-Length") or 0)
-                body = self.rfile.read(max(0, n))
                 errs = []
+                try:
+                    body = self._read_body()   # ioutil.ReadAll(r.Body)
+                except (_BadBody, OSError) as e:
+                    self.close_connection = True
+                    body = b""
+                    log.debug("qa-http: reading the request body: %s", e)
                 try:
                     sol = _string_slice(fastjson.loads(body))
                 except _PartialSlice as e:

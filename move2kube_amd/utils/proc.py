@@ -120,26 +120,39 @@ def run(argv, cwd=None, stdout=PIPE, stderr=DEVNULL, timeout=None):
 def run_many(argvs, parallel=None, cwd=None, stdout=PIPE, stderr=DEVNULL, timeout=None):
     """``[run(a, ...) for a in argvs]`` with up to ``parallel`` children alive
     at once (all of them by default); a raised error is returned in its slot.
-    No threads: the children run concurrently and are collected in order,
-    each against its own deadline."""
-    import time
+    Each child is waited for on its own thread from the moment it starts (the
+    native wait releases the GIL), so every live child's pipes drain at once,
+    its deadline counts from its start, and a slot is refilled as soon as any
+    child exits."""
+    import queue
+    import threading
     n = len(argvs)
     if parallel is None or parallel < 1:
         parallel = n
     out = [None] * n
-    live = []  # (index, child, start)
+    done = queue.SimpleQueue()
+
+    def waiter(i, c):
+        try:
+            r = c.wait(timeout)
+            done.put((i, _timeout_error(r, timeout) if r.timed_out else r))
+        except BaseException as e:  # noqa: BLE001 - reported in the child's slot
+            done.put((i, e))
+
+    live = 0
     nxt = 0
     while nxt < n or live:
-        while nxt < n and len(live) < parallel:
+        while nxt < n and live < parallel:
             try:
-                live.append((nxt, spawn(argvs[nxt], cwd=cwd, stdout=stdout, stderr=stderr), time.monotonic()))
+                c = spawn(argvs[nxt], cwd=cwd, stdout=stdout, stderr=stderr)
             except OSError as e:
                 out[nxt] = e
+            else:
+                threading.Thread(target=waiter, args=(nxt, c), name="m2k-proc-wait", daemon=True).start()
+                live += 1
             nxt += 1
-        if not live:
-            continue
-        i, c, t0 = live.pop(0)
-        left = None if timeout is None else max(0.001, timeout - (time.monotonic() - t0))
-        r = c.wait(left)
-        out[i] = _timeout_error(r, timeout) if r.timed_out else r
+        if live:
+            i, r = done.get()
+            out[i] = r
+            live -= 1
     return out

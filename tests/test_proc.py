@@ -103,6 +103,21 @@ def test_bounded_parallelism(mode, tmp_path):
     assert [r.returncode for r in out] == [0, 0, 0, 0]
 
 
+def test_run_many_drains_every_child_and_refills_slots(mode):
+    # a later child writing more than a pipe holds is not blocked behind a
+    # slow earlier one (its pipe drains while the first is waited for) ...
+    big = [sys.executable, "-c", "import sys; sys.stdout.write('x' * 1000000)"]
+    out = proc.run_many([["/bin/sh", "-c", "sleep 1; echo slow"], big], stdout=proc.PIPE, timeout=5)
+    assert out[0].stdout == b"slow\n" and len(out[1].stdout) == 1000000
+    # ... and with two slots, the quick children go through the slot the
+    # first quick one frees while the slow one still runs
+    cmds = [["/bin/sh", "-c", "sleep 1.2; echo a"]] + [["/bin/sh", "-c", "sleep 0.3; echo %d" % i] for i in range(3)]
+    t = time.monotonic()
+    out = proc.run_many(cmds, parallel=2, stdout=proc.PIPE)
+    assert time.monotonic() - t < 1.9          # serial head-of-line waiting would take 1.2 + 0.6 + ...
+    assert [r.stdout for r in out] == [b"a\n", b"0\n", b"1\n", b"2\n"]
+
+
 def test_cold_tool_paths_do_not_import_subprocess(tmp_path):
     """The CNB podman probe, operator-sdk and the collectors run their tools
     without importing subprocess (its import is the cost this module avoids)."""

@@ -4,6 +4,8 @@ import io
 
 import pytest
 import json
+import re
+import socket
 import threading
 import urllib.error
 import urllib.request
@@ -179,6 +181,85 @@ def test_rest_engine_wire_bytes_follow_net_http():
                     % (len(sol), sol)) == b"HTTP/1.1 200 OK\r\nDate: X\r\nContent-Length: 0\r\n\r\n"
         t.join(20)
         assert got["ans"] == "é"
+    finally:
+        e.stop()
+
+
+def _read_response(c):
+    """One response off a keep-alive connection: (head, body)."""
+    data = b""
+    while b"\r\n\r\n" not in data:
+        chunk = c.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    head, _, body = data.partition(b"\r\n\r\n")
+    m = re.search(rb"Content-Length: (\d+)", head)
+    n = int(m.group(1)) if m else 0
+    while len(body) < n:
+        body += c.recv(65536)
+    return re.sub(rb"Date: [^\r]+", b"Date: X", head), body
+
+
+def test_rest_engine_keep_alive_drains_unread_bodies():
+    """net/http reads and discards a body the handler left unread before it
+    answers (server.go chunkWriter.writeHeader, up to maxPostHandlerReadBytes),
+    so the next request on the connection parses; a chunked solution body is
+    read as ioutil.ReadAll reads it; a bad Content-Length or an unsupported
+    Transfer-Encoding is refused before any handler (server.go readRequest)."""
+    e = HTTPRESTEngine(0, "127.0.0.1")
+    qaengine.reset()
+    qaengine.add_engine(e)
+    got = {}
+
+    def ask():
+        p = qa.new_input_problem("Name?", [], "d")
+        got["ans"] = qaengine.fetch_answer(p).get_string_answer()
+
+    t = threading.Thread(target=ask, daemon=True)
+    t.start()
+    try:
+        with socket.create_connection(("127.0.0.1", e.port), timeout=20) as c:
+            # a POST with a body to an unknown route, a chunked POST to the
+            # GET route, then a GET: all on one connection
+            c.sendall(b"POST /nope HTTP/1.1\r\nHost: x\r\nContent-Length: 5\r\n\r\nhello")
+            head, body = _read_response(c)
+            assert head.startswith(b"HTTP/1.1 404 Not Found") and body == b"404 page not found\n"
+            assert b"Connection: close" not in head
+            c.sendall(b"POST /problems/current HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+                      b"3\r\nabc\r\n0\r\n\r\n")
+            head, body = _read_response(c)
+            assert head.startswith(b"HTTP/1.1 405 Method Not Allowed") and b"Connection: close" not in head
+            c.sendall(b"GET /problems/current HTTP/1.1\r\nHost: x\r\n\r\n")
+            head, body = _read_response(c)
+            assert head.startswith(b"HTTP/1.1 200 OK") and json.loads(body)["description"] == "Name?"
+            # the answer as a chunked body, on the same connection
+            c.sendall(b"POST /problems/current/solution HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n"
+                      b"\r\n4\r\n[\"na\r\n4;ext=1\r\nme\"]\r\n0\r\nX-Trailer: 1\r\n\r\n")
+            head, body = _read_response(c)
+            assert head == b"HTTP/1.1 200 OK\r\nDate: X\r\nContent-Length: 0"
+        t.join(20)
+        assert got["ans"] == "name"
+        for bad, want in ((b"Content-Length: x1", b"400 Bad Request"),
+                          (b"Content-Length: -1", b"400 Bad Request"),
+                          (b"Content-Length: 1\r\nContent-Length: 2", b"400 Bad Request"),
+                          (b"Transfer-Encoding: gzip", b"501 Not Implemented")):
+            with socket.create_connection(("127.0.0.1", e.port), timeout=20) as c:
+                c.sendall(b"POST /problems/current/solution HTTP/1.1\r\nHost: x\r\n" + bad + b"\r\n\r\n")
+                data = b""
+                while True:
+                    chunk = c.recv(65536)
+                    if not chunk:
+                        break
+                    data += chunk
+            text = b"400 Bad Request" if want.startswith(b"400") else b"Unsupported transfer encoding"
+            assert data == (b"HTTP/1.1 " + want + b"\r\nContent-Type: text/plain; charset=utf-8\r\n"
+                            b"Connection: close\r\n\r\n" + text)
+        # a body too big to discard closes the connection after the reply
+        with socket.create_connection(("127.0.0.1", e.port), timeout=20) as c:
+            c.sendall(b"POST /nope HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n" % (1 << 20))
+            head, body = _read_response(c)
+            assert head.startswith(b"HTTP/1.1 404") and b"Connection: close" in head
     finally:
         e.stop()
 
