@@ -392,6 +392,23 @@ class ContainerRuntimeProvider:
             except OSError as e:
                 children.append(e)
         self._pending = (hello, todo, children)
+        _register_prefetch_reaper()
+
+    def abandon_prefetch(self):
+        """Kill and reap probes started by :meth:`start_prefetch` that nobody
+        collected (the command ended before the planner needed them)."""
+        pending, self._pending = self._pending, None
+        if pending is None:
+            return
+        import signal
+        for c in pending[2]:
+            if isinstance(c, BaseException):
+                continue
+            try:
+                os.kill(c.pid, signal.SIGKILL)
+            except OSError:
+                pass
+            c.wait()
 
     def _finish_prefetch(self):
         pending, self._pending = self._pending, None
@@ -703,6 +720,26 @@ def reset_providers():
     for p in old or ():
         if isinstance(p, ContainerRuntimeProvider):
             p._finish_prefetch()  # reap probes nobody asked for
+
+
+_reaper_registered = []
+
+
+def _register_prefetch_reaper():
+    """At interpreter exit (the CLI runs the atexit handlers before its
+    ``os._exit``), kill the prefetch probes still running: the reference
+    starts none of them unless the planner reaches the provider."""
+    if _reaper_registered:
+        return
+    _reaper_registered.append(True)
+    import atexit
+    atexit.register(_reap_prefetch)
+
+
+def _reap_prefetch():
+    for p in _providers or ():
+        if isinstance(p, ContainerRuntimeProvider):
+            p.abandon_prefetch()
 
 
 def start_runtime_prefetch(builders):

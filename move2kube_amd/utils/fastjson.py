@@ -90,8 +90,9 @@ def _go_string(s):
     """``encodeState.string`` (Go 1.15): compact escapes only for quote,
     backslash, newline, carriage return and tab, ``\\u00XX`` for the other
     control characters (``\\b`` and ``\\f`` included), ``<``, ``>``, ``&`` and
-    U+2028/U+2029 as ``\\uXXXX``, every other character raw UTF-8; a lone
-    surrogate (undecodable input) becomes U+FFFD."""
+    U+2028/U+2029 as ``\\uXXXX``, every other character raw UTF-8; a byte
+    that was not UTF-8 (surrogateescape) is written as the escape text
+    ``\\ufffd``."""
     out = []
     for ch in s:
         e = _GO_ENC_ESC.get(ch)
@@ -100,10 +101,28 @@ def _go_string(s):
         elif ch < " ":
             out.append("\\u%04x" % ord(ch))
         elif "\ud800" <= ch <= "\udfff":
-            out.append("\ufffd")
+            out.append("\\ufffd")
         else:
             out.append(ch)
     return '"' + "".join(out) + '"'
+
+
+class UnsupportedValueError(ValueError):
+    """encoding/json UnsupportedValueError (NaN and infinities)."""
+
+
+def _go_float(f):
+    """floatEncoder.encode (Go 1.15, 64 bits): the shortest 'f' form, or the
+    shortest 'e' form below 1e-6 and from 1e21 on, with e-09 written e-9."""
+    from .gofmt import format_float
+    if f != f or f in (float("inf"), float("-inf")):
+        raise UnsupportedValueError("json: unsupported value: " + format_float(f, "g", -1))
+    a = abs(f)
+    fmt = "e" if a != 0 and (a < 1e-6 or a >= 1e21) else "f"
+    b = format_float(f, fmt, -1)
+    if fmt == "e" and len(b) >= 4 and b[-4] == "e" and b[-3] == "-" and b[-2] == "0":
+        b = b[:-2] + b[-1]
+    return b
 
 
 def _go_value(v, out):
@@ -116,7 +135,7 @@ def _go_value(v, out):
     elif isinstance(v, int):
         out.append(str(v))
     elif isinstance(v, float):
-        out.append(repr(v) if v != int(v) or abs(v) >= 1e21 else str(int(v)))
+        out.append(_go_float(v))
     elif isinstance(v, str):
         out.append(_go_string(v))
     elif isinstance(v, dict):

@@ -412,6 +412,37 @@ def test_runtime_probes_start_in_the_background(monkeypatch, tmp_path):
     providers.reset_providers()
 
 
+def test_unused_runtime_probes_are_killed_at_exit(tmp_path):
+    """A process that started the podman probes and ended before the planner
+    used them kills and reaps them in its atexit handlers (the CLI runs them
+    before its os._exit): no probe outlives the command."""
+    import subprocess
+    import sys
+    import time
+    podman = tmp_path / "bin" / "podman"
+    podman.parent.mkdir()
+    pidfile = tmp_path / "pids"
+    podman.write_text('#!/bin/sh\necho $$ >> %s\nexec sleep 30\n' % pidfile)
+    podman.chmod(0o755)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from move2kube_amd.containerizer.cnb import providers\n"
+            "providers.DOCKER_SOCK = %r\n"
+            "providers.start_runtime_prefetch(['b1', 'b2'])\n"
+            "import time; time.sleep(0.5)\n"
+            "from move2kube_amd import _cli_exit\n"
+            "_cli_exit(0)\n") % (root, str(tmp_path / "no.sock"))
+    env = dict(os.environ, PATH=str(podman.parent) + os.pathsep + "/usr/bin:/bin", M2K_DISABLE_CNB="0")
+    t = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], env=env, timeout=60)
+    assert r.returncode == 0 and time.monotonic() - t < 20
+    pids = [int(x) for x in pidfile.read_text().split()]
+    assert len(pids) == 3   # hello-world and two image checks
+    for pid in pids:
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)
+
+
 def test_no_background_probes_when_the_docker_socket_exists(monkeypatch, tmp_path):
     sock = tmp_path / "docker.sock"
     sock.write_text("")
