@@ -29,6 +29,10 @@ def native_target():
     return os.path.join(HERE, "_m2k_native" + _ext_suffix())
 
 
+def sshkey_target():
+    return os.path.join(HERE, "_m2k_sshkey" + _ext_suffix())
+
+
 def hip_target():
     return os.path.join(HERE, "libm2k_ed_hip.so")
 
@@ -76,6 +80,28 @@ def build_native(force=False, out=None, sanitize=None):
     return out
 
 
+SSHKEY_SOURCES = [os.path.join(CSRC, "sshkey.cpp"), os.path.join(CSRC, "blowfish_pi.h")]
+
+
+def build_sshkey(force=False, out=None, sanitize=None):
+    """Build ``_m2k_sshkey`` (private SSH keys parsed and re-encoded in
+    process, ``csrc/sshkey.cpp``), linked against the system's libcrypto.  A
+    separate extension so that only a command that reads a key maps it."""
+    import pybind11
+    out = out or sshkey_target()
+    if not force and not _stale(out, SSHKEY_SOURCES):
+        return out
+    inc = sysconfig.get_paths()["include"]
+    cxx = os.environ.get("CXX", "g++")
+    opt = (["-O2", "-fvisibility-inlines-hidden", "-ffunction-sections", "-fdata-sections", "-Wl,--gc-sections",
+            "-static-libstdc++", "-static-libgcc", "-Wl,--exclude-libs,ALL", "-s"]
+           if not sanitize else ["-O1", "-g"] + SANITIZERS[sanitize])
+    _run([cxx] + opt + ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall",
+                        "-I" + pybind11.get_include(), "-I" + inc, SSHKEY_SOURCES[0], "-o", out + ".tmp", "-lcrypto"])
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def find_hipcc():
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
         if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
@@ -119,6 +145,7 @@ def build_startcache(force=False):
 
 def build_all(force=False):
     outs = [build_native(force)]
+    outs.append(build_sshkey(force))
     outs.append(build_hip(force))
     outs.append(build_bytecode(force))
     outs.append(build_startcache(force))
@@ -133,6 +160,7 @@ def build_report(force=True):
     import time
     report = []
     for name, fn, target in (("_m2k_native (g++, C++17/pybind11)", build_native, native_target()),
+                             ("_m2k_sshkey (g++, C++17/pybind11, libcrypto)", build_sshkey, sshkey_target()),
                              ("libm2k_ed_hip (hipcc --offload-arch=gfx950)", build_hip, hip_target()),
                              ("_bytecode.bin (package bytecode bundle)", build_bytecode,
                               os.path.join(os.path.dirname(HERE), "_bytecode.bin")),

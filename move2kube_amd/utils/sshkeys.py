@@ -2,9 +2,14 @@
 
 Public host keys for github.com, gitlab.com and bitbucket.org are built in;
 the user's ``~/.ssh/known_hosts`` and private keys are only read after a QA
-confirmation.  Private keys are re-encoded to PEM (RSA/ECDSA, the formats
-Tekton's git-init accepts) with ``ssh-keygen``; an encrypted key is decrypted
-with a passphrase asked through a Password problem (never cached).
+confirmation.  Private keys are parsed, decrypted and re-encoded to PEM
+(PKCS#1 RSA / SEC1 EC, what ``x509.MarshalPKCS1PrivateKey`` /
+``MarshalECPrivateKey`` write and Tekton's git-init accepts) in process by the
+native ``_m2k_sshkey`` extension (``ops/csrc/sshkey.cpp``: OpenSSH, legacy
+encrypted PEM, PKCS#1/#8, SEC1), as ``ssh.ParseRawPrivateKey`` does in the
+reference; a key is encrypted when parsing says so, and its passphrase is
+asked through a Password problem (never cached).  Where the extension is not
+built, ``ssh-keygen`` does the re-encoding instead.
 """
 
 import os
@@ -203,13 +208,65 @@ def _is_encrypted(path):
     return p.returncode != 0 and b"incorrect passphrase" in p.stderr
 
 
+def _native():
+    """The in-process converter (``ops/csrc/sshkey.cpp``), or None."""
+    if os.environ.get("M2K_DISABLE_NATIVE"):
+        return None
+    try:
+        from ..ops import _m2k_sshkey as m
+    except ImportError:
+        if os.environ.get("M2K_REQUIRE_NATIVE"):
+            raise
+        return None
+    return m
+
+
+_PEM_OK, _NEEDS_PASSPHRASE, _PARSE_ERROR, _UNKNOWN_TYPE = 0, 1, 2, 3
+
+
 def load_ssh_key(filename):
+    """``loadSSHKey`` (sshkeys.go:191-232): the key file as PKCS#1 RSA or SEC1
+    EC PEM; an encrypted key (``PassphraseMissingError``) asks for its
+    passphrase; other key types are ``Unknown key type [%T]``."""
     from ..models import qa
     from ..qaengine import fetch_answer
     path = os.path.join(_state["key_dir"], filename)
+    m = _native()
+    if m is None:
+        return _load_with_ssh_keygen(path, filename)
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError as e:
+        err = common.go_path_error(e, "open")
+        log.error("Failed to read the private key file at path %s Error: %s", _q(path), _q(str(err)))
+        raise
+    status, text = m.private_key_pem(data, None)
+    if status == _PARSE_ERROR:
+        log.error("Failed to parse the private key file at path %s Error %s", _q(path), _q(text))
+        raise KeyError_(text)
+    if status == _NEEDS_PASSPHRASE:
+        prob = qa.new_password_problem("Enter the password to decrypt the private key %s : " % _q(filename),
+                                       ["Password:"])
+        password = fetch_answer(prob).get_string_answer()
+        status, text = m.private_key_pem(data, password.encode("utf-8", "surrogateescape"))
+        if status == _PARSE_ERROR:
+            log.error("Failed to parse the encrypted private key file at path %s Error %s", _q(path), _q(text))
+            raise KeyError_(text)
+    if status == _UNKNOWN_TYPE:
+        log.error("Unknown key type [%s]", text)
+        raise KeyError_("Unknown key type [%s]" % text)
+    return text
+
+
+def _load_with_ssh_keygen(path, filename):
+    """The fallback without the extension: ``ssh-keygen`` re-encodes the key."""
+    from ..models import qa
+    from ..qaengine import fetch_answer
     passphrase = None
     if _is_encrypted(path):
-        prob = qa.new_password_problem("Enter the password to decrypt the private key %r : " % filename, ["Password:"])
+        prob = qa.new_password_problem("Enter the password to decrypt the private key %s : " % _q(filename),
+                                       ["Password:"])
         passphrase = fetch_answer(prob).get_string_answer()
     return _to_pem(path, passphrase)
 
@@ -228,6 +285,7 @@ def get_ssh_key(domain):
     if name == "NONE":
         log.debug("No key selected for domain %s", domain)
         return "", False
+    log.debug("%s", "Loading the key" + name)   # log.Debug("Loading the key", filename): fmt.Sprint
     try:
         return load_ssh_key(name), True
     except (OSError, ValueError, subprocess.SubprocessError) as e:

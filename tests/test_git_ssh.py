@@ -285,9 +285,15 @@ def test_select_key_through_qa_cache(qa_home, tmp_path):
     assert sshkeys.get_ssh_key("other.example") == ("", False)
 
 
+@pytest.fixture
+def keygen_fallback(monkeypatch):
+    """The path without the native key converter: ssh-keygen re-encodes."""
+    monkeypatch.setattr(sshkeys, "_native", lambda: None)
+
+
 @pytest.mark.skipif(not HAVE_KEYGEN, reason="ssh-keygen not installed")
 @pytest.mark.parametrize("fmt", [None, "PEM"])
-def test_encrypted_key_through_password_problem(qa_home, monkeypatch, fmt):
+def test_encrypted_key_through_password_problem(qa_home, monkeypatch, fmt, keygen_fallback):
     secret = "correct horse battery"
     _keygen(qa_home / ".ssh" / "id_rsa", "rsa", passphrase=secret, fmt=fmt)
     eng = _Answers({"The CI/CD pipeline needs access": ["true"], "These are the files": ["id_rsa"],
@@ -312,14 +318,17 @@ def test_encrypted_key_through_password_problem(qa_home, monkeypatch, fmt):
 
 
 @pytest.mark.skipif(not HAVE_KEYGEN, reason="ssh-keygen not installed")
-def test_wrong_password_keeps_placeholder(qa_home):
+@pytest.mark.parametrize("fallback", [False, True])
+def test_wrong_password_keeps_placeholder(qa_home, monkeypatch, fallback):
+    if fallback:
+        monkeypatch.setattr(sshkeys, "_native", lambda: None)
     _keygen(qa_home / ".ssh" / "id_rsa", "rsa", passphrase="right-one")
     qaengine.add_engine(_Answers({"The CI/CD pipeline needs access": ["true"], "These are the files": ["id_rsa"],
                                   "Select the key": ["id_rsa"], "Enter the password": ["wrong-one"]}))
     assert sshkeys.get_ssh_key("git.corp.example") == ("", False)
 
 
-def test_missing_ssh_keygen_is_a_warning_not_an_openssh_key(qa_home, monkeypatch, capsys):
+def test_missing_ssh_keygen_is_a_warning_not_an_openssh_key(qa_home, monkeypatch, capsys, keygen_fallback):
     k = qa_home / ".ssh" / "id_rsa"
     k.write_text("-----BEGIN OPENSSH PRIVATE KEY-----\nAAAA\n-----END OPENSSH PRIVATE KEY-----\n")
     k.chmod(stat.S_IRUSR | stat.S_IWUSR)

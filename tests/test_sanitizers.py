@@ -167,3 +167,53 @@ def test_native_runtime_under_sanitizer(kind, lib, tmp_path):
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
     assert p.returncode == 0 and "SANITIZER-DRIVER-OK" in p.stdout, p.stdout[-4000:]
     assert "WARNING: ThreadSanitizer" not in p.stdout and "ERROR: AddressSanitizer" not in p.stdout, p.stdout[-4000:]
+
+
+SSHKEY_DRIVER = textwrap.dedent(r'''
+    import glob, os, sys, threading
+    sys.path.insert(0, sys.argv[1])
+    import _m2k_sshkey as m
+    fix = sys.argv[2]
+    keys = sorted(glob.glob(os.path.join(fix, "*.key")))
+    assert len(keys) >= 15
+    def run(k):
+        data = open(k, "rb").read()
+        st, txt = m.private_key_pem(data, None)
+        if st == 1:
+            st, txt = m.private_key_pem(data, b"m2k-pass")
+        exp = k[:-4] + ".expected.pem"
+        if os.path.exists(exp):
+            assert (st, txt) == (0, open(exp).read()), (k, st, txt)
+        # every truncation and a byte flip at each of a few hundred offsets:
+        # errors, never a crash or an out-of-bounds access
+        for i in range(0, len(data), max(1, len(data) // 150)):
+            m.private_key_pem(data[:i], None)
+            bad = bytearray(data)
+            bad[i] ^= 0x5A
+            m.private_key_pem(bytes(bad), None)
+            m.private_key_pem(bytes(bad), b"m2k-pass")
+    ts = [threading.Thread(target=run, args=(k,)) for k in keys]
+    for t in ts: t.start()
+    for t in ts: t.join()
+    print("SANITIZER-DRIVER-OK")
+''')
+
+
+def test_sshkey_converter_under_asan(tmp_path):
+    rt = _runtime("libasan.so")
+    if rt is None:
+        pytest.skip("libasan.so runtime not installed")
+    moddir = tmp_path / "mod"
+    moddir.mkdir()
+    so = str(moddir / ("_m2k_sshkey" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")))
+    build.build_sshkey(force=True, out=so, sanitize="address")
+    cxx = _runtime("libstdc++.so.6")
+    env = dict(os.environ, LD_PRELOAD=rt + (" " + cxx if cxx else ""),
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    drv = tmp_path / "driver.py"
+    drv.write_text(SSHKEY_DRIVER)
+    p = subprocess.run([sys.executable, str(drv), str(moddir), os.path.join(ROOT, "tests", "fixtures", "sshkeys")],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=900)
+    assert p.returncode == 0 and "SANITIZER-DRIVER-OK" in p.stdout, p.stdout[-4000:]
+    assert "ERROR: AddressSanitizer" not in p.stdout and "runtime error" not in p.stdout, p.stdout[-4000:]
