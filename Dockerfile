@@ -23,8 +23,11 @@ ARG OPERATOR_SDK_URL=
 ARG PACK_VERSION=v0.12.0
 ARG KUBECTL_VERSION=
 COPY scripts/installdeps.sh scripts/installdeps.sh
-# (the ARGs reach the script as environment variables; empty means its default)
-RUN INSTALL_DOCKER=0 MOVE2KUBE_DEP_INSTALL_PATH=/opt/m2k-deps bash scripts/installdeps.sh -y
+# (the ARGs reach the script as environment variables; empty means its default).
+# FORCE_INSTALL=1: all three tools land in /opt/m2k-deps even when the builder
+# base already has one on PATH, so the runtime stage's COPY always finds them
+RUN INSTALL_DOCKER=0 FORCE_INSTALL=1 MOVE2KUBE_DEP_INSTALL_PATH=/opt/m2k-deps bash scripts/installdeps.sh -y \
+ && test -x /opt/m2k-deps/operator-sdk && test -x /opt/m2k-deps/pack && test -x /opt/m2k-deps/kubectl
 COPY . .
 RUN PYTORCH_ROCM_ARCH=gfx950 python3 -m move2kube_amd.ops.build \
  && python3 -m pytest tests -q -m "not gpu" -x -p no:cacheprovider

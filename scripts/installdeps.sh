@@ -21,6 +21,9 @@
 #   KUBECTL_VERSION (stable.txt)    KUBECTL_URL
 #   OPERATOR_SDK_VERSION (v1.0.0)   OPERATOR_SDK_URL
 #   INSTALL_DOCKER=0                never run the docker convenience script
+#   FORCE_INSTALL=1                 install pack, kubectl and operator-sdk into
+#                                   the install directory even when PATH has
+#                                   them (the image build copies all three)
 set -eu
 
 QUIET=false
@@ -40,8 +43,12 @@ DEST="${MOVE2KUBE_DEP_INSTALL_PATH:-$PWD/bin}"
 PACK_VERSION="${PACK_VERSION:-v0.12.0}"
 OPERATOR_SDK_VERSION="${OPERATOR_SDK_VERSION:-v1.0.0}"
 INSTALL_DOCKER="${INSTALL_DOCKER:-1}"
+FORCE_INSTALL="${FORCE_INSTALL:-0}"
 
 have() { command -v "$1" >/dev/null 2>&1; }
+
+# present <tool>: on PATH and not to be (re)installed into $DEST
+present() { [ "$FORCE_INSTALL" != 1 ] && have "$1"; }
 
 # operator-sdk v0 cannot scaffold a Helm operator with `init --plugins=helm`
 sdk_is_v1() {
@@ -127,14 +134,14 @@ if ! have docker && [ "$OS" = linux ] && [ "$INSTALL_DOCKER" != 0 ]; then
   fi
 fi
 
-if ! have pack; then
+if ! present pack; then
   echo "Installing pack ${PACK_VERSION}..."
   fetch "${PACK_URL:-https://github.com/buildpacks/pack/releases/download/${PACK_VERSION}/pack-${PACK_VERSION}-${PACK_OS}.tgz}" "$WORK/pack.tgz"
   tar -xzf "$WORK/pack.tgz" -C "$WORK"
   install -m 0755 "$WORK/pack" "$DEST/pack"
 fi
 
-if ! have kubectl; then
+if ! present kubectl; then
   if [ -z "${KUBECTL_URL:-}" ]; then
     KUBECTL_VERSION="${KUBECTL_VERSION:-$(curl -fsSL https://storage.googleapis.com/kubernetes-release/release/stable.txt)}"
     KUBECTL_URL="https://storage.googleapis.com/kubernetes-release/release/${KUBECTL_VERSION}/bin/${OS}/${ARCH}/kubectl"
@@ -144,8 +151,8 @@ if ! have kubectl; then
   install -m 0755 "$WORK/kubectl" "$DEST/kubectl"
 fi
 
-if ! sdk_is_v1; then
-  have operator-sdk && echo "operator-sdk on PATH is not v1 ($(command -v operator-sdk)); installing ${OPERATOR_SDK_VERSION} ahead of it"
+if [ "$FORCE_INSTALL" = 1 ] || ! sdk_is_v1; then
+  have operator-sdk && ! sdk_is_v1 && echo "operator-sdk on PATH is not v1 ($(command -v operator-sdk)); installing ${OPERATOR_SDK_VERSION} ahead of it"
   echo "Installing operator-sdk ${OPERATOR_SDK_VERSION}..."
   fetch "${OPERATOR_SDK_URL:-https://github.com/operator-framework/operator-sdk/releases/download/${OPERATOR_SDK_VERSION}/operator-sdk-${OPERATOR_SDK_VERSION}-${SDK_ARCH}-${SDK_OS}}" "$WORK/operator-sdk"
   install -m 0755 "$WORK/operator-sdk" "$DEST/operator-sdk"

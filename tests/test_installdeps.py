@@ -137,3 +137,21 @@ def test_prompt_declined_installs_nothing(env, tmp_path):
                        timeout=60)
     assert p.returncode == 1 and "nothing installed" in p.stdout.decode()
     assert not (tmp_path / "deps").exists()
+
+
+def test_force_install_ignores_tools_already_on_path(env, tmp_path):
+    # FORCE_INSTALL=1 (the image build): every tool goes to the install
+    # directory even when PATH has a good one
+    for t, body in (("pack", "echo pack"), ("kubectl", "echo kubectl"),
+                    ("operator-sdk", 'echo \'operator-sdk version: "v1.2.0", commit: "x"\'')):
+        p = tmp_path / "stub" / t
+        p.write_text("#!/bin/sh\n%s\n" % body)
+        p.chmod(0o755)
+    p = _run(env, "-y")
+    assert p.returncode == 0 and not (tmp_path / "deps" / "pack").exists()   # present: nothing to do
+    p = _run(dict(env, FORCE_INSTALL="1"), "-y")
+    out = p.stdout.decode()
+    assert p.returncode == 0, out
+    for t in ("pack", "kubectl", "operator-sdk"):
+        assert os.access(str(tmp_path / "deps" / t), os.X_OK), t
+    assert "is not v1" not in out

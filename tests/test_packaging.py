@@ -28,7 +28,9 @@ def test_builddist_and_install(tmp_path):
     p = subprocess.run(["bash", os.path.join(ROOT, "scripts", "install.sh"), str(out / tgz), str(prefix)],
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, cwd=str(elsewhere), env=env)
     assert p.returncode == 0, p.stdout.decode()
-    assert p.stdout.decode().splitlines()[-1] == "v0.3.1+unreleased"   # install.sh ends with `move2kube version`
+    # install.sh ends by running the installed launcher's `move2kube version`
+    lines = p.stdout.decode().splitlines()
+    assert "v0.3.1+unreleased" in lines and lines[-1] == "Done!"
     long = subprocess.run([str(prefix / "bin" / "move2kube"), "version", "-l"], stdout=subprocess.PIPE, check=True,
                           cwd=str(elsewhere), env=env)
     assert long.stdout.decode().splitlines()[:3] == ["version: v0.3.1+unreleased", "gitCommit: abc123",
@@ -92,3 +94,69 @@ def test_wheel_with_the_images_setuptools(tmp_path):
     assert "move2kube_amd/_bytecode.bin" not in names  # installed files get new mtimes: it would never be valid
     if os.path.exists(os.path.join(ROOT, "move2kube_amd", "ops", "libm2k_ed_hip.so")):
         assert "move2kube_amd/ops/libm2k_ed_hip.so" in names
+
+
+def _workflow(name):
+    import yaml
+    with open(os.path.join(ROOT, ".github", "workflows", name)) as f:
+        wf = yaml.safe_load(f)
+    # PyYAML reads the bare key `on` as the boolean True
+    wf["on"] = wf.get("on", wf.get(True))
+    return wf
+
+
+def _runs(job):
+    return "\n".join(s.get("run", "") for s in job["steps"])
+
+
+def test_release_workflow_follows_the_reference():
+    """release.yml (reference .github/workflows/release.yml:37-160): on v* tags,
+    test; build, e2e-check and push the image under the tag; draft a release;
+    upload every dist archive with its checksum to it."""
+    wf = _workflow("release.yml")
+    assert wf["on"] == {"push": {"tags": ["v*"]}}
+    jobs = wf["jobs"]
+    assert set(jobs) == {"build", "image-build", "create-release-draft", "upload-release-assets"}
+    assert "pytest tests" in _runs(jobs["build"])
+    img = jobs["image-build"]
+    assert img["needs"] == ["build"]
+    runs = _runs(img)
+    assert "make cbuild" in runs and "VERSION=${{ steps.vars.outputs.tag }}" in runs
+    assert "scripts/image_e2e.sh" in runs
+    assert "docker push quay.io/konveyor/move2kube-amd:${{ steps.vars.outputs.tag }}" in runs
+    draft = jobs["create-release-draft"]
+    runs = _runs(draft)
+    assert "make dist" in runs and "VERSION=${GITHUB_REF#refs/tags/}" in runs
+    assert "gh release create" in runs and "--draft" in runs
+    assert any(s.get("uses", "").startswith("actions/upload-artifact") and s["with"]["path"] == "dist/"
+               for s in draft["steps"])
+    up = jobs["upload-release-assets"]
+    assert up["needs"] == ["create-release-draft"]
+    runs = _runs(up)
+    for suffix in (".tar.gz", ".tar.gz.sha256sum", ".zip", ".zip.sha256sum"):
+        assert "amd64%s\"" % suffix in runs
+    assert "gh release upload" in runs
+    # the names are what scripts/builddist.py writes and scripts/install.sh downloads
+    with open(os.path.join(ROOT, "scripts", "install.sh")) as f:
+        assert 'DIST="move2kube-amd-$TAG-$OS-$ARCH.tar.gz"' in f.read()
+
+
+def test_tag_and_ci_workflows():
+    tag = _workflow("tag.yml")
+    assert "workflow_dispatch" in tag["on"] and "git push origin" in _runs(tag["jobs"]["tag"])
+    ci = _workflow("ci.yml")
+    assert ci["on"]["push"] == {"branches": ["main"]}          # tags: release.yml
+    runs = _runs(ci["jobs"]["image"])
+    assert "move2kube-amd:latest" in runs and "refs/heads/main" in str(ci["jobs"]["image"]["steps"])
+
+
+def test_image_build_installs_every_tool_it_copies():
+    # a builder base with pack/kubectl/operator-sdk already on PATH must still
+    # fill /opt/m2k-deps, since the runtime stage copies all three from there
+    with open(os.path.join(ROOT, "Dockerfile")) as f:
+        text = f.read()
+    builder = text[:text.index("FROM ${RUNTIME_IMAGE}")]
+    assert "FORCE_INSTALL=1" in builder and "scripts/installdeps.sh -y" in builder
+    for tool in ("operator-sdk", "pack", "kubectl"):
+        assert "test -x /opt/m2k-deps/%s" % tool in builder
+        assert "/opt/m2k-deps/%s" % tool in text[text.index("FROM ${RUNTIME_IMAGE}"):]
