@@ -268,9 +268,10 @@ def _emit(p, ir, outpath, qadisablecli):
 
 def _emit_artifacts(p, ir, outpath, qadisablecli):
     # For a Helm chart the main transformer starts operator-sdk once the chart
-    # is written and waits for it at the end; the compose and CI/CD files and
-    # the QA cache do not feed the chart, so they are written in that wait
-    # (same bytes, same files).  Every question is asked before the chart.
+    # is written and waits for it at the end; the compose file, the CI/CD
+    # objects (built and written) and the QA cache do not feed the chart, so
+    # they are done in that wait (same bytes, same files, same questions in
+    # the same order: the Kubernetes transform asks none).
     overlap = [] if p.kubernetes.artifact_type == plantypes.HELM else None
 
     def later(fn):
@@ -307,22 +308,26 @@ def _emit_artifacts(p, ir, outpath, qadisablecli):
         if any(c.new for c in ir.containers):
             cicd = transformer.CICDTransformer()
 
-            def write_cicd():
+            def transform_and_write_cicd():
+                try:
+                    with trace.span("CICDTransformer", "transform"):
+                        cicd.transform(ir)
+                except Exception as e:  # noqa: BLE001
+                    if isinstance(e, log.FatalError):
+                        raise
+                    log.error("Error while genrationg CI/CD resource fomr the IR. Error: %r", str(e))  # sic
+                    return
                 try:
                     cicd.write_objects(outpath)
                 except Exception as e:  # noqa: BLE001
                     if isinstance(e, log.FatalError):
                         raise
                     log.error("Unable to write the CI/CD artifacts to files. Error: %r", str(e))
-            try:
-                with trace.span("CICDTransformer", "transform"):
-                    cicd.transform(ir)
-            except Exception as e:  # noqa: BLE001
-                if isinstance(e, log.FatalError):
-                    raise
-                log.error("Error while genrationg CI/CD resource fomr the IR. Error: %r", str(e))  # sic
-            else:
-                later(write_cicd)
+            # the Tekton objects read the final IR but feed nothing the
+            # Kubernetes transform or the chart reads, and the Kubernetes
+            # transform asks no question: for a Helm chart they are built
+            # while operator-sdk runs, with their questions in the same order
+            later(transform_and_write_cicd)
 
         ir.add_copy_sources_warning = qadisablecli
         t = transformer.get_transformer(ir)

@@ -175,10 +175,8 @@ def collect():
 
 def _gotemplate_stamp():
     from ..utils import startcache
-    mtime, size = startcache.source_stamp(startcache.GOTEMPLATE_SRC)
-    with open(startcache.GOTEMPLATE_SRC, "rb") as f:
-        digest = hashlib.sha1(f.read()).hexdigest()
-    return mtime, size, digest
+    mtime, size = startcache.source_stamp(startcache.parser_sources())
+    return mtime, size, startcache.source_digest(startcache.parser_sources())
 
 
 def write(out=None):

@@ -31,7 +31,12 @@ import sys
 FILENAME = "_startcache.bin"
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PATH = os.path.join(os.path.dirname(_HERE), FILENAME)
-GOTEMPLATE_SRC = os.path.join(_HERE, "gotemplate.py")
+GOTEMPLATE_SRC = os.path.join(_HERE, "gotemplate.py")          # the node classes
+GOTEMPLATE_PARSE_SRC = os.path.join(_HERE, "gotemplate_parse.py")  # the parser
+
+
+def parser_sources():
+    return (GOTEMPLATE_SRC, GOTEMPLATE_PARSE_SRC)
 
 _state = None  # None: not read yet; False: unusable; else (templates, regexes)
 
@@ -41,9 +46,19 @@ def interpreter_tag():
     return "%s|%s|%d|%d" % (sys.version, sys.implementation.cache_tag, _sre.MAGIC, _sre.CODESIZE)
 
 
-def source_stamp(path):
-    st = os.stat(path)
-    return int(st.st_mtime), st.st_size
+def source_stamp(paths):
+    """(newest mtime, total size) of the files ``paths``."""
+    sts = [os.stat(p) for p in ((paths,) if isinstance(paths, str) else paths)]
+    return max(int(st.st_mtime) for st in sts), sum(st.st_size for st in sts)
+
+
+def source_digest(paths):
+    import hashlib
+    h = hashlib.sha1()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
 
 
 def _load():
@@ -69,11 +84,9 @@ def _same_parser(stamp):
     size and mtime, or (an installed copy has new mtimes) its SHA-1."""
     try:
         mtime, size, digest = stamp
-        if (mtime, size) == source_stamp(GOTEMPLATE_SRC):
+        if (mtime, size) == source_stamp(parser_sources()):
             return True
-        import hashlib
-        with open(GOTEMPLATE_SRC, "rb") as f:
-            return hashlib.sha1(f.read()).hexdigest() == digest
+        return source_digest(parser_sources()) == digest
     except (OSError, ValueError, TypeError):
         return False
 
