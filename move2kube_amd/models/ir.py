@@ -70,7 +70,10 @@ class Service:
     # PodSpec conveniences
     @property
     def containers(self):
-        return self.pod_spec.setdefault("containers", [])
+        # reading leaves pod_spec as it was (a Go range over a nil slice does
+        # not allocate one); assign through the setter to add containers
+        cs = self.pod_spec.get("containers")
+        return cs if cs is not None else []
 
     @containers.setter
     def containers(self, v):

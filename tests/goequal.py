@@ -44,3 +44,16 @@ def diff(got, want, path="$"):
 def assert_deep_equal(got, want):
     d = diff(got, want)
     assert d is None, d
+
+
+def subtests(*cases):
+    """One ``pytest.param`` per row of a Go table test: the first item of each
+    case is the subtest name, used as the pytest id; a repeated name gets
+    ``#01``, ``#02``, ... as testing.T names it."""
+    import pytest
+    seen, out = {}, []
+    for c in cases:
+        n = seen.get(c[0], 0)
+        seen[c[0]] = n + 1
+        out.append(pytest.param(*c[1:], id=c[0] + ("#%02d" % n if n else "")))
+    return out

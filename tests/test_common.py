@@ -1,4 +1,5 @@
-"""Common helpers (table cases mirror ``internal/common/utils_test.go``)."""
+"""Common helpers beyond ``internal/common/utils_test.go`` (whose subtests are
+ported one by one in ``test_reference_utils.py``)."""
 
 import json
 import os
@@ -9,112 +10,9 @@ from conftest import ref_path
 from move2kube_amd.utils import common, tarutil
 
 
-@pytest.mark.parametrize("inp,out", [
-    ("foobar%${/2\n\tinv.json.yaml.", "2-inv.json.yaml-d65d80a1c389718f"),
-    ("foobar", "foobar-534a426c0464b01e"),
-    ("thisisalongfilenamefoobar", "thisisalongfile-730bb88a395ce114"),
-    ("foobar.json", "foobar.json-f161da8efa921f1f"),
-    ("path/to/a/file/foobar.json", "foobar.json-b1760918996ebb3"),
-])
-def test_normalize_for_filename(inp, out):
-    assert common.normalize_for_filename(inp) == out
-
-
-@pytest.mark.parametrize("inp,out", [("foobar.website.registration.", "foobar-website-registration-"),
-                                     ("foobar", "foobar"), ("thisisalongservicenamefoobar", "thisisalongservicenamefoobar")])
-def test_normalize_for_service_name(inp, out):
-    assert common.normalize_for_service_name(inp) == out
-
-
 def test_is_string_present_is_case_insensitive():
-    assert common.is_string_present(["foo", "bar"], "foo")
+    # utils_test.go's cases are in test_reference_utils.py; Go's IsStringPresent uses EqualFold
     assert common.is_string_present(["foo", "bar"], "FOO")
-    assert not common.is_string_present(["foo", "bar"], "str1")
-
-
-def test_is_int_present():
-    assert not common.is_int_present([], 0)
-    assert common.is_int_present([100, 0, 1, -1, -42], 0)
-    assert not common.is_int_present([100, 0, 1, -1, -42], 200)
-
-
-@pytest.mark.parametrize("a,b,out", [([], [], []), ([], ["foo", "bar"], ["foo", "bar"]), (["foo", "bar"], [], ["foo", "bar"]),
-                                     (["foo", "bar"], ["foo", "bar", "item1", "item2"], ["foo", "bar", "item1", "item2"])])
-def test_merge_string_slices(a, b, out):
-    assert common.merge_string_slices(a, b) == out
-
-
-def test_merge_int_slices():
-    assert common.merge_int_slices([100, -42, -1, 0], [10, -1, -1, 0, 2]) == [100, -42, -1, 0, 10, 2]
-
-
-def test_merge_string_maps():
-    assert common.merge_string_maps({"key1": "val1", "key2": "val2"}, {"key2": "newval2", "key3": "val3"}) == \
-        {"key1": "val1", "key2": "newval2", "key3": "val3"}
-
-
-@pytest.mark.parametrize("tpl,data,out,err", [
-    ("", "", "", False),
-    ("", {}, "", False),
-    ("", {"Name": "", "ID": 0}, "", False),
-    ("Hello! My name is {{.Name}} and my ID is {{.ID}}", {"Name": "", "ID": 0}, "Hello! My name is  and my ID is 0", False),
-    ("Hello! My name is {{.Name}} and my ID is {{.ID}}", {"Name": "foobar", "ID": 42},
-     "Hello! My name is foobar and my ID is 42", False),
-])
-def test_get_string_from_template(tpl, data, out, err):
-    assert common.get_string_from_template(tpl, data) == out
-
-
-def test_write_template_to_missing_dir_fails():
-    with pytest.raises(OSError):
-        common.write_template_to_file("x{{.A}}", {"A": 1}, "/this/path/does/not/exist/foobar", 0o644)
-
-
-@pytest.mark.parametrize("opts,q,out", [([], "foo", ""), (["foo", "bar"], "foo", "foo"), (["foo", "bar"], "bar2", "bar")])
-def test_get_closest_matching_string(opts, q, out):
-    assert common.get_closest_matching_string(opts, q) == out
-
-
-@pytest.mark.parametrize("inp,out", [
-    ("", ""), ("foo\n123.bar%4.inv#22.-", "foo-123.bar-4.inv-22.-"), ("foo/bar/", "bar"),
-    ("path/prefix/foo_bar_baz", "foo-bar-baz"), ("foo.bar.baz", "foo.bar.baz"),
-    ("0123456789" * 8, "0123456789" * 8),
-])
-def test_make_file_name_compliant(inp, out):
-    assert common.make_file_name_compliant(inp) == out
-
-
-@pytest.mark.parametrize("inp,out", [
-    ([], ""), (["/foo/bar/baz", "/foo/bar", "/foo"], "/foo"), (["/foo/bar/baz", "/foo/bar", "/app1/service1/module1"], "/"),
-    (["/app1/./service1/", "/app1/service1/module2/", "/app1/./service1/../service1/module1"], "/app1/service1"),
-    (["/foo/bar///baz", "/foo/bar///.", "/app1/./service1/../service1/module1"], "/"),
-    (["/foo/bar/baz"] * 3, "/foo/bar/baz"), (["/", "/.", "/..", "/.app/.bar", "/.app/.bar"], "/"),
-    (["/foo/bar", "/", "/foo/bar/baz"], "/"), (["/foo/bar/baz////", "/foo/bar/baz", "/foo/bar/baz/././../baz/"], "/foo/bar/baz"),
-])
-def test_clean_and_find_common_directory(inp, out):
-    assert common.clean_and_find_common_directory(inp) == out
-
-
-@pytest.mark.parametrize("inp,out", [([], []), (["foo", "bar", "baz"], ["foo", "bar", "baz"]),
-                                     (["abc", "foo", "bar", "foo", "baz", "foo", "abc", "abc"], ["abc", "foo", "bar", "baz"]),
-                                     (["foo"] * 7, ["foo"])])
-def test_unique_strings(inp, out):
-    assert common.unique_strings(inp) == out
-
-
-def test_image_name_and_tag():
-    assert common.get_image_name_and_tag("konveyor/getting-started:1.2.3-alpha.beta.gamma+hello.123.world") == \
-        ("getting-started", "1.2.3-alpha.beta.gamma+hello.123.world")
-    assert common.get_image_name_and_tag("konveyor/getting-started") == ("getting-started", "latest")
-
-
-@pytest.mark.reference
-def test_yaml_attr_present():
-    td = ref_path("internal", "common", "testdata")
-    assert common.yaml_attr_present("foobar", "attr1")[0] is False
-    assert common.yaml_attr_present(os.path.join(td, "invalidfiles", "test1.yaml"), "attr1")[0] is False
-    assert common.yaml_attr_present(os.path.join(td, "validfiles", "test1.yaml"), "attr1")[0] is False
-    assert common.yaml_attr_present(os.path.join(td, "validfiles", "test1.yaml"), "kind") == (True, "ClusterMetadata")
 
 
 def test_tar_roundtrip(tmp_path):
