@@ -11,10 +11,10 @@ pytestmark = pytest.mark.reference
 
 
 @pytest.mark.parametrize("obj,kind", [
-    (collection.ImageInfo(), collection.IMAGE_METADATA_KIND),
-    (collection.CfContainerizers(), collection.CF_CONTAINERIZERS_KIND),
-    (collection.CfInstanceApps(), collection.CF_INSTANCE_APPS_KIND),
-    (qa.Cache("cache.yaml"), qa.QACACHE_KIND),
+    pytest.param(collection.ImageInfo(), collection.IMAGE_METADATA_KIND, id="TestNewImageInfo"),
+    pytest.param(collection.CfContainerizers(), collection.CF_CONTAINERIZERS_KIND, id="TestNewCfContainerizers"),
+    pytest.param(collection.CfInstanceApps(), collection.CF_INSTANCE_APPS_KIND, id="TestNewCfInstanceApps"),
+    pytest.param(qa.Cache("cache.yaml"), qa.QACACHE_KIND, id="TestNewCache"),
 ])
 def test_new_typed_files(obj, kind):
     assert obj.kind == kind

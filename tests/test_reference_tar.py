@@ -52,6 +52,12 @@ def _walk_expected(root, ignored=()):
     return exp
 
 
+def test_tar_path_does_not_exist(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    with pytest.raises(tarutil.TarError, match="^lstat foobar: no such file or directory$"):
+        tarutil.tar_as_string("foobar", [])
+
+
 def test_tar_a_single_file(tmp_path):
     src = os.path.join(TOBETARRED, "test1.yaml")
     dst = tmp_path / "test1.yaml"
@@ -120,8 +126,11 @@ def test_untar_invalid_tar(untar_data, tmp_path):
         tarutil.untar_string(untar_data["untar_an_invalid_tarstring"], str(tmp_path))
 
 
-@pytest.mark.parametrize("key", ["untar_into_a_directory_we_dont_have_permission_to_write_to",
-                                 "untar_a_single_file_into_a_directory_we_dont_have_permission_to_write_to"])
+@pytest.mark.parametrize("key", [
+    pytest.param("untar_into_a_directory_we_dont_have_permission_to_write_to",
+                 id="untar into a directory we don't have permission to write to"),
+    pytest.param("untar_a_single_file_into_a_directory_we_dont_have_permission_to_write_to",
+                 id="untar a single file into a directory we don't have permission to write to")])
 def test_untar_into_unwritable_dir(untar_data, unprivileged, key):
     """tar_test.go:281-305: untarring below a directory with mode 0 fails."""
     d = os.path.join(unprivileged.tmp, "nopermstowrite")
