@@ -4,7 +4,7 @@ configuration (its last command), after an untimed priming run: every module
 imported after ``site``, self and cumulative microseconds, median of
 ``--runs`` processes, largest self time first.  One JSON line.
 
-    python benchmarks/cold_importtime.py helm-openshift [--runs 9]
+    python benchmarks/cold_importtime.py helm-openshift [--runs 9] [--tree .ab_base/r04]
 """
 import argparse
 import json
@@ -39,13 +39,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("config")
     ap.add_argument("--runs", type=int, default=9)
+    ap.add_argument("--tree", default=refconfigs.ROOT, help="the source tree to import (e.g. .ab_base/r04)")
     a = ap.parse_args()
     root, _ = refconfigs.workdir_root("auto")
     work = tempfile.mkdtemp(prefix="m2k-imptime-", dir=root)
     try:
         run = refconfigs.Run(a.config, work).prepare()
         env = run.env()
-        env["PYTHONPATH"] = refconfigs.ROOT
+        env["PYTHONPATH"] = os.path.abspath(a.tree)
         argv = run.cli_commands()[-1]
         for argv0 in run.cli_commands()[:-1]:  # e.g. cf's collect, so translate sees its output
             subprocess.run([sys.executable, "-m", "move2kube_amd"] + argv0, env=env, cwd=work,

@@ -93,7 +93,7 @@ class APIResource:
         return ignored
 
     def get_updated_resources(self, ir):
-        objs = self.handler.create_new_resources(ir, self.get_cluster_supported_kinds())
+        objs = self.handler.create_new_resources(ir, self.get_cluster_supported_kinds()) or []
         for obj in objs:
             if not self._load(obj, objs, ir):
                 log.error("Object created seems to be of an incompatible type : %r", obj.get("kind"))

@@ -59,7 +59,7 @@ class NetworkPolicy(IAPIResource):
     def create_new_resources(self, ir, supported):
         if not common.is_string_present(supported, NETWORK_POLICY):
             log.error("Could not find a valid resource type in cluster to create a NetworkPolicy")
-            return []
+            return None   # nil in the reference; an empty list when the kind is supported
         objs = []
         for service in ir.sorted_services():
             for net in service.networks:

@@ -50,7 +50,7 @@ from .gofmt import (NO_VALUE, GoUint8, quote as go_quote, sorted_keys, sprint, s
                     sprintf, sprintln, type_string)
 
 INTERPRET = os.environ.get("M2K_TEMPLATE_INTERPRET", "") == "1"  # the tree walker instead of closures
-COMPILE_AFTER = 1  # executions of a template interpreted before it is compiled to closures
+COMPILE_AFTER = int(os.environ.get("M2K_TEMPLATE_COMPILE_AFTER", "1"))  # interpreted runs before compiling
 MAX_EXEC_DEPTH = 100000  # exec.go: maxExecDepth
 
 
@@ -1065,7 +1065,12 @@ def render(src, data, funcs=None):
 
 def __getattr__(name):
     """The lexer/parser and compiler names (``_lex``, ``I_*``, ``_c_*``, ...)
-    live in modules loaded on use; tests reach them through this module."""
+    live in modules loaded on use; tests reach them through this module.
+    Dunder names are never forwarded: the import system probes ``__path__``
+    on every ``from gotemplate import X``, and answering it would load both
+    modules in every process."""
+    if name.startswith("__"):
+        raise AttributeError("module %r has no attribute %r" % (__name__, name))
     for mod in ("gotemplate_parse", "gotemplate_compile"):
         import importlib
         m = importlib.import_module("." + mod, __package__)

@@ -11,7 +11,10 @@ and are left out."""
 def _fields(o):
     d = getattr(o, "__dict__", None)
     if d is None:
-        return None
+        slots = [n for c in type(o).__mro__ for n in getattr(c, "__slots__", ())]
+        if not slots:
+            return None
+        d = {n: getattr(o, n) for n in slots if hasattr(o, n)}
     return {k: v for k, v in d.items() if not k.startswith("_")}
 
 

@@ -2,7 +2,8 @@
 ``func TestX(t *testing.T)`` without subtests is ``TestX``; each subtest is
 ``TestX/<name>`` with the name as written in ``t.Run("<name>", ...)``, or, for
 a table-driven ``t.Run(tc.name, ...)``, each ``name: "<name>"`` of the table
-in that function.  ``tests/test_reference_ledger.py`` checks that every one
+in that function; a testify ``suite.Run(t, new(S))`` has one subtest per
+``Test*`` method of ``S``.  ``tests/test_reference_ledger.py`` checks that every one
 is mapped to a pytest in ``tests/reference_ledger.json``."""
 
 import os
@@ -11,6 +12,7 @@ import re
 _FUNC = re.compile(r"^func (Test\w+)\(t \*testing\.T\) \{", re.M)
 _RUN_LIT = re.compile(r't\.Run\("((?:[^"\\]|\\.)*)"')
 _RUN_VAR = re.compile(r"t\.Run\((\w+)\.(\w+),")
+_SUITE = re.compile(r"suite\.Run\(t, (?:new\((\w+)\)|&(\w+)\{\})")
 _TABLE = re.compile(r"\w+\s*:?=\s*\[\]struct\s*\{")
 _GO_STR = re.compile(r'"((?:[^"\\]|\\.)*)"')
 
@@ -123,6 +125,9 @@ def test_names(path):
         for r in _RUN_VAR.finditer(body):
             runs.append((r.start(), _table_names(body, r.group(2))))
         subs = [s for _, names in sorted(runs) for s in names]
+        suite = _SUITE.search(body)
+        if suite:   # testify: one subtest per Test* method, in reflect's (sorted) method order
+            subs += sorted(re.findall(r"^func \(\w+ \*%s\) (Test\w+)\(\)" % (suite.group(1) or suite.group(2)), src, re.M))
         if subs:
             seen = {}
             for s in subs:   # testing.T: a repeated subtest name gets #01, #02, ...

@@ -38,6 +38,9 @@ class _FakeDockerd(BaseHTTPRequestHandler):
         n = int(self.headers.get("Content-Length") or 0)
         body = self.rfile.read(n) if n else b""
         if self.path.startswith("/images/create"):
+            self.state.setdefault("pulls", []).append(self.path)
+            if "doesnotexist" in self.path:   # what dockerd answers for an image no registry has
+                return self._json(404, {"message": "pull access denied for this/doesnotexist"})
             return self._json(200, {"status": "pulled"})
         if self.path == "/containers/create":
             cfg = json.loads(body or b"{}")
@@ -83,6 +86,36 @@ def fake_dockerd(tmp_path, monkeypatch):
     yield sock
     srv.shutdown()
     srv.server_close()
+
+
+# --- internal/containerizer/cnb/dockerapiprovider_test.go: TestIsBuilderAvailable ---------
+# The Go test needs a Docker daemon that can pull cloudfoundry/cnb:cflinuxfs3;
+# the fake dockerd above answers the same Engine API calls.
+
+CF_BUILDER = "cloudfoundry/cnb:cflinuxfs3"
+
+
+def _pulls(builder):
+    return [p for p in _FakeDockerd.state.get("pulls", []) if "cloudfoundry%2Fcnb" in p]
+
+
+def test_is_builder_available_normal_use_case(fake_dockerd):
+    _FakeDockerd.state.clear()
+    assert providers.DockerAPIProvider().is_builder_available(CF_BUILDER)
+
+
+def test_is_builder_available_result_from_cache(fake_dockerd):
+    _FakeDockerd.state.clear()
+    p = providers.DockerAPIProvider()
+    assert p.is_builder_available(CF_BUILDER)
+    assert sorted(p.available_images) == [CF_BUILDER]
+    assert p.is_builder_available(CF_BUILDER)
+    assert len(_pulls(CF_BUILDER)) == 1   # the second answer came from the cache
+
+
+def test_is_builder_available_non_existent_image(fake_dockerd):
+    _FakeDockerd.state.clear()
+    assert not providers.DockerAPIProvider().is_builder_available("this/doesnotexist:foobar")
 
 
 def test_docker_api_provider(fake_dockerd, tmp_path):

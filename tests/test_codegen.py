@@ -1,4 +1,5 @@
-"""Code generator (``internal/common/generator`` test data shapes)."""
+"""Code generator: the Python modules it writes, and (``--go``) the reference's
+Go output checked against ``internal/common/generator/testdata``."""
 
 import importlib.util
 import os
@@ -63,3 +64,124 @@ def _load_str(text, tmp_path):
     p = tmp_path / "g.py"
     p.write_text(text)
     return _load(str(p))
+
+
+# --- internal/common/generator/generator_test.go, one pytest per subtest -------------------
+# The Go generator writes Go source; ``--go`` mode writes the same bytes.
+
+GEN_TESTDATA = ref_path("internal", "common", "generator", "testdata")
+
+
+@pytest.fixture
+def gen_cwd(tmp_path, monkeypatch):
+    """cwd holding a writable copy of the generator's testdata (the Go test
+    writes constants.go into testdata/datafortempfilled)."""
+    import shutil
+    shutil.copytree(GEN_TESTDATA, str(tmp_path / "testdata"))
+    for dp, dns, fns in os.walk(str(tmp_path / "testdata")):
+        os.chmod(dp, 0o755)
+        for fn in fns:
+            os.chmod(os.path.join(dp, fn), 0o644)
+    monkeypatch.chdir(tmp_path)
+    return tmp_path
+
+
+def _skip_timestamp(path, want_lines, drop_last=False):
+    with open(path) as f:
+        lines = f.read().split("\n")
+    assert len(lines) == want_lines
+    return "\n".join(lines[:2] + lines[3:len(lines) - 1 if drop_last else len(lines)])
+
+
+@pytest.mark.reference
+def test_generate_code_for_non_existent_directory(gen_cwd):
+    with pytest.raises(OSError):
+        codegen.go_make_constants("testdata/nonexistent", codegen.GO_MAPS)
+
+
+@pytest.mark.reference
+@pytest.mark.parametrize("tpl,fixture", [
+    pytest.param("GO_MAPS", "maptempemptyskiptimestamp.txt", id="read empty directory and generate code with maptemp"),
+    pytest.param("GO_CONSTS", "conststempemptyskiptimestamp.txt",
+                 id="read empty directory and generate code with conststemp")])
+def test_generate_code_for_empty_directory(gen_cwd, tpl, fixture):
+    d = gen_cwd / "foobar"
+    d.mkdir()
+    codegen.go_make_constants(str(d), getattr(codegen, tpl))
+    with open(os.path.join("testdata", fixture)) as f:
+        assert _skip_timestamp(str(d / "constants.go"), 8 + 17) == f.read()
+
+
+@pytest.mark.reference
+@pytest.mark.parametrize("tpl,fixture", [
+    pytest.param("GO_MAPS", "maptempfilledskiptimestamp.txt", id="read filled directory and generate code with maptemp"),
+    pytest.param("GO_CONSTS", "conststempfilledskiptimestamp.txt",
+                 id="read filled directory and generate code with conststemp")])
+def test_generate_code_for_filled_directory(gen_cwd, tpl, fixture):
+    codegen.go_make_constants("testdata/datafortempfilled", getattr(codegen, tpl))
+    with open(os.path.join("testdata", fixture)) as f:
+        assert _skip_timestamp("testdata/datafortempfilled/constants.go", 22 + 17) == f.read()
+
+
+def _unreadable_file_dir(unprivileged):
+    p = os.path.join(unprivileged.tmp, "nopermstoread")
+    with open(p, "w") as f:
+        f.write("no permission to read this file")
+    unprivileged.chown()
+    os.chmod(p, 0)
+    return unprivileged.tmp
+
+
+def _unwritable_dir(unprivileged):
+    d = os.path.join(unprivileged.tmp, "foobar")
+    os.mkdir(d)
+    unprivileged.chown()
+    os.chmod(d, 0o400)
+    return d
+
+
+@pytest.mark.parametrize("make", [
+    pytest.param(lambda d: codegen.go_make_constants(d, codegen.GO_CONSTS),
+                 id="generate code from directory containing files that we have no permissions to read"),
+    pytest.param(codegen.go_make_tar, id="make a tar when the directory has files which we have no permissions to read")])
+def test_generate_code_unreadable_file(unprivileged, make):
+    d = _unreadable_file_dir(unprivileged)
+
+    def check():
+        with pytest.raises((OSError, tarutil.TarError)):
+            make(d)
+    unprivileged.run(check)
+
+
+@pytest.mark.parametrize("make", [
+    pytest.param(lambda d: codegen.go_make_constants(d, codegen.GO_CONSTS),
+                 id="generate code from directory that we have no permissions to write to"),
+    pytest.param(codegen.go_make_tar, id="make a tar in a directory that we have no permissions to write to")])
+def test_generate_code_unwritable_directory(unprivileged, make):
+    d = _unwritable_dir(unprivileged)
+
+    def check():
+        with pytest.raises(OSError):
+            make(d)
+    unprivileged.run(check)
+
+
+@pytest.mark.reference
+def test_make_a_tar_using_a_filled_directory(gen_cwd):
+    codegen.go_make_tar("testdata/datafortempfilled")
+    with open("testdata/tartempfilledskiptimestampandtar.txt") as f:
+        assert _skip_timestamp("testdata/datafortempfilled/constants.go", 6 + 17, drop_last=True) == f.read()
+    # the last line holds the tree, without constants.go itself
+    with open("testdata/datafortempfilled/constants.go") as f:
+        last = f.read().split("\n")[-1]
+    assert last.startswith("const Tar =  `") and last.endswith("`")
+    names = sorted(m[0] for m in _tar_members(last[len("const Tar =  `"):-1]))
+    assert names == [".", "test1.json", "test2.yml", "testconfigs", "testconfigs/test3.yml"]
+
+
+def _tar_members(b64):
+    import base64
+    import io
+    import tarfile
+    with tarfile.open(fileobj=io.BytesIO(base64.b64decode(b64)), mode="r:") as tr:
+        return [(m.name, m.size) for m in tr]

@@ -1,4 +1,5 @@
-"""Any2Kube discovery / translation parity with ``internal/source/any2kube_test.go``."""
+"""``internal/source/any2kube_test.go``, one pytest per Go subtest, comparing
+whole service lists and whole IRs as the Go test does."""
 
 import base64
 import os
@@ -7,6 +8,7 @@ import shutil
 import pytest
 
 from conftest import ref_path
+from goequal import assert_deep_equal
 from move2kube_amd.models import ir as irtypes
 from move2kube_amd.models import plan as plantypes
 from move2kube_amd.source.any2kube import Any2KubeTranslator
@@ -15,10 +17,6 @@ from move2kube_amd.utils import tarutil, yamlio
 pytestmark = pytest.mark.reference
 
 SRC_TESTDATA = ref_path("internal", "source", "testdata")
-
-
-def _svc_dump(services):
-    return yamlio.dump([s.to_yaml() for s in services])
 
 
 def _plan_for(root, name="nodejs-app"):
@@ -58,6 +56,8 @@ def layout(tmp_path, monkeypatch, fake_cnb):
     return cwd
 
 
+# --- TestGetServiceOptions ------------------------------------------------------------
+
 def test_non_existent_dir(tmp_path, assets_dir):
     services = Any2KubeTranslator().get_service_options(str(tmp_path / "nope"), plantypes.new_plan())
     assert services == []
@@ -89,7 +89,21 @@ def test_nodejs_app_empty_plan(layout):
     root = os.path.abspath("../../samples/nodejs")
     want = plantypes.read_plan("testdata/expectedservicesfornodejsapp.yaml").services["nodejs"]
     got = _strip_repo(Any2KubeTranslator().get_service_options(root, _plan_for(root)))
-    assert _svc_dump(got) == _svc_dump(want)
+    assert_deep_equal(got, want)
+
+
+def test_nodejs_app_filled_plan(layout):
+    """Services of the plan whose source directories lie elsewhere do not hide the app."""
+    root = os.path.abspath("../../samples/nodejs")
+    p = _plan_for(root)
+    svc1 = plantypes.Service.new("svc1", "Any2Kube")
+    svc1.source_artifacts[plantypes.SOURCE_DIRECTORY_ARTIFACT] = ["foo/"]
+    svc2 = plantypes.Service.new("svc2", "Any2Kube")
+    svc2.source_artifacts[plantypes.SOURCE_DIRECTORY_ARTIFACT] = ["bar/"]
+    p.services = {"svc1": [svc1], "svc2": [svc2]}
+    want = plantypes.read_plan("testdata/expectedservicesfornodejsapp.yaml").services["nodejs"]
+    got = _strip_repo(Any2KubeTranslator().get_service_options(root, p))
+    assert_deep_equal(got, want)
 
 
 def test_nodejs_app_already_containerized(layout):
@@ -105,14 +119,14 @@ def test_m2kignore_dir_but_not_subdirs(layout):
     root = os.path.abspath("testdata/nodejsappwithm2kignorecase1")
     want = plantypes.read_plan("testdata/expectedservicesfornodejsappwithm2kignorecase1.yaml").services["includeme"]
     got = _strip_repo(Any2KubeTranslator().get_service_options(root, _plan_for(root)))
-    assert _svc_dump(got) == _svc_dump(want)
+    assert_deep_equal(got, want)
 
 
 def test_m2kignore_everything_but_one_subdir(layout):
     root = os.path.abspath("testdata/javamavenappwithm2kignorecase2")
     want = plantypes.read_plan("testdata/expectedservicesforjavamavenappwithm2kignorecase2.yaml").services["java-maven"]
     got = _strip_repo(Any2KubeTranslator().get_service_options(root, _plan_for(root, "java-maven-app")))
-    assert _svc_dump(got) == _svc_dump(want)
+    assert_deep_equal(got, want)
 
 
 def test_m2kignore_include_dir_ignore_subdirs(tmp_path, assets_dir):
@@ -130,31 +144,53 @@ def test_multiple_hierarchical_m2kignores(tmp_path, assets_dir):
     assert Any2KubeTranslator().get_service_options(root, plantypes.new_plan()) == []
 
 
+# --- TestTranslate -----------------------------------------------------------------------
+
 def test_translate_no_services(assets_dir):
     p = plantypes.new_plan()
-    ir = Any2KubeTranslator().translate([], p)
-    assert ir.services == {} and ir.containers == [] and ir.storages == []
+    assert_deep_equal(Any2KubeTranslator().translate([], p), irtypes.new_ir(p))
+
+
+_GO_K8S_KEYS = {"containers": "containers", "name": "name", "image": "image", "ports": "ports",
+                "containerport": "containerPort"}
+
+
+def _go_yaml_k8s(v):
+    """A k8s struct as go-yaml fills it: keys are lowercased Go field names;
+    here they go back to the object's JSON names."""
+    if isinstance(v, dict):
+        return {_GO_K8S_KEYS[k]: _go_yaml_k8s(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_go_yaml_k8s(x) for x in v]
+    return v
+
+
+def _go_yaml_ir(d):
+    """irtypes.IR as common.ReadYaml fills it from expectedirfornodejsapp.yaml
+    (fields the file leaves out are zero: NewIR's empty values, EquateEmpty)."""
+    ir = irtypes.new_ir(plantypes.new_plan())
+    ir.name = d["name"]
+    for name, sd in d["services"].items():
+        s = irtypes.Service(sd["name"])
+        s.pod_spec = _go_yaml_k8s(sd["podspec"])
+        s.port_forwardings = [irtypes.PortForwarding(irtypes.Port(f["serviceport"]["number"]),
+                                                     irtypes.Port(f["podport"]["number"]))
+                              for f in sd["servicetopodportforwardings"]]
+        ir.services[name] = s
+    for cd in d["containers"]:
+        c = irtypes.Container(cd["containerbuildtype"], "", cd["new"])
+        c.image_names = cd["imagenames"]
+        c.new_files = cd["newfiles"]
+        c.exposed_ports = cd["exposedports"]
+        c.user_id = cd["userid"]
+        ir.containers.append(c)
+    ir.kubernetes = plantypes.KubernetesOutput.from_yaml(d["kubernetes"])
+    return ir
 
 
 def test_translate_nodejs_services_to_ir():
-    data = yamlio.load_raw(open(os.path.join(SRC_TESTDATA, "datafortestingtranslate", "servicesfromnodejsapp.yaml")).read())
+    td = os.path.join(SRC_TESTDATA, "datafortestingtranslate")
+    data = yamlio.load_raw(open(os.path.join(td, "servicesfromnodejsapp.yaml")).read())
     services = [plantypes.Service.from_yaml(d) for d in data]
-    want = yamlio.load(open(os.path.join(SRC_TESTDATA, "datafortestingtranslate", "expectedirfornodejsapp.yaml")).read())
-    ir = Any2KubeTranslator().translate(services, plantypes.new_plan())
-    assert ir.name == want["name"]
-    assert sorted(ir.services) == sorted(want["services"]) == ["nodejs"]
-    s = ir.services["nodejs"]
-    ws = want["services"]["nodejs"]
-    assert s.containers == [{"name": "nodejs", "image": "nodejs:latest", "ports": [{"containerPort": 8080}]}]
-    assert ws["podspec"]["containers"][0]["ports"][0]["containerport"] == 8080
-    assert [(f.service_port.number, f.pod_port.number) for f in s.port_forwardings] == [(8080, 8080)]
-    assert len(ir.containers) == 1
-    c, wc = ir.containers[0], want["containers"][0]
-    assert c.container_build_type == wc["containerbuildtype"]
-    assert c.image_names == wc["imagenames"]
-    assert c.new is True and c.exposed_ports == wc["exposedports"] and c.user_id == wc["userid"]
-    assert sorted(c.new_files) == sorted(wc["newfiles"])
-    # byte for byte, license header included
-    assert c.new_files["nodejs-cnb-build.sh"] == wc["newfiles"]["nodejs-cnb-build.sh"]
-    assert ir.kubernetes.artifact_type == want["kubernetes"]["artifactType"]
-    assert ir.kubernetes.target_cluster_type == want["kubernetes"]["targetCluster"]["type"]
+    want = _go_yaml_ir(yamlio.load(open(os.path.join(td, "expectedirfornodejsapp.yaml")).read()))
+    assert_deep_equal(Any2KubeTranslator().translate(services, plantypes.new_plan()), want)

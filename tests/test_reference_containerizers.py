@@ -1,4 +1,6 @@
-"""Containerizer GetContainer parity (``internal/containerizer/*_test.go`` fixtures)."""
+"""``internal/containerizer/{dockerfile,s2i,reuse,manual}containerizer_test.go``,
+one pytest per Go subtest: the returned container is compared whole with the
+fixture's (or ``NewContainer``'s), as ``cmp.Equal`` does."""
 
 import os
 import shutil
@@ -6,6 +8,7 @@ import shutil
 import pytest
 
 from conftest import ref_path
+from goequal import assert_deep_equal
 from move2kube_amd.containerizer.base import ContainerizerError
 from move2kube_amd.containerizer.dockerfile import DockerfileContainerizer
 from move2kube_amd.containerizer.manual import ManualContainerizer
@@ -39,75 +42,68 @@ def _case(kind, case):
     return plan, service, want
 
 
-def _check(cont, want):
-    assert cont.container_build_type == want["containerbuildtype"]
-    assert cont.image_names == want["imagenames"]
-    assert cont.new == want["new"]
-    assert cont.exposed_ports == want["exposedports"]
-    assert cont.user_id == want["userid"]
-    assert cont.accessed_dirs == (want.get("accesseddirs") or [])
-    assert cont.repo_info.target_path == want["repoinfo"]["targetPath"]
-    assert sorted(cont.new_files) == sorted(want["newfiles"])
-    # byte for byte, license headers included (the fixtures are the reference's output)
-    for k, v in want["newfiles"].items():
-        assert cont.new_files[k] == v, k
+def _go_yaml_container(d):
+    """irtypes.Container as mustreadyaml fills it from container.yaml (go-yaml:
+    lowercased field names; RepoInfo keeps its yaml tags)."""
+    c = irtypes.Container(d.get("containerbuildtype", ""), "", bool(d.get("new")))
+    c.image_names = list(d.get("imagenames") or [])
+    c.repo_info = plantypes.RepoInfo.from_yaml(d.get("repoinfo") or {})
+    c.new_files = dict(d.get("newfiles") or {})
+    c.exposed_ports = list(d.get("exposedports") or [])
+    c.user_id = d.get("userid", 0)
+    c.accessed_dirs = list(d.get("accesseddirs") or [])
+    return c
 
 
-def test_dockerfile_normal(layout):
+def test_dockerfile_get_container_for_the_sample_nodejs_app(layout):
     plan, _, want = _case("dockerfilecontainerizer", "normal")
-    service = plan.services["dockerfile"][0]
-    cz = DockerfileContainerizer()
-    cont = cz.get_container(plan, service)
-    _check(cont, want)
+    cont = DockerfileContainerizer().get_container(plan, plan.services["dockerfile"][0])
+    assert_deep_equal(cont, _go_yaml_container(want))
 
 
-@pytest.mark.parametrize("case", ["incorrectservice", "incorrectbuilder"])
+@pytest.mark.parametrize("case", [
+    pytest.param("incorrectservice", id="get container for the dockerfile sample when the service is wrong"),
+    pytest.param("incorrectbuilder", id="get container for the dockerfile sample when the container build type is wrong")])
 def test_dockerfile_errors(layout, case):
     plan, service, _ = _case("dockerfilecontainerizer", case)
     with pytest.raises(ContainerizerError):
         DockerfileContainerizer().get_container(plan, service)
 
 
-def test_s2i_normal(layout):
+def test_s2i_get_container_for_the_sample_nodejs_app(layout):
     plan, _, want = _case("s2icontainerizer", "normal")
-    service = plan.services["nodejs"][0]
-    cont = S2IContainerizer().get_container(plan, service)
-    _check(cont, want)
+    cont = S2IContainerizer().get_container(plan, plan.services["nodejs"][0])
+    assert_deep_equal(cont, _go_yaml_container(want))
 
 
-@pytest.mark.parametrize("case", ["incorrectservice", "incorrectbuilder"])
+@pytest.mark.parametrize("case", [
+    pytest.param("incorrectservice", id="get container for the nodejs app when the service is wrong"),
+    pytest.param("incorrectbuilder", id="get container for the nodejs app when the container build type is wrong")])
 def test_s2i_errors(layout, case):
     plan, service, _ = _case("s2icontainerizer", case)
     with pytest.raises(ContainerizerError):
         S2IContainerizer().get_container(plan, service)
 
 
-def test_reuse_normal(layout):
+def test_reuse_get_container_for_the_sample_nodejs_app(layout):
     plan, service, _ = _case("reusecontainerizer", "normal")
     cont = ReuseContainerizer().get_container(plan, service)
-    want = irtypes.new_container(plantypes.REUSE, service.image, False)
-    assert vars_of(cont) == vars_of(want)
+    assert_deep_equal(cont, irtypes.new_container(plantypes.REUSE, service.image, False))
 
 
-def test_reuse_error(layout):
+def test_reuse_get_container_when_the_service_is_wrong(layout):
     plan, service, _ = _case("reusecontainerizer", "incorrectservice")
     with pytest.raises(ContainerizerError):
         ReuseContainerizer().get_container(plan, service)
 
 
-def test_manual_normal(layout):
+def test_manual_get_container_for_the_sample_nodejs_app(layout):
     plan, service, _ = _case("manualcontainerizer", "normal")
     cont = ManualContainerizer().get_container(plan, service)
-    want = irtypes.new_container(plantypes.MANUAL, service.image, True)
-    assert vars_of(cont) == vars_of(want)
+    assert_deep_equal(cont, irtypes.new_container(plantypes.MANUAL, service.image, True))
 
 
-def test_manual_error(layout):
+def test_manual_get_container_when_the_service_is_wrong(layout):
     plan, service, _ = _case("manualcontainerizer", "incorrectservice")
     with pytest.raises(ContainerizerError):
         ManualContainerizer().get_container(plan, service)
-
-
-def vars_of(c):
-    return (c.container_build_type, c.image_names, c.new, c.new_files, c.exposed_ports, c.user_id, c.accessed_dirs,
-            c.repo_info.to_yaml())

@@ -7,17 +7,13 @@ import shutil
 import pytest
 
 from conftest import ref_path
+from goequal import assert_deep_equal
 from move2kube_amd import api, move2kube
 from move2kube_amd.models import plan as plantypes
 from move2kube_amd.utils import common
 from move2kube_amd.utils.constants import settings
 
 pytestmark = pytest.mark.reference
-
-
-def _dump(p):
-    from move2kube_amd.utils import yamlio
-    return yamlio.dump(p.to_yaml())
 
 
 def test_write_plan_roundtrip_is_byte_identical(tmp_path, assets_dir, monkeypatch):
@@ -43,7 +39,7 @@ def test_set_root_dir_matches_templated_fixture(tmp_path, assets_dir, monkeypatc
     want_yaml = common.get_string_from_template(tpl, {"PWD": str(cwd), "TempDir": settings.temp_path})
     from move2kube_amd.utils import yamlio
     want = plantypes.Plan.from_yaml(yamlio.load_raw(want_yaml))
-    assert _dump(p) == _dump(want)
+    assert_deep_equal(p, want)
 
 
 def test_set_root_dir_and_back(tmp_path, assets_dir, monkeypatch):
@@ -55,15 +51,22 @@ def test_set_root_dir_and_back(tmp_path, assets_dir, monkeypatch):
     orig = plantypes.read_plan(fixture)
     p.set_root_dir(os.path.abspath("new/root/directory"))
     p.set_root_dir(os.path.abspath("../../samples/nodejs"))
-    assert _dump(p) == _dump(orig)
+    assert_deep_equal(p, orig)
 
 
-def test_create_plan_for_empty_dir(tmp_path, assets_dir):
-    p = move2kube.create_plan(str(tmp_path), "project1")
+@pytest.mark.parametrize("with_cache_dir", [
+    pytest.param(False, id="create plan for empty app and without the cache folder"),
+    pytest.param(True, id="create plan for empty app")])
+def test_create_plan_for_empty_dir(tmp_path, assets_dir, with_cache_dir):
+    app = tmp_path / "app"
+    app.mkdir()
+    if with_cache_dir:
+        os.makedirs(settings.assets_path, exist_ok=True)
+    p = move2kube.create_plan(str(app), "project1")
     want = plantypes.new_plan()
     want.name = "project1"
-    want.set_root_dir(str(tmp_path))
-    assert _dump(p) == _dump(want)
+    want.set_root_dir(str(app))
+    assert_deep_equal(p, want)
 
 
 def test_create_plan_for_reference_nodejs_sample(tmp_path, monkeypatch):
@@ -81,7 +84,7 @@ def test_create_plan_for_reference_nodejs_sample(tmp_path, monkeypatch):
     # the CNB option needs a Docker daemon (the reference test needs one too)
     for name in want.services:
         want.services[name] = [s for s in want.services[name] if s.container_build_type != plantypes.CNB]
-    assert _dump(actual) == _dump(want)
+    assert_deep_equal(actual, want)
 
 
 def test_create_plan_for_reference_nodejs_sample_with_cnb(tmp_path, monkeypatch):
@@ -105,4 +108,4 @@ def test_create_plan_for_reference_nodejs_sample_with_cnb(tmp_path, monkeypatch)
         for svc in services:
             svc.repo_info = plantypes.RepoInfo()
     assert [s.container_build_type for s in actual.services["nodejs"]] == ["NewDockerfile", "S2I", "CNB"]
-    assert _dump(actual) == _dump(want)
+    assert_deep_equal(actual, want)

@@ -1,13 +1,15 @@
-"""QA engine parity (``internal/qaengine/{cache,default,}engine_test.go``)."""
+"""``internal/qaengine/{cache,default,}engine_test.go``, one pytest per Go
+subtest, plus engine behaviour beyond them."""
 
 import pytest
 
 from conftest import ref_path
+from goequal import assert_deep_equal
 from move2kube_amd import qaengine
 from move2kube_amd.models import qa
 from move2kube_amd.qaengine.cache_engine import CacheEngine
 from move2kube_amd.qaengine.default_engine import DefaultEngine
-from move2kube_amd.utils import yamlio
+from move2kube_amd.utils import constants, yamlio
 
 CACHE = ref_path("internal", "qaengine", "testdata", "qaenginetest.yaml")
 
@@ -21,14 +23,16 @@ def cache_engine(tmp_path):
     qaengine.reset()
 
 
+# --- cacheengine_test.go: TestCacheEngine --------------------------------------------
+
 @pytest.mark.reference
-def test_cache_input(cache_engine):
+def test_cache_new_input_problem(cache_engine):
     p = qa.new_input_problem("Enter the container registry username : ", ["Enter username for container registry login"], "")
     assert qaengine.fetch_answer(p).get_string_answer() == "testuser"
 
 
 @pytest.mark.reference
-def test_cache_select(cache_engine):
+def test_cache_new_select_problem(cache_engine):
     p = qa.new_select_problem("What type of container registry login do you want to use?",
                               ["Docker login from config mode, will use the default config from your local machine."],
                               "No authentication", ["Use existing pull secret", "No authentication", "UserName/Password"])
@@ -36,25 +40,26 @@ def test_cache_select(cache_engine):
 
 
 @pytest.mark.reference
-def test_cache_multiline(cache_engine):
+def test_cache_new_multiline_input_problem(cache_engine):
     p = qa.new_multiline_input_problem("Multiline input problem test description : ",
                                        ["Multiline input problem test context."], "")
     assert qaengine.fetch_answer(p).get_string_answer() == "line1 \nline2 \nline3 \n"
 
 
 @pytest.mark.reference
-def test_cache_confirm(cache_engine):
+def test_cache_new_confirm_problem(cache_engine):
     p = qa.new_confirm_problem("Confirm problem test description : ", ["Confirm input problem test context."], True)
     assert qaengine.fetch_answer(p).get_bool_answer() is True
 
 
 @pytest.mark.reference
-def test_cache_multiselect_and_write_cache(cache_engine):
+def test_cache_new_multi_select_problem(cache_engine):
     d = ["Option A", "Option C"]
     p = qa.new_multiselect_problem("MultiSelect input problem test description : ",
                                    ["MultiSelect input problem test context"], d,
                                    ["Option A", "Option B", "Option C", "Option D"])
-    assert qaengine.fetch_answer(p).get_slice_answer() == d
+    assert_deep_equal(qaengine.fetch_answer(p).get_slice_answer(), d)
+    # beyond Go: the write cache records the solution
     qaengine.flush_write_cache()
     written = yamlio.load(cache_engine.read_text())
     assert written["kind"] == "QACache"
@@ -74,14 +79,55 @@ def test_cache_regex_description_match(tmp_path):
     assert qaengine.fetch_answer(p).get_string_answer() == "quay.io"
 
 
-def test_default_engine_answers():
+# --- defaultengine_test.go: TestDefaultEngine --------------------------------------------
+
+@pytest.fixture
+def default_engine():
     qaengine.reset()
     qaengine.add_engine(DefaultEngine())
-    assert qaengine.fetch_answer(qa.new_input_problem("in", [], "def")).get_string_answer() == "def"
-    assert qaengine.fetch_answer(qa.new_select_problem("sel", [], "b", ["a", "b"])).get_string_answer() == "b"
-    assert qaengine.fetch_answer(qa.new_multiselect_problem("ms", [], ["a"], ["a", "b"])).get_slice_answer() == ["a"]
-    assert qaengine.fetch_answer(qa.new_confirm_problem("c", [], True)).get_bool_answer() is True
-    assert qaengine.fetch_answer(qa.new_multiline_input_problem("ml", [], "x\ny")).get_string_answer() == "x\ny"
+    yield
+    qaengine.reset()
+
+
+def test_default_new_input_problem(default_engine):
+    p = qa.new_input_problem("Enter the name of the registry : ", ["Ex : " + constants.DEFAULT_REGISTRY_URL],
+                             constants.DEFAULT_REGISTRY_URL)
+    assert qaengine.fetch_answer(p).get_string_answer() == constants.DEFAULT_REGISTRY_URL
+
+
+def test_default_new_select_problem(default_engine):
+    p = qa.new_select_problem("Test description", ["Test context"], "Option B", ["Option A", "Option B", "Option C"])
+    assert qaengine.fetch_answer(p).get_string_answer() == "Option B"
+
+
+def test_default_new_multi_select_problem(default_engine):
+    d = ["Option A", "Option C"]
+    p = qa.new_multiselect_problem("Test description", ["Test context"], d,
+                                   ["Option A", "Option B", "Option C", "Option D"])
+    assert_deep_equal(qaengine.fetch_answer(p).get_slice_answer(), d)
+
+
+def test_default_new_confirm_problem(default_engine):
+    p = qa.new_confirm_problem("Test description", ["Test context"], True)
+    assert qaengine.fetch_answer(p).get_bool_answer() is True
+
+
+def test_default_new_multiline_input_problem(default_engine):
+    d = "line1\n\t\tline2\n\t\tline3"
+    p = qa.new_multiline_input_problem("Test description", ["Test context"], d)
+    assert qaengine.fetch_answer(p).get_string_answer() == d
+
+
+# --- engine_test.go: TestEngine ---------------------------------------------------------------
+
+def test_add_engine():
+    qaengine.reset()
+    try:
+        qaengine.add_engine(DefaultEngine())
+        assert len(qaengine.engines()) == 1
+        assert_deep_equal(qaengine.engines()[0], DefaultEngine())
+    finally:
+        qaengine.reset()
 
 
 def test_caches_are_prepended_and_last_added_wins(tmp_path):
