@@ -26,13 +26,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("config")
     ap.add_argument("--runs", type=int, default=15)
+    ap.add_argument("--tree", default=refconfigs.ROOT, help="the source tree to run (e.g. .ab_base/r04)")
     a = ap.parse_args()
     root, _ = refconfigs.workdir_root("auto")
     work = tempfile.mkdtemp(prefix="m2k-coldtrace-", dir=root)
     try:
         run = refconfigs.Run(a.config, work).prepare()
         env = run.env()
-        env["PYTHONPATH"] = refconfigs.ROOT
+        env["PYTHONPATH"] = os.path.abspath(a.tree)
         cmds = run.cli_commands()
         spans, walls = {}, []
         for i in range(a.runs + 1):  # the first run primes the bytecode and page caches

@@ -50,7 +50,8 @@ CF_APP = os.path.join(FIXTURES, "extra_samples", "cfapp")
 GOLDEN_REF = os.path.join(ROOT, "tests", "golden", "reference")
 PROJECT = "myproject"  # the CLI default (-n)
 
-# name -> (layout, source dir relative to <work>, QA caches, CNB probing on, collect annotations)
+# name -> (layout, source dir relative to <work>, QA caches, CNB probing on, collect annotations
+#          [, extra environment])
 CONFIGS = {
     "golang": ("samples", "samples/golang", [], False, None),
     "docker-compose": ("samples", "samples/docker-compose", [], False, None),
@@ -75,6 +76,8 @@ GOLDEN_COVERAGE = os.path.join(GOLDEN_REF, "coverage")
 CARRIED_OVER = os.path.join(FIXTURES, "carried_over")
 CARRIED_OVER_KINDS = os.path.join(FIXTURES, "carried_over_kinds")
 GIT_REPOS = os.path.join(FIXTURES, "git_repos")
+STORAGE_CLASS = os.path.join(FIXTURES, "storage_class")
+FIXED = {"M2K_COMPAT": "fixed"}
 Q_ARTIFACT = "Choose the artifact type:"
 Q_CLUSTER = "Choose the cluster type:"
 
@@ -99,6 +102,15 @@ def _coverage_configs():
         out["carried-over-kinds/" + p] = ("carried-kinds", "carried", {Q_CLUSTER: p}, False, None)
     # source trees that are git repos with an origin remote
     out["git-repos"] = ("git", "git", {}, False, None)
+    # two compose services with a named volume each: two PVCs, one storage
+    # class question for all of them (the reference assigns
+    # the answer to a loop copy, so no PVC gets it)
+    out["storage-class"] = ("storage", "storage", {}, False, None)
+    # M2K_COMPAT=fixed wherever it changes bytes (DEVIATIONS.md section 5):
+    # cf (app2 containerized as Manual, Manualimages.md written) and the
+    # storage class applied to the PVCs
+    out["compat-fixed/cf"] = ("cf", "cf", {}, True, ["cf"], FIXED)
+    out["compat-fixed/storage-class"] = ("storage", "storage", {}, False, None, FIXED)
     return out
 
 
@@ -141,7 +153,8 @@ class Run:
     def __init__(self, name, work):
         self.name = name
         self.work = os.path.abspath(work)
-        layout, src, caches, cnb, collect = _lookup(name)
+        layout, src, caches, cnb, collect, *extra = _lookup(name)
+        self.extra_env = dict(extra[0]) if extra else {}
         self.layout = layout
         self.src = os.path.join(self.work, src)
         self.answers = caches if isinstance(caches, dict) else None
@@ -177,6 +190,8 @@ class Run:
             shutil.copytree(CARRIED_OVER_KINDS, self.src, symlinks=True)
         elif self.layout == "git":
             _copy_git_repos(self.src)
+        elif self.layout == "storage":
+            shutil.copytree(STORAGE_CLASS, self.src, symlinks=True)
         if self.answers:
             with open(self.caches[0], "w") as f:
                 f.write(qacache_text(self.answers))
@@ -189,15 +204,21 @@ class Run:
         env["HOME"] = self.home
         env["M2K_NO_NETWORK"] = "1"
         env["M2K_DISABLE_CNB"] = "0" if self.cnb else "1"
+        env.update(self.extra_env)
         return env
 
     # -- in-process -------------------------------------------------------
     def apply_env(self):
         """Switch this process to the configuration's environment; returns an undo."""
-        saved = {k: os.environ.get(k) for k in ("PATH", "HOME", "M2K_NO_NETWORK", "M2K_DISABLE_CNB")}
+        keys = ("PATH", "HOME", "M2K_NO_NETWORK", "M2K_DISABLE_CNB") + tuple(self.extra_env)
+        saved = {k: os.environ.get(k) for k in keys}
         os.environ.update(self.env())
+        from move2kube_amd.utils.constants import settings
+        saved_compat = settings.compat
+        settings.compat = os.environ.get("M2K_COMPAT", "reference")   # read once at start-up by the CLI
 
         def restore():
+            settings.compat = saved_compat
             for k, v in saved.items():
                 if v is None:
                     os.environ.pop(k, None)

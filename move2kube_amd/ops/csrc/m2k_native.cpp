@@ -11,6 +11,7 @@
 //   sniff_dockerfiles()  multi-threaded "first non-ARG instruction" scan
 //   run_commands()       bounded-parallel posix_spawn pool with captured stdout
 //   proc_spawn/wait      one external tool without the subprocess module (proc_spawn.cpp)
+//   procgroup_*          several tools waited for together in one poll loop (proc_spawn.cpp)
 //   crc64_ecma/fnv64a    naming hashes (utils.go:292, compose/utils.go:121)
 //   edit_distance_batch  weighted edit distance matrix (bit-parallel LCS for 1,1,2)
 //   closest_batch        fused argmin over options for every query
@@ -928,6 +929,21 @@ static py::object schema_marshal(py::object obj, py::object type_name) {
 extern "C" PyObject* m2k_proc_spawn(PyObject* argv, PyObject* cwd, long out_mode, long err_mode);
 extern "C" PyObject* m2k_proc_wait(long pid, long out_fd, long err_fd, double timeout_s);
 
+extern "C" PyObject* m2k_procgroup_new();
+extern "C" PyObject* m2k_procgroup_add(PyObject* cap, long key, long pid, long out_fd, long err_fd, double timeout_s);
+extern "C" PyObject* m2k_procgroup_wait_any(PyObject* cap);
+
+static py::object steal_or_throw(PyObject* r) {
+  if (!r) throw py::error_already_set();
+  return py::reinterpret_steal<py::object>(r);
+}
+
+static py::object procgroup_new() { return steal_or_throw(m2k_procgroup_new()); }
+static py::object procgroup_add(py::object g, long key, long pid, long out_fd, long err_fd, double timeout_s) {
+  return steal_or_throw(m2k_procgroup_add(g.ptr(), key, pid, out_fd, err_fd, timeout_s));
+}
+static py::object procgroup_wait_any(py::object g) { return steal_or_throw(m2k_procgroup_wait_any(g.ptr())); }
+
 static py::object proc_spawn(py::object argv, py::object cwd, long out_mode, long err_mode) {
   PyObject* r = m2k_proc_spawn(argv.ptr(), cwd.ptr(), out_mode, err_mode);
   if (!r) throw py::error_already_set();
@@ -963,6 +979,10 @@ PYBIND11_MODULE(_m2k_native, m) {
   m.def("schema_marshal", &schema_marshal, py::arg("obj"), py::arg("type_name"));
   m.def("proc_spawn", &proc_spawn, py::arg("argv"), py::arg("cwd"), py::arg("stdout"), py::arg("stderr"));
   m.def("proc_wait", &proc_wait, py::arg("pid"), py::arg("out_fd"), py::arg("err_fd"), py::arg("timeout_s"));
+  m.def("procgroup_new", &procgroup_new);
+  m.def("procgroup_add", &procgroup_add, py::arg("group"), py::arg("key"), py::arg("pid"), py::arg("out_fd"),
+        py::arg("err_fd"), py::arg("timeout_s"));
+  m.def("procgroup_wait_any", &procgroup_wait_any, py::arg("group"));
   m.def("run_commands", &run_commands, py::arg("argvs"), py::arg("cwds"), py::arg("parallel") = 8,
         py::arg("timeout_s") = 0.0);
 }

@@ -246,3 +246,175 @@ extern "C" PyObject *m2k_proc_wait(long pid_l, long out_fd_l, long err_fd_l, dou
   return Py_BuildValue("(iy#y#O)", returncode_of(status), bufs[0].data(), (Py_ssize_t)bufs[0].size(),
                        bufs[1].data(), (Py_ssize_t)bufs[1].size(), timed_out ? Py_True : Py_False);
 }
+
+// ---------------------------------------------------------------------------
+// A group of running children waited for together (utils/proc.run_many):
+//
+//   procgroup_new() -> group
+//   procgroup_add(group, key, pid, out_rfd, err_rfd, timeout_s)
+//   procgroup_wait_any(group) -> (key, returncode, out, err, timed_out), or
+//       None when the group is empty
+//
+// One poll() covers the pipes and pidfds of every live member, so all of them
+// drain at once (none blocks on a full pipe while another is waited for), each
+// member's deadline counts from its add, and wait_any returns the first member
+// that has exited and closed its pipes -- the caller can start the next child
+// at once.  No threads, no GIL held while waiting.  A group dropped with live
+// members kills and reaps them.
+// ---------------------------------------------------------------------------
+
+namespace {
+
+struct Member {
+  long key;
+  pid_t pid;
+  int fds[2];
+  int pidfd;
+  double deadline;  // 0: none
+  std::string bufs[2];
+  bool reaped = false, timed_out = false;
+  int status = 0;
+};
+
+struct ProcGroup {
+  std::vector<Member> members;
+  ~ProcGroup() {
+    for (auto &m : members) {
+      if (!m.reaped) {
+        kill(m.pid, SIGKILL);
+        int st;
+        waitpid(m.pid, &st, 0);
+      }
+      close_quiet(m.fds[0]);
+      close_quiet(m.fds[1]);
+      close_quiet(m.pidfd);
+    }
+  }
+};
+
+const char *kGroupName = "m2k.procgroup";
+
+void group_free(PyObject *cap) {
+  delete static_cast<ProcGroup *>(PyCapsule_GetPointer(cap, kGroupName));
+}
+
+ProcGroup *group_of(PyObject *cap) {
+  return static_cast<ProcGroup *>(PyCapsule_GetPointer(cap, kGroupName));
+}
+
+void reap_nohang(Member &m) {
+  if (m.reaped) return;
+  pid_t w = waitpid(m.pid, &m.status, WNOHANG);
+  if (w == m.pid || (w < 0 && errno == ECHILD)) {
+    m.reaped = true;
+    close_quiet(m.pidfd);
+  }
+}
+
+void kill_member(Member &m) {
+  if (!m.reaped) {
+    kill(m.pid, SIGKILL);
+    waitpid(m.pid, &m.status, 0);
+    m.reaped = true;
+    close_quiet(m.pidfd);
+  }
+}
+
+}  // namespace
+
+extern "C" PyObject *m2k_procgroup_new() {
+  return PyCapsule_New(new ProcGroup(), kGroupName, group_free);
+}
+
+extern "C" PyObject *m2k_procgroup_add(PyObject *cap, long key, long pid, long out_fd, long err_fd,
+                                       double timeout_s) {
+  ProcGroup *g = group_of(cap);
+  if (!g) return nullptr;
+  Member m;
+  m.key = key;
+  m.pid = (pid_t)pid;
+  m.fds[0] = (int)out_fd;
+  m.fds[1] = (int)err_fd;
+  m.pidfd = pidfd_for(m.pid);
+  m.deadline = timeout_s > 0 ? mono_s() + timeout_s : 0;
+  g->members.push_back(std::move(m));
+  Py_RETURN_NONE;
+}
+
+extern "C" PyObject *m2k_procgroup_wait_any(PyObject *cap) {
+  ProcGroup *g = group_of(cap);
+  if (!g) return nullptr;
+  if (g->members.empty()) Py_RETURN_NONE;
+  size_t done = (size_t)-1;
+  int interrupted = 0;
+  Py_BEGIN_ALLOW_THREADS
+  std::vector<struct pollfd> pf;
+  std::vector<std::pair<size_t, int>> who;  // (member, 0/1 pipe, 2 pidfd)
+  for (;;) {
+    for (size_t i = 0; i < g->members.size() && done == (size_t)-1; i++) {
+      Member &m = g->members[i];
+      reap_nohang(m);
+      if (m.reaped && m.fds[0] < 0 && m.fds[1] < 0) done = i;
+    }
+    if (done != (size_t)-1) break;
+    double now = mono_s();
+    int wait_ms = 100;
+    for (size_t i = 0; i < g->members.size() && done == (size_t)-1; i++) {
+      Member &m = g->members[i];
+      if (m.deadline > 0 && m.deadline <= now) {
+        kill_member(m);
+        m.timed_out = true;
+        done = i;
+      } else if (m.deadline > 0 && (m.deadline - now) * 1000 < wait_ms) {
+        wait_ms = (int)((m.deadline - now) * 1000) + 1;
+      }
+      if (!m.reaped && m.pidfd < 0 && wait_ms > 2) wait_ms = 2;  // no pidfd: poll the exit
+    }
+    if (done != (size_t)-1) break;
+    pf.clear();
+    who.clear();
+    for (size_t i = 0; i < g->members.size(); i++) {
+      Member &m = g->members[i];
+      for (int k = 0; k < 2; k++)
+        if (m.fds[k] >= 0) {
+          pf.push_back({m.fds[k], POLLIN, 0});
+          who.push_back({i, k});
+        }
+      if (!m.reaped && m.pidfd >= 0) {
+        pf.push_back({m.pidfd, POLLIN, 0});
+        who.push_back({i, 2});
+      }
+    }
+    int pr = poll(pf.data(), (nfds_t)pf.size(), wait_ms);
+    if (pr < 0 && errno == EINTR) {
+      Py_BLOCK_THREADS
+      interrupted = PyErr_CheckSignals();
+      Py_UNBLOCK_THREADS
+      if (interrupted) break;
+      continue;
+    }
+    for (size_t j = 0; j < pf.size() && pr > 0; j++) {
+      if (who[j].second == 2 || !(pf[j].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+      Member &m = g->members[who[j].first];
+      int k = who[j].second;
+      char buf[65536];
+      ssize_t r = read(m.fds[k], buf, sizeof(buf));
+      if (r > 0)
+        m.bufs[k].append(buf, (size_t)r);
+      else if (r == 0 || (errno != EINTR && errno != EAGAIN))
+        close_quiet(m.fds[k]);
+    }
+  }
+  Py_END_ALLOW_THREADS
+  if (interrupted) {  // Ctrl-C: every member is killed, as proc_wait does for its one child
+    for (auto &m : g->members) kill_member(m);
+    return nullptr;
+  }
+  Member m = std::move(g->members[done]);
+  g->members.erase(g->members.begin() + (long)done);
+  close_quiet(m.fds[0]);
+  close_quiet(m.fds[1]);
+  close_quiet(m.pidfd);
+  return Py_BuildValue("(liy#y#O)", m.key, returncode_of(m.status), m.bufs[0].data(), (Py_ssize_t)m.bufs[0].size(),
+                       m.bufs[1].data(), (Py_ssize_t)m.bufs[1].size(), m.timed_out ? Py_True : Py_False);
+}

@@ -120,15 +120,50 @@ def run(argv, cwd=None, stdout=PIPE, stderr=DEVNULL, timeout=None):
 def run_many(argvs, parallel=None, cwd=None, stdout=PIPE, stderr=DEVNULL, timeout=None):
     """``[run(a, ...) for a in argvs]`` with up to ``parallel`` children alive
     at once (all of them by default); a raised error is returned in its slot.
-    Each child is waited for on its own thread from the moment it starts (the
-    native wait releases the GIL), so every live child's pipes drain at once,
-    its deadline counts from its start, and a slot is refilled as soon as any
-    child exits."""
-    import queue
-    import threading
+    Every live child's pipes drain at once, its deadline counts from its start,
+    and a slot is refilled as soon as any child exits: natively one poll loop
+    over all of them (``procgroup_*``, ``ops/csrc/proc_spawn.cpp``), otherwise
+    one waiting thread per child."""
     n = len(argvs)
     if parallel is None or parallel < 1:
         parallel = n
+    m = native.module()
+    if m is not None and hasattr(m, "procgroup_new"):
+        return _run_many_native(m, argvs, parallel, cwd, stdout, stderr, timeout)
+    return _run_many_threads(argvs, parallel, cwd, stdout, stderr, timeout)
+
+
+def _run_many_native(m, argvs, parallel, cwd, stdout, stderr, timeout):
+    n = len(argvs)
+    out = [None] * n
+    group = m.procgroup_new()
+    live = 0
+    nxt = 0
+    while nxt < n or live:
+        while nxt < n and live < parallel:
+            try:
+                c = spawn(argvs[nxt], cwd=cwd, stdout=stdout, stderr=stderr)
+            except OSError as e:
+                out[nxt] = e
+            else:
+                ofd, efd, c._out_fd, c._err_fd = c._out_fd, c._err_fd, -1, -1   # the group owns them now
+                m.procgroup_add(group, nxt, c.pid, ofd, efd, float(timeout or 0))
+                out[nxt] = c
+                live += 1
+            nxt += 1
+        if live:
+            i, rc, o, e, timed_out = m.procgroup_wait_any(group)
+            c = out[i]
+            r = c._done = Completed(c.args, rc, o if c._pipes[0] else None, e if c._pipes[1] else None, timed_out)
+            out[i] = _timeout_error(r, timeout) if timed_out else r
+            live -= 1
+    return out
+
+
+def _run_many_threads(argvs, parallel, cwd, stdout, stderr, timeout):
+    import queue
+    import threading
+    n = len(argvs)
     out = [None] * n
     done = queue.SimpleQueue()
 

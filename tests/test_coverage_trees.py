@@ -10,7 +10,11 @@ configurations (``benchmarks/refconfigs.py:COVERAGE_CONFIGS``):
   handlers and the GroupVersion conversion of ``k8stransformer.go:106-141``;
 * ``git-repos``: source trees that are git repos with remotes
   (``dockerfile2kube.go:146-263``, ``types/plan/plan.go:232-272``,
-  ``tektonapiresourceset.go:203-286``, ``pipeline.go:78-143``).
+  ``tektonapiresourceset.go:203-286``, ``pipeline.go:78-143``);
+* ``storage-class``: two compose services with a named volume each
+  (``v3.go:405-470``, ``storagecustomizer.go:40-80``);
+* ``compat-fixed/*``: ``M2K_COMPAT=fixed`` where it changes bytes
+  (``cf``, ``storage-class``; DEVIATIONS.md section 5).
 
 The trees were written by ``python benchmarks/refconfigs.py --write`` and
 audited file class by file class (``tests/golden/reference/PROVENANCE.md``);
@@ -46,6 +50,33 @@ def test_coverage_tree_matches_expected(name, tmp_path):
     golden = refconfigs.golden_dir(name)
     assert os.path.isdir(golden), golden
     assert refconfigs.diff_files(out, golden, work=run.work) == []
+
+
+# files in which a fixed-mode tree differs from its reference-mode counterpart
+# (DEVIATIONS.md section 5)
+COMPAT_FIXED = {
+    "compat-fixed/cf": (os.path.join(refconfigs.GOLDEN_REF, "cf"), {
+        "Manualimages.md", "NOTES.txt", "cicd/myproject-clone-build-push-pipeline.yaml", "docker-compose.yaml",
+        "m2kqacache.yaml", "myproject/app2-deployment.yaml", "myproject/app2-service.yaml",
+        "myproject/myproject-ingress.yaml"}),
+    "compat-fixed/storage-class": (refconfigs.golden_dir("storage-class"), {
+        "myproject/cachedata-persistentvolumeclaim.yaml", "myproject/dbdata-persistentvolumeclaim.yaml"}),
+}
+
+
+@pytest.mark.parametrize("name", sorted(COMPAT_FIXED))
+def test_compat_fixed_trees_differ_only_where_documented(name):
+    counterpart, files = COMPAT_FIXED[name]
+    assert refconfigs.diff_files(refconfigs.golden_dir(name), counterpart) == sorted(files)
+    dev = open(os.path.join(refconfigs.GOLDEN_REF, "DEVIATIONS.md")).read()
+    assert "`%s`" % name.split("/", 1)[1] in dev.split("## 5.")[1].split("## 6.")[0]
+    if name == "compat-fixed/cf":
+        with open(os.path.join(refconfigs.golden_dir(name), "Manualimages.md")) as f:
+            assert f.read().rstrip().endswith("app2:latest")
+    else:
+        for f in files:
+            with open(os.path.join(refconfigs.golden_dir(name), f)) as fh:
+                assert yamlio.load(fh.read())["spec"]["storageClassName"] == "default"
 
 
 def _objects(name, sub="myproject"):

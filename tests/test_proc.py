@@ -128,9 +128,11 @@ def test_cold_tool_paths_do_not_import_subprocess(tmp_path):
             "from move2kube_amd.utils import common, proc\n"
             "r = common.run_tool(['/bin/echo', 'hi'], stdout=proc.PIPE)\n"
             "assert r.stdout == b'hi\\n'\n"
-            "print('subprocess' in sys.modules)\n" % root)
+            "rs = proc.run_many([['/bin/echo', 'a'], ['/bin/echo', 'b']], parallel=1)\n"
+            "assert [x.stdout for x in rs] == [b'a\\n', b'b\\n']\n"
+            "print([m for m in ('subprocess', 'queue') if m in sys.modules])\n" % root)
     p = subprocess.run([sys.executable, "-S", "-c", code], stdout=subprocess.PIPE, check=True)
-    assert p.stdout.strip() == b"False"
+    assert p.stdout.strip() == b"[]"   # run_many waits natively: no thread per child
 
 
 def test_child_gets_only_the_standard_descriptors(mode):

@@ -71,6 +71,24 @@ DRIVER = textwrap.dedent(r'''
             assert m.proc_wait(pid, o, e, 10.0) == (3, b"x\n", b"", False)
         pid, o, e = m.proc_spawn([b"/bin/sh", b"-c", b"exec sleep 5"], None, -2, -2)
         assert m.proc_wait(pid, o, e, 0.05)[3] is True
+        # procgroup_*: several children in one poll loop, one of them timing
+        # out, a big output, and a group dropped with a live member
+        g = m.procgroup_new()
+        for key, cmd, to in ((0, b"echo a; echo b >&2", 10.0), (1, b"exec sleep 5", 0.05),
+                             (2, b"head -c 300000 /dev/zero", 10.0)):
+            pid, o, e = m.proc_spawn([b"/bin/sh", b"-c", cmd], None, -1, -1)
+            m.procgroup_add(g, key, pid, o, e, to)
+        got = {}
+        while True:
+            r = m.procgroup_wait_any(g)
+            if r is None:
+                break
+            got[r[0]] = r
+        assert got[0][1:] == (0, b"a\n", b"b\n", False) and got[1][4] is True and len(got[2][2]) == 300000
+        g = m.procgroup_new()
+        pid, o, e = m.proc_spawn([b"/bin/sh", b"-c", b"exec sleep 5"], None, -1, -1)
+        m.procgroup_add(g, 0, pid, o, e, 0.0)
+        del g   # kills and reaps the sleeper
         try:
             m.proc_spawn([b"m2k-no-such-tool"], None, -1, -2)
         except FileNotFoundError:
