@@ -16,7 +16,8 @@ from move2kube_amd.utils import fastjson
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
 
-STALE_ON_BOX = ("argparse", "gettext", "locale", "json", "base64", "copy")
+STALE_ON_BOX = ("argparse", "gettext", "locale", "json", "base64", "copy",
+                "queue", "heapq")  # queue + heapq: 1.9 ms per process there (profiles/r05_perf2/cold_importtime.jsonl)
 
 _CHILD = """
 import sys
@@ -28,12 +29,19 @@ sys.exit(rc)
 """
 
 
-@pytest.mark.parametrize("config", ["golang", "docker-compose", "helm-openshift"])
+@pytest.mark.parametrize("config", ["golang", "docker-compose", "java-cnb", "cf", "helm-openshift"])
 def test_cold_translate_skips_stale_stdlib_modules(tmp_path, config):
     import refconfigs
     run = refconfigs.Run(config, str(tmp_path)).prepare()
     argv = run.cli_commands()[-1]
     env = run.env()
+    if len(run.cli_commands()) > 1:   # cf: collect first, its output copied into the source tree
+        env["PYTHONPATH"] = ROOT
+        import shutil
+        for argv0 in run.cli_commands()[:-1]:
+            subprocess.run([sys.executable, "-m", "move2kube_amd"] + argv0, env=env, cwd=str(tmp_path),
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True, timeout=120)
+        shutil.copytree(os.path.join(str(tmp_path), "collect", "m2k_collect"), os.path.join(run.src, "m2k_collect"))
     p = subprocess.run([sys.executable, "-c", _CHILD % (ROOT, argv, STALE_ON_BOX)], env=env, cwd=str(tmp_path),
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
