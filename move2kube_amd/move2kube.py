@@ -258,7 +258,7 @@ def _emit(p, ir, outpath, qadisablecli):
                       common.go_path_error(e, "unlinkat"))
             log.error("Anything in the output path will get overwritten.")
     try:
-        _emit_artifacts(p, ir, outpath, qadisablecli)
+        _emit_artifacts(p, ir, outpath, qadisablecli, remover[0].join if remover is not None else None)
     finally:
         if remover is not None:
             remover[0].join()
@@ -266,7 +266,7 @@ def _emit(p, ir, outpath, qadisablecli):
                 log.warning("Failed to remove the previous output: %s", e)
 
 
-def _emit_artifacts(p, ir, outpath, qadisablecli):
+def _emit_artifacts(p, ir, outpath, qadisablecli, join_remover=None):
     # For a Helm chart the main transformer starts operator-sdk once the chart
     # is written and waits for it at the end; the compose file, the CI/CD
     # objects (built and written) and the QA cache do not feed the chart, so
@@ -341,6 +341,10 @@ def _emit_artifacts(p, ir, outpath, qadisablecli):
         if overlap is not None:
             overlap.append(qaengine.flush_write_cache)
             t.overlap_work = overlap
+            # the previous tree is unlinked on a thread; let it finish before
+            # operator-sdk copies the chart: both on one tmpfs, the unlinks slow
+            # the tool's writes (box A/B, profiles/r05_rmab/remove_ab.jsonl)
+            t.before_operator = join_remover
         try:
             with trace.span(type(t).__name__ + ".write_objects", "transform"):
                 t.write_objects(outpath)

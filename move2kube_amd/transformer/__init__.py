@@ -192,6 +192,7 @@ class K8sTransformer(Transformer):
         self.exposed_service_paths = {}
         self.add_copy_sources_warning = False
         self.overlap_work = []  # callables run while operator-sdk runs (Helm only)
+        self.before_operator = None  # called just before operator-sdk starts (Helm only)
 
     def transform(self, ir):
         log.debug("Starting Kubernetes transform")
@@ -255,6 +256,8 @@ class K8sTransformer(Transformer):
         except OSError as e:
             log.error("Error occurred while writing transformed objects %s", e)
         if self.helm:
+            if self.before_operator is not None:
+                self.before_operator()
             operator = self.start_operator(self.name, outpath)
             try:
                 new_images = self._write_containers(outpath)

@@ -68,3 +68,32 @@ def test_large_output_does_not_block(tmp_path, monkeypatch, warnings_seen):
     assert started is not None
     assert K8sTransformer.finish_operator(started) is False
     assert warnings_seen and warnings_seen[0].count("\n") == 3000
+
+
+def test_previous_output_is_gone_before_operator_sdk_starts(tmp_path, monkeypatch):
+    """A Helm translate over an existing output: the old tree, unlinked on a
+    thread while the new one is built, is gone before operator-sdk starts
+    (the tool copies the chart on the same filesystem)."""
+    import sys
+    import threading
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "benchmarks"))
+    import refconfigs
+    run = refconfigs.Run("helm-openshift", str(tmp_path)).prepare()
+    seen = []
+    orig = K8sTransformer.start_operator
+
+    def start(project, basepath):
+        seen.append([t.name for t in threading.enumerate() if t.name == "m2k-remove-old-output"])
+        seen.append([n for n in os.listdir(os.path.dirname(os.path.abspath(basepath))) if ".m2k-old-" in n])
+        return orig(project, basepath)
+    monkeypatch.setattr(K8sTransformer, "start_operator", staticmethod(start))
+    undo = run.apply_env()
+    try:
+        with run.session() as s:
+            run.step(s)
+            seen.clear()
+            run.step(s)
+    finally:
+        undo()
+    assert seen == [[], []]
+    assert refconfigs.diff_files(run.out, refconfigs.golden_dir("helm-openshift"), work=run.work) == []
