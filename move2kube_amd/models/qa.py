@@ -513,13 +513,17 @@ class Cache:
         self.write_behind = False
         self.dirty = False
 
-    def to_yaml(self):
+    def _head(self):
         d = {}
         if self.api_version:
             d["apiVersion"] = self.api_version
         d["kind"] = self.kind
         if self.name:
             d["metadata"] = {"name": self.name}
+        return d
+
+    def to_yaml(self):
+        d = self._head()
         if self.problems:
             d["spec"] = {"solutions": [p.to_yaml() for p in self.problems]}
         return d
@@ -564,7 +568,7 @@ class Cache:
         :meth:`to_yaml` in one go."""
         if not self.problems:
             return yamlio.dump(self.to_yaml())
-        head = {k: v for k, v in self.to_yaml().items() if k != "spec"}
+        head = self._head()
         live = {id(p) for p in self.problems}
         for k in [k for k in self._chunks if k not in live]:
             del self._chunks[k]

@@ -425,9 +425,9 @@ class _State:
 
     # -- variables -------------------------------------------------------------
     def var_value(self, node, name):
-        for k in range(len(self.vars) - 1, -1, -1):
-            if self.vars[k][0] == name:
-                return self.vars[k][1]
+        for n, v in reversed(self.vars):   # exec.go varValue: innermost first
+            if n == name:
+                return v
         raise _exec_error(self, node, "undefined variable: %s" % name)
 
     def set_var(self, node, name, value):

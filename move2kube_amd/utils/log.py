@@ -73,8 +73,22 @@ class FatalError(RuntimeError):
     """Raised where the reference calls ``log.Fatalf``."""
 
 
+_stamp = (None, "")  # (whole second, its RFC3339 text): a run logs many lines per second
+
+
 def _rfc3339(t):
     """time.RFC3339 of a local time (logrus' default timestamp format)."""
+    global _stamp
+    sec = int(t)
+    cached = _stamp   # one tuple, replaced whole: threads never see a torn pair
+    if cached[0] == sec:
+        return cached[1]
+    text = _rfc3339_uncached(sec)
+    _stamp = (sec, text)
+    return text
+
+
+def _rfc3339_uncached(t):
     lt = time.localtime(t)
     off = lt.tm_gmtoff
     stamp = time.strftime("%Y-%m-%dT%H:%M:%S", lt)
