@@ -185,3 +185,16 @@ def _tar_members(b64):
     import tarfile
     with tarfile.open(fileobj=io.BytesIO(base64.b64decode(b64)), mode="r:") as tr:
         return [(m.name, m.size) for m in tr]
+
+
+@pytest.mark.reference
+def test_go_mode_cli(gen_cwd, capsys):
+    """``codegen <dir> makemaps --go`` is generator.go's ``main`` (os.Args[2] ==
+    "makemaps"); no mode argument writes the consts template."""
+    assert codegen.main(["testdata/datafortempfilled", "makemaps", "--go"]) == 0
+    with open("testdata/maptempfilledskiptimestamp.txt") as f:
+        assert _skip_timestamp("testdata/datafortempfilled/constants.go", 22 + 17) == f.read()
+    assert codegen.main(["testdata/datafortempfilled", "--go"]) == 0
+    with open("testdata/conststempfilledskiptimestamp.txt") as f:
+        assert _skip_timestamp("testdata/datafortempfilled/constants.go", 22 + 17) == f.read()
+    assert capsys.readouterr().out.splitlines() == ["testdata/datafortempfilled/constants.go"] * 2
