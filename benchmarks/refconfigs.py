@@ -111,6 +111,12 @@ def _coverage_configs():
     # storage class applied to the PVCs
     out["compat-fixed/cf"] = ("cf", "cf", {}, True, ["cf"], FIXED)
     out["compat-fixed/storage-class"] = ("storage", "storage", {}, False, None, FIXED)
+    # ... the version conversion of carried-over objects (k8s/convert.py:convert_fixed)
+    for p in ("Kubernetes", "Openshift", "AWS-EKS", "IBM-Openshift"):
+        out["compat-fixed/carried-over/" + p] = ("carried", "carried", {Q_CLUSTER: p}, False, None, FIXED)
+    # ... and the generated Ingress on the profiles that prefer networking.k8s.io/v1beta1
+    for p in ("AWS-EKS", "Azure-AKS", "GCP-GKE"):
+        out["compat-fixed/profiles/" + p] = ("samples", "samples", {Q_CLUSTER: p}, False, None, FIXED)
     return out
 
 

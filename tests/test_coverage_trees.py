@@ -62,6 +62,16 @@ COMPAT_FIXED = {
     "compat-fixed/storage-class": (refconfigs.golden_dir("storage-class"), {
         "myproject/cachedata-persistentvolumeclaim.yaml", "myproject/dbdata-persistentvolumeclaim.yaml"}),
 }
+_WORKLOADS = {"myproject/db-statefulset.yaml", "myproject/legacy-beta1-deployment.yaml",
+              "myproject/legacy-ext-deployment.yaml", "myproject/node-agent-daemonset.yaml",
+              "myproject/old-agent-daemonset.yaml"}
+for _p, _ing in (("Kubernetes", {"beta-ing", "old-ing"}), ("Openshift", {"beta-ing"}),
+                 ("IBM-Openshift", {"beta-ing"}), ("AWS-EKS", {"new-ing", "old-ing", "web"})):
+    COMPAT_FIXED["compat-fixed/carried-over/" + _p] = (
+        refconfigs.golden_dir("carried-over/" + _p), _WORKLOADS | {"myproject/%s-ingress.yaml" % i for i in _ing})
+for _p in ("AWS-EKS", "Azure-AKS", "GCP-GKE"):
+    COMPAT_FIXED["compat-fixed/profiles/" + _p] = (refconfigs.golden_dir("profiles/" + _p),
+                                                 {"myproject/myproject-ingress.yaml"})
 
 
 @pytest.mark.parametrize("name", sorted(COMPAT_FIXED))
@@ -69,14 +79,26 @@ def test_compat_fixed_trees_differ_only_where_documented(name):
     counterpart, files = COMPAT_FIXED[name]
     assert refconfigs.diff_files(refconfigs.golden_dir(name), counterpart) == sorted(files)
     dev = open(os.path.join(refconfigs.GOLDEN_REF, "DEVIATIONS.md")).read()
-    assert "`%s`" % name.split("/", 1)[1] in dev.split("## 5.")[1].split("## 6.")[0]
+    assert "`%s`" % name in dev.split("## 5.")[1].split("## 6.")[0]
+    fixed = refconfigs.golden_dir(name)
     if name == "compat-fixed/cf":
-        with open(os.path.join(refconfigs.golden_dir(name), "Manualimages.md")) as f:
+        with open(os.path.join(fixed, "Manualimages.md")) as f:
             assert f.read().rstrip().endswith("app2:latest")
-    else:
+    elif name == "compat-fixed/storage-class":
         for f in files:
-            with open(os.path.join(refconfigs.golden_dir(name), f)) as fh:
+            with open(os.path.join(fixed, f)) as fh:
                 assert yamlio.load(fh.read())["spec"]["storageClassName"] == "default"
+    else:   # objects relabelled to a version the profile lists, workloads with a selector
+        from move2kube_amd import metadata
+        from move2kube_amd.models import plan as plantypes
+        profile = name.rsplit("/", 1)[1]
+        spec = metadata.ClusterMDLoader.get_clusters(plantypes.new_plan())[profile].spec
+        for f in files:
+            with open(os.path.join(fixed, f)) as fh:
+                obj = yamlio.load(fh.read())
+            assert obj["apiVersion"] in (spec.get_supported_versions(obj["kind"]) or []), (f, obj["apiVersion"])
+            if obj["kind"] in ("Deployment", "DaemonSet", "StatefulSet"):
+                assert obj["spec"]["selector"]["matchLabels"], f
 
 
 def _objects(name, sub="myproject"):
