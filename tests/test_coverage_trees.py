@@ -254,3 +254,22 @@ def test_kind_conversions_to_the_cluster():
     assert obj("minimal-cluster", "seed-pod.yaml")["spec"]["restartPolicy"] == "OnFailure"
     svc = obj("minimal-cluster", "gateway-service.yaml")["spec"]
     assert svc == {"ports": [{"name": "web", "port": 0}], "type": "NodePort"}
+
+
+_FIXED_COUNTERPARTS = {n[len("compat-fixed/"):] for n in COMPAT_FIXED}
+
+
+@pytest.mark.parametrize("name", sorted(n for n in list(refconfigs.CONFIGS) + list(refconfigs.COVERAGE_CONFIGS)
+                                        if not n.startswith("compat-fixed/") and n not in _FIXED_COUNTERPARTS))
+def test_fixed_mode_changes_no_other_tree(name, tmp_path):
+    """DEVIATIONS section 5 lists every tree ``M2K_COMPAT=fixed`` changes: on
+    every other configuration the fixed mode writes the same bytes."""
+    run = refconfigs.Run(name, str(tmp_path)).prepare()
+    run.extra_env["M2K_COMPAT"] = "fixed"
+    undo = run.apply_env()
+    try:
+        with run.session() as s:
+            out = run.step(s)
+    finally:
+        undo()
+    assert refconfigs.diff_files(out, refconfigs.golden_dir(name), work=run.work) == []
