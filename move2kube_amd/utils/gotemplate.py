@@ -62,6 +62,13 @@ class _GoError(Exception):
     """An error a builtin returns (``error calling NAME: ...``)."""
 
 
+class _TooDeep(Exception):
+    """The interpreter's stack ran out inside a ``{{template}}`` call; carries
+    that call (``st``, ``node``) so :meth:`Template.execute` reports Go's
+    depth error at it.  Built without a Python ``__init__``: it is raised
+    where the stack has no room left."""
+
+
 _MISSING = object()  # exec.go: missingVal (no final value in a pipeline)
 
 
@@ -372,6 +379,9 @@ class Template:
                 from .gotemplate_compile import _c_list
                 run = self._run = _c_list(self.root)
             run(st, data)
+        except _TooDeep as e:
+            # exec.go walkTemplate: s.depth == maxExecDepth, reported at the call
+            raise _exec_error(e.st, e.node, "exceeded maximum template depth (%d)" % MAX_EXEC_DEPTH) from None
         except RecursionError:
             raise TemplateError("template: %s: exceeded maximum template depth (%d)" % (self.name, MAX_EXEC_DEPTH))
         return "".join(out)
@@ -492,7 +502,12 @@ class _State:
         newdot = self.eval_pipeline(dot, n.pipe) if n.pipe is not None else NO_VALUE
         st = _State(self.tmpl, n.name, self.funcs, self.out, self.depth + 1)
         st.vars = [("$", newdot)]
-        st.walk_list(newdot, body)
+        try:
+            st.walk_list(newdot, body)
+        except RecursionError:
+            e = _TooDeep()
+            e.st, e.node = self, n
+            raise e
 
     # -- pipelines -------------------------------------------------------------
     def eval_pipeline(self, dot, pipe):

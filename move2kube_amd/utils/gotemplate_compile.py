@@ -5,7 +5,7 @@ template's second execution, so a command that runs each template once
 
 from .gofmt import quote as go_quote
 from .gotemplate import (MAX_EXEC_DEPTH, NO_VALUE, TemplateError, _Action, _Bool, _Branch, _Chain, _Dot, _Field,
-                         _GoError, _Ident, _MISSING, _Nil, _Number, _Pipe, _SPECS, _State, _String, _Text,
+                         _GoError, _Ident, _TooDeep, _MISSING, _Nil, _Number, _Pipe, _SPECS, _State, _String, _Text,
                          _Variable, _check_arity, _exec_error, _field, _final_type, _invoke, _literal_arg,
                          _literal_command, _nil_arg, _node_str, _not_a_function, _print_value, _range_items, _spec,
                          _truth, _validate)
@@ -113,7 +113,12 @@ def _c_template(n):
         newdot = pipe(st, dot) if pipe is not None else NO_VALUE
         sub = _State(st.tmpl, name, st.funcs, st.out, st.depth + 1)
         sub.vars = [("$", newdot)]
-        body(sub, newdot)
+        try:
+            body(sub, newdot)
+        except RecursionError:
+            e = _TooDeep()
+            e.st, e.node = st, n
+            raise e
     return call_node
 
 

@@ -191,6 +191,12 @@ def test_whole_data_prints_as_a_go_map():
     # a field chain .x.y is positioned at its second field (parse.go operand: newChain(t.peek().pos))
     ('{{define "t"}}{{.x.y}}{{end}}{{template "t" .}}',
      'template: :1:18: executing "t" at <.x.y>: nil pointer evaluating interface {}.y'),
+    # exec.go walkTemplate: unbounded {{template}} recursion stops at maxExecDepth,
+    # reported at the call inside the recursing template, positioned at its
+    # name token (parse.go templateControl: newTemplate(token.pos, ...)); this
+    # stack runs out before depth 100000: the text is Go's, the depth is not
+    ('{{define "a"}}x{{template "a" .}}{{end}}{{template "a" .}}',
+     'template: :1:26: executing "a" at <{{template "a" .}}>: exceeded maximum template depth (100000)'),
 ])
 def test_error_location_and_context(src, want):
     data = {"port": 8080.0, "x": None}
