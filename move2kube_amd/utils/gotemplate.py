@@ -340,7 +340,12 @@ class Template:
         self.text = src
         from .gotemplate_parse import parse
         names = _BUILTIN_NAMES if not funcs else _BUILTIN_NAMES | frozenset(funcs)
-        self.root, self.defines = parse(src, names, name)
+        try:
+            self.root, self.defines = parse(src, names, name)
+        except RecursionError:
+            # Go's recursive-descent parser has no depth limit (its stacks grow);
+            # this one stops at the interpreter's recursion limit (DEVIATIONS.md 6)
+            raise TemplateError("template: %s: nested too deeply to parse (recursion limit)" % name) from None
 
     # -- the parsed form as plain data (utils/startcache.py) -----------------
     def to_data(self):
@@ -383,7 +388,8 @@ class Template:
             # exec.go walkTemplate: s.depth == maxExecDepth, reported at the call
             raise _exec_error(e.st, e.node, "exceeded maximum template depth (%d)" % MAX_EXEC_DEPTH) from None
         except RecursionError:
-            raise TemplateError("template: %s: exceeded maximum template depth (%d)" % (self.name, MAX_EXEC_DEPTH))
+            # nesting (not {{template}} calls) deeper than the interpreter's stack
+            raise TemplateError("template: %s: nested too deeply to execute (recursion limit)" % self.name) from None
         return "".join(out)
 
     def compiled_define(self, name):

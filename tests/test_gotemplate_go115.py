@@ -253,3 +253,16 @@ def test_user_detector_template_go_accepts_renders(tmp_path, monkeypatch, capsys
                                      "FROM x\n{{if eq .port 8080.0}}EXPOSE {{.port}}{{end}} {{printf \"%q\" .name}}\n")
     assert "Template conversion failed" not in capsys.readouterr().err
     assert len(found) == 1 and open(found[0]).read() == 'FROM x\nEXPOSE 8080 "web"\n'
+
+
+def test_user_detector_template_nested_beyond_the_stack_fails_cleanly(tmp_path, monkeypatch, capsys):
+    """Go's parser has no nesting limit (its stacks grow); this one stops at
+    the interpreter's recursion limit.  Such a template is a template error
+    (logged, empty Dockerfile), not a crash of the command (DEVIATIONS.md 6)."""
+    deep = "FROM x\n{{" + "(" * 2000 + ".port" + ")" * 2000 + "}}\n"
+    with pytest.raises(gotemplate.TemplateError, match="nested too deeply to parse"):
+        gotemplate.Template(deep)
+    found = _translate_with_detector(tmp_path, monkeypatch, deep)
+    err = capsys.readouterr().err
+    assert "Template conversion failed" in err and "nested too deeply" in err
+    assert len(found) == 1 and open(found[0]).read() == ""
