@@ -386,9 +386,9 @@ struct Der {
     Bytes v = raw(0x02);
     if (v.empty()) fail("asn1: syntax error: empty integer");
     if (v.size() > 8) fail("asn1: structure error: integer too large");
-    int64_t r = (v[0] & 0x80) ? -1 : 0;
+    uint64_t r = (v[0] & 0x80) ? ~uint64_t{0} : 0;  // sign-extended, shifted unsigned (no UB)
     for (unsigned char c : v) r = (r << 8) | c;
-    return r;
+    return static_cast<int64_t>(r);
   }
 
   std::string oid() {
@@ -781,6 +781,8 @@ void bcrypt_hash(uint8_t out[32], const Bytes& shapass, const Bytes& shasalt) {
   }
 }
 
+constexpr uint32_t kMaxBcryptRounds = 4096;
+
 Bytes bcrypt_pbkdf(const Bytes& password, const Bytes& salt, int64_t rounds, int64_t key_len) {
   if (rounds < 1) fail("bcrypt_pbkdf: number of rounds is too small");
   if (password.empty()) fail("bcrypt_pbkdf: empty password");
@@ -869,6 +871,12 @@ Key parse_openssh(const Bytes& data, const Bytes* passphrase) {
     Wire o(kdfopts);
     Bytes salt = o.str();
     uint32_t rounds = o.u32();
+    // x/crypto/ssh passes any count to bcrypt_pbkdf: a file asking for 2^32
+    // rounds makes the reference (and ssh-keygen) spin for days; refused here
+    // (DEVIATIONS.md 6).  ssh-keygen writes 16 unless told otherwise (-a).
+    if (rounds > kMaxBcryptRounds)
+      fail("ssh: bcrypt_pbkdf rounds " + std::to_string(rounds) + " exceed the limit of " +
+           std::to_string(kMaxBcryptRounds));
     Bytes k = bcrypt_pbkdf(*passphrase, salt, rounds, 32 + 16);
     Bytes key = k.substr(0, 32), iv = k.substr(32);
     if (cipher == "aes256-ctr") {
@@ -1056,6 +1064,15 @@ Key parse_raw(const Bytes& data, const Bytes* passphrase) {
 
 // (status, text): 0 the PEM, 1 passphrase missing, 2 an error, 3 an
 // unsupported key type (its Go %T).
+// A Go string as Python text: error messages can carry bytes of the key
+// file, which need not be UTF-8; they survive as surrogate escapes (the
+// caller's %q prints them as \xNN, as Go's does).
+py::str go_text(const std::string& s) {
+  PyObject* o = PyUnicode_DecodeUTF8(s.data(), (Py_ssize_t)s.size(), "surrogateescape");
+  if (!o) throw py::error_already_set();
+  return py::reinterpret_steal<py::str>(o);
+}
+
 py::tuple private_key_pem(py::bytes data, py::object passphrase) {
   Bytes in = data;
   Bytes pass;
@@ -1086,7 +1103,7 @@ py::tuple private_key_pem(py::bytes data, py::object passphrase) {
     }
   }
   OPENSSL_cleanse(&pass[0], pass.size());
-  return py::make_tuple(status, text);
+  return py::make_tuple(status, go_text(text));
 }
 
 py::bytes py_bcrypt_pbkdf(py::bytes password, py::bytes salt, int64_t rounds, int64_t key_len) {
@@ -1101,8 +1118,8 @@ py::object py_pem_decode(py::bytes data) {
   PemBlock b;
   if (!pem_decode(data, b)) return py::none();
   py::list headers;
-  for (auto& h : b.headers) headers.append(py::make_tuple(h.first, h.second));
-  return py::make_tuple(b.type, headers, py::bytes(b.bytes));
+  for (auto& h : b.headers) headers.append(py::make_tuple(go_text(h.first), go_text(h.second)));
+  return py::make_tuple(go_text(b.type), headers, py::bytes(b.bytes));
 }
 
 }  // namespace

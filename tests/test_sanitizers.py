@@ -210,6 +210,24 @@ SSHKEY_DRIVER = textwrap.dedent(r'''
             bad[i] ^= 0x5A
             m.private_key_pem(bytes(bad), None)
             m.private_key_pem(bytes(bad), b"m2k-pass")
+        # the same on the decoded body, re-armoured: every length field of
+        # openssh-key-v1 / DER reached with huge, zero and off-by-one values
+        import base64
+        lines = data.decode("ascii", "replace").strip().splitlines()
+        head = [l for l in lines if l.startswith("-----BEGIN")]
+        if not head or any(":" in l for l in lines[1:4]):
+            return
+        body = base64.b64decode("".join(l for l in lines if not l.startswith("-----")))
+        tail = head[0].replace("BEGIN", "END")
+        def armour(b):
+            t = base64.b64encode(b).decode()
+            return ("\n".join([head[0]] + [t[j:j + 70] for j in range(0, len(t), 70)] + [tail]) + "\n").encode()
+        for i in range(0, len(body), max(1, len(body) // 120)):
+            for patch in (b"\xff\xff\xff\xff", b"\x00\x00\x00\x00", b"\x7f\xff\xff\xfe", b"\x00\x00\x00\x11"):
+                b2 = body[:i] + patch + body[i + 4:]
+                m.private_key_pem(armour(b2), None)
+                m.private_key_pem(armour(b2), b"m2k-pass")
+            m.private_key_pem(armour(body[:i]), b"m2k-pass")
     ts = [threading.Thread(target=run, args=(k,)) for k in keys]
     for t in ts: t.start()
     for t in ts: t.join()

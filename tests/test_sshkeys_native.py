@@ -182,3 +182,45 @@ def test_wrong_password_and_ed25519_keep_the_placeholder(home_without_keygen, ca
     err = capsys.readouterr().err
     assert "x509: decryption password incorrect" in err
     assert "Unknown key type [*ed25519.PrivateKey]" in err
+
+
+def _rearmour(name, mutate):
+    """An OpenSSH key file with its binary body changed by ``mutate``."""
+    import base64
+    lines = _read(name + ".key").decode().strip().splitlines()
+    body = bytearray(base64.b64decode("".join(lines[1:-1])))
+    mutate(body)
+    t = base64.b64encode(bytes(body)).decode()
+    return ("\n".join([lines[0]] + [t[i:i + 70] for i in range(0, len(t), 70)] + [lines[-1]]) + "\n").encode()
+
+
+def _kdf_rounds_offset(body):
+    """Offset of the bcrypt rounds field: magic, cipher, kdf, then kdfoptions
+    (string salt, uint32 rounds)."""
+    import struct
+    off = len(b"openssh-key-v1\0")
+    for _ in range(2):                       # ciphername, kdfname
+        off += 4 + struct.unpack(">I", bytes(body[off:off + 4]))[0]
+    off += 4                                 # kdfoptions length
+    salt_len = struct.unpack(">I", bytes(body[off:off + 4]))[0]
+    return off + 4 + salt_len
+
+
+def test_hostile_bcrypt_rounds_are_refused():
+    """A key asking for 2^32-1 bcrypt rounds would make x/crypto (and
+    ssh-keygen) spin for days; it is refused (DEVIATIONS.md 6)."""
+    def huge(body):
+        o = _kdf_rounds_offset(body)
+        body[o:o + 4] = b"\xff\xff\xff\xff"
+    status, text = native.private_key_pem(_rearmour("rsa_openssh_ctr", huge), PASS.encode())
+    assert (status, text) == (2, "ssh: bcrypt_pbkdf rounds 4294967295 exceed the limit of 4096")
+
+
+def test_error_text_with_bytes_that_are_not_utf8():
+    """Error texts can carry bytes of the file: Go's %q escapes them where it
+    quotes; raw bytes elsewhere come back as surrogate escapes instead of
+    failing the call (a fuzz run under ASan found one)."""
+    data = b"-----BEGIN \xf4\x90 KEY-----\nAAAA\n-----END \xf4\x90 KEY-----\n"
+    assert native.private_key_pem(data, None) == (2, 'ssh: unsupported key type "\\xf4\\x90 KEY"')
+    block = native.pem_decode(b"-----BEGIN K-----\nX-\xff: \xfe\n\naGVs\n-----END K-----\n")
+    assert block == ("K", [("X-\udcff", "\udcfe")], b"hel")
