@@ -121,6 +121,29 @@ DRIVER = textwrap.dedent(r'''
             m.yaml_load(text[:i], mode, True, yamlio.go_resolve_number, unsup)
             m.yaml_load(text[:i], mode, False, yamlio.go_resolve_number, unsup)
     assert m.yaml_load(text, 0, True, yamlio.go_resolve_number, unsup)[0] == doc
+    # mutation fuzzing over the YAML files of samples/: flipped, dropped and
+    # inserted bytes (YAML indicators, quotes, tabs, newlines, non-ASCII)
+    import glob, random
+    rnd = random.Random(5)
+    corpus = []
+    for pth in sorted(glob.glob(os.path.join(sys.argv[2], "samples", "**", "*.y*ml"), recursive=True))[:12]:
+        with open(pth, encoding="utf-8", errors="replace") as fh:
+            corpus.append(fh.read()[:4000])
+    alphabet = list(":-[]{}\"'|>#&*!%@`?,\t\n ") + ["\u00e9", "\ufeff", "\x00", "\\u00", "0x", "1e9", ".inf"]
+    for doc_text in corpus:
+        for _ in range(150):
+            t = list(doc_text)
+            for _ in range(rnd.randint(1, 6)):
+                op, i = rnd.randint(0, 2), rnd.randrange(len(t) + 1)
+                if op == 0 and i < len(t):
+                    del t[i]
+                elif op == 1:
+                    t.insert(i, rnd.choice(alphabet))
+                elif i < len(t):
+                    t[i] = rnd.choice(alphabet)
+            mutated = "".join(t)
+            for mode in (0, 1, 2):
+                m.yaml_load(mutated, mode, True, yamlio.go_resolve_number, unsup)
     # repeated keys are left to PyYAML
     assert m.yaml_load("a: 1\nb: {c: 1, c: 2}\n", 0, False, yamlio.go_resolve_number, unsup) is unsup
     # the struct marshaller (k8s_marshal.cpp) against its Python specification
