@@ -13,7 +13,7 @@ import sys
 from .. import assets
 from ..models import plan as plantypes
 from ..utils import fsindex, log, yamlio
-from ..utils.common import go_abs, go_clean, go_join, go_path_error
+from ..utils.common import go_abs, go_clean, go_error_text, go_join, go_path_error
 from ..utils.constants import (APP_NAME_SHORT, DEFAULT_DIRECTORY_PERMISSION, DEFAULT_PLAN_FILE, DEFAULT_PROJECT_NAME,
                                QA_CACHE_FILE, settings)
 from ..utils.lazyre import LazyModule
@@ -114,7 +114,7 @@ def translate_handler(a):
         try:
             p = plantypes.read_plan(planfile)
         except Exception as e:  # noqa: BLE001
-            log.fatal("Unable to read the plan at path %s Error: %r", planfile, str(e))
+            log.fatal("Unable to read the plan at path %s Error: %r", planfile, go_error_text(e))
         if a.name_changed:
             p.name = a.name
         if a.source_changed:

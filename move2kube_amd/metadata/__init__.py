@@ -31,7 +31,7 @@ def _read_cluster_metadata(path):
     try:
         data = common.read_move2kube_yaml(path)
     except Exception as e:  # noqa: BLE001
-        log.debug("Failed to read the cluster metadata at path %r Error: %r", path, str(e))
+        log.debug("Failed to read the cluster metadata at path %r Error: %r", path, common.go_error_text(e))
         raise
     cm = collection.ClusterMetadata.from_yaml(data)
     if cm.kind != collection.CLUSTER_METADATA_KIND:
@@ -155,7 +155,7 @@ class QACacheLoader(Loader):
             try:
                 data = common.read_move2kube_yaml(f)
             except Exception as e:  # noqa: BLE001
-                log.debug("Failed to read the yaml file at path %r Error: %r", f, str(e))
+                log.debug("Failed to read the yaml file at path %r Error: %r", f, common.go_error_text(e))
                 continue
             if not isinstance(data, dict) or data.get("kind") != qa.QACACHE_KIND:
                 continue

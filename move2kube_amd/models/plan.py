@@ -469,7 +469,7 @@ def read_plan(path):
     try:
         plan = Plan.from_yaml(common.read_move2kube_yaml(path))
     except Exception as e:  # noqa: BLE001 - logged like ReadPlan, then returned to the caller
-        log.error("Failed to load the plan file at path %r Error %r", path, str(e))
+        log.error("Failed to load the plan file at path %r Error %r", path, common.go_error_text(e))
         raise
     plan.root_dir = common.go_abs(plan.root_dir) if plan.root_dir else os.getcwd()
     _convert_paths(plan, plan.get_absolute_path)

@@ -90,7 +90,7 @@ class CfManifestTranslator(Translator):
                 try:
                     data = common.read_move2kube_yaml(f)
                 except Exception as e:  # noqa: BLE001
-                    log.debug("Failed to read the yaml file at path %r Error: %r", f, str(e))
+                    log.debug("Failed to read the yaml file at path %r Error: %r", f, common.go_error_text(e))
                     continue
             kind = data.get("kind") if isinstance(data, dict) else None
             if kind != collection.CF_INSTANCE_APPS_KIND:

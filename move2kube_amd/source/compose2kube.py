@@ -128,7 +128,7 @@ class ComposeTranslator(Translator):
                 try:
                     im = _read_image_info(path)
                 except Exception as e:  # noqa: BLE001
-                    log.error("Failed to read image info yaml at path %s Error: %r", path, str(e))
+                    log.error("Failed to read image info yaml at path %s Error: %r", path, common.go_error_text(e))
                     continue
                 ir.add_container(irtypes.new_container_from_image_info(im))
         return ir

@@ -77,7 +77,7 @@ def write_containers(containers, outpath, root_dir, registry_url, registry_names
             batch.append((wp, c.new_files[rel], mode))
     for (wp, _, _), err in zip(batch, native.write_files(batch)):
         if err is not None:
-            log.warning("Error writing file at %s : %s", wp, err)
+            log.warning("Error writing file at %s : %s", wp, common.go_path_error(err, "open"))
     if manualimages:
         wp = os.path.join(outpath, "Manualimages.md")
         if settings.fixed:
@@ -158,7 +158,7 @@ def write_transformed_objects(path, objs):
     # one batched, parallel write (ops/csrc/m2k_native.cpp:write_files)
     for (f, _, _), kind, err in zip(batch, kinds, native.write_files(batch)):
         if err is not None:
-            log.error("Failed to write %r Error: %r", kind, str(err))
+            log.error("Failed to write %r Error: %r", kind, common.go_path_error(err, "open"))
             continue
         written.append(f)
         log.debug("%r created", f)

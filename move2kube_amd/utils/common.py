@@ -137,7 +137,12 @@ def read_bytes(path):
     import stat
     fd = os.open(path, os.O_RDONLY | os.O_NONBLOCK | os.O_CLOEXEC)
     try:
-        if not stat.S_ISREG(os.fstat(fd).st_mode):
+        mode = os.fstat(fd).st_mode
+        if stat.S_ISDIR(mode):   # Go opens a directory and fails on the read
+            e = IsADirectoryError(errno.EISDIR, os.strerror(errno.EISDIR), path)
+            e.go_op = "read"
+            raise e
+        if not stat.S_ISREG(mode):
             raise OSError(errno.EINVAL, "not a regular file", path)
         with open(fd, "rb", closefd=False) as f:
             return f.read()
@@ -512,10 +517,19 @@ def go_path_error(e, op):
     if path is None or not getattr(e, "errno", None):
         return str(e)
     import errno as _errno
+    op = getattr(e, "go_op", op)
     code = e.errno
     if op == "mkdir" and code == _errno.EEXIST:
         code = _errno.ENOTDIR
     return "%s %s: %s" % (op, os.fsdecode(path), go_errno_text(code))
+
+
+def go_error_text(e, op="open"):
+    """Text of an error caught broadly: an OSError with a path as Go's
+    ``*os.PathError`` (:func:`go_path_error`), anything else as it is."""
+    if isinstance(e, OSError):
+        return go_path_error(e, op)
+    return str(e)
 
 
 class GoExecNotFoundError(FileNotFoundError):

@@ -209,3 +209,17 @@ def test_verbose_flag_turns_on_debug_lines(work, capsys):
         log.set_verbose(False)
     assert cli.main(["plan", "-s", str(work / "src"), "-p", str(work / "cwd" / "q.plan")]) == 0
     assert "debug" not in {lv for lv, _m in logparse.messages(capsys.readouterr().err)}
+
+
+def test_plan_that_is_a_directory_reads_like_ioutil_readfile(work, capsys):
+    """translate.go:131-155 with <dir>/m2k.plan itself a directory: ReadFile
+    opens it and fails on the read, so ReadPlan (planutils.go:168) and the
+    fatal line carry ``read <path>: is a directory``."""
+    (work / "plans" / "m2k.plan").mkdir(parents=True)
+    w = str(work)
+    assert cli.main(["translate", "-p", w + "/plans", "--qaskip"]) == 1
+    err = capsys.readouterr().err
+    assert logparse.logged(err, 'Failed to load the plan file at path "%s/plans/m2k.plan" Error '
+                           '"read %s/plans/m2k.plan: is a directory"' % (w, w), "error")
+    assert logparse.logged(err, 'Unable to read the plan at path %s/plans/m2k.plan Error: '
+                           '"read %s/plans/m2k.plan: is a directory"' % (w, w), "fatal")

@@ -101,3 +101,23 @@ def test_unwritable_readme_is_logged_and_the_run_goes_on(tmp_path, capsys):
     K8sTransformer.write_readme("p", False, False, False, str(tmp_path))
     msgs = logparse.messages(capsys.readouterr().err)
     assert msgs[-1] == ("error", "Unable to write readme : open %s: is a directory" % (tmp_path / "Readme.md"))
+
+
+def test_failed_object_and_container_writes_print_go_path_errors(tmp_path, capsys):
+    """transformer.go:96 and :197 print the *os.PathError of ioutil.WriteFile
+    (``open <path>: <errno text>``), not Python's OSError text."""
+    import logparse
+    from move2kube_amd import transformer
+    from move2kube_amd.models import ir as irtypes
+    log.set_verbose(False)
+    (tmp_path / "web-service.yaml").mkdir()
+    obj = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "web"}, "spec": {}}
+    assert transformer.write_transformed_objects(str(tmp_path), [obj]) == []
+    c = irtypes.new_container("NewDockerfile", "img:latest", True)
+    c.new_files = {"svc/Dockerfile.svc": "FROM x\n"}
+    (tmp_path / "containers" / "svc" / "Dockerfile.svc").mkdir(parents=True)
+    transformer.write_containers([c], str(tmp_path), str(tmp_path), "quay.io", "ns")
+    msgs = logparse.messages(capsys.readouterr().err)
+    assert ("error", 'Failed to write "Service" Error: "open %s/web-service.yaml: is a directory"' % tmp_path) in msgs
+    assert ("warning", "Error writing file at %s/containers/svc/Dockerfile.svc : open %s/containers/svc/Dockerfile.svc: "
+            "is a directory" % (tmp_path, tmp_path)) in msgs
