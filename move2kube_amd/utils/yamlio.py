@@ -672,6 +672,37 @@ def _construct_raw_scalar(loader, node):
     return node.value
 
 
+def _construct_untagged(loader, node):
+    """A node whose tag go-yaml does not resolve (``!foo``, ``!!foo``,
+    ``!!set``, ``!!omap``, ``!!pairs``, ``!!timestamp``, ``!!python/...``):
+    decode.go decodes it by kind, a scalar as its text (resolve.go
+    ``resolvableTag``; an explicit ``!!timestamp`` would be a time.Time there,
+    its text here: parity unpinned)."""
+    import yaml
+    if isinstance(node, yaml.MappingNode):
+        return loader.construct_mapping(node, deep=True)
+    if isinstance(node, yaml.SequenceNode):
+        return loader.construct_sequence(node, deep=True)
+    return node.value
+
+
+def _construct_go_binary(loader, node):
+    """decode.go scalar(): ``!!binary`` is base64.StdEncoding (line breaks
+    ignored) decoded into a string; bad data is ``failf("!!binary value
+    contains invalid base64 data")``."""
+    import base64
+    import binascii
+    try:
+        data = base64.b64decode(loader.construct_scalar(node).replace("\r", "").replace("\n", ""), validate=True)
+    except (binascii.Error, ValueError):
+        raise _GoDecodeError("!!binary value contains invalid base64 data") from None
+    return data.decode("utf-8", errors="surrogateescape")
+
+
+class _GoDecodeError(Exception):
+    """A go-yaml decoder failf(): the text after ``yaml: ``."""
+
+
 class _Loaders:
     """PyYAML plus the three go-yaml flavoured loaders, built once."""
 
@@ -711,6 +742,11 @@ class _Loaders:
         for tag in ("tag:yaml.org,2002:int", "tag:yaml.org,2002:float", "tag:yaml.org,2002:bool",
                     "tag:yaml.org,2002:timestamp"):
             self.raw.add_constructor(tag, _construct_raw_scalar)
+        for cls in (self.typed, self.v2, self.raw):
+            cls.add_constructor(None, _construct_untagged)
+            for tag in ("set", "omap", "pairs") + (("timestamp",) if cls is not self.raw else ()):
+                cls.add_constructor("tag:yaml.org,2002:" + tag, _construct_untagged)
+            cls.add_constructor("tag:yaml.org,2002:binary", _construct_go_binary)
 
 
 _loaders = None
@@ -1009,6 +1045,79 @@ def go_unmarshal_type_error(text, value, into="map[string]interface {}"):
     return "yaml: unmarshal errors:\n  line %d: cannot unmarshal %s%s into %s" % (line, tag, shown, into)
 
 
+class _InvalidMapKey(Exception):
+    """A sequence or mapping used as a mapping key (PyYAML's "found unhashable
+    key"); ``key`` is the key's decoded value."""
+
+    def __init__(self, key):
+        super().__init__(key)
+        self.key = key
+
+
+def _first_invalid_key(node):
+    """The first collection key node in go-yaml's decode order (a key is
+    decoded, then checked, then its value), or None."""
+    import yaml
+    stack = [node]
+    seen = set()
+    while stack:
+        n = stack.pop()
+        if id(n) in seen:
+            continue
+        seen.add(id(n))
+        if isinstance(n, yaml.MappingNode):
+            todo = []
+            for k, v in n.value:
+                todo.append(("key", k))
+                todo.append(("val", v))
+            for what, child in reversed(todo):
+                stack.append(child)
+                if what == "key" and isinstance(child, (yaml.MappingNode, yaml.SequenceNode)) and \
+                        not (isinstance(child, yaml.ScalarNode) and child.value == "<<"):
+                    stack.append(("check", child))
+        elif isinstance(n, yaml.SequenceNode):
+            stack.extend(reversed(n.value))
+        elif isinstance(n, tuple):
+            inner = _first_invalid_key(n[1])
+            return inner if inner is not None else n[1]
+    return None
+
+
+def _go_sharp_v(v, v2):
+    """``fmt.Sprintf("%#v", v)`` of a value go-yaml decoded into interface{}
+    (an element: a nil is ``interface {}(nil)``)."""
+    from . import gofmt
+    if v is None:
+        return "interface {}(nil)"
+    if isinstance(v, list):
+        return "[]interface {}{" + ", ".join(_go_sharp_v(x, v2) for x in v) + "}"
+    if isinstance(v, dict):
+        # decode.go mapping(): v3 makes map[string]interface{} when every key is
+        # a string; v2 always map[interface{}]interface{}
+        typ = "map[string]interface {}" if not v2 and all(isinstance(k, str) for k in v) else \
+            "map[interface {}]interface {}"
+        return typ + "{" + ", ".join("%s:%s" % (_go_sharp_v(k, v2), _go_sharp_v(v[k], v2))
+                                      for k in gofmt.sorted_keys(v)) + "}"
+    return gofmt.sprintf("%#v", [v])
+
+
+def _construct(loader, node):
+    """construct_document, turning "found unhashable key" into
+    :class:`_InvalidMapKey` with the offending key decoded."""
+    import yaml
+    try:
+        return loader.construct_document(node)
+    except yaml.constructor.ConstructorError as e:
+        if e.problem != "found unhashable key":
+            raise
+        key = _first_invalid_key(node)
+        if key is None:
+            raise
+        loader.constructed_objects = {}
+        loader.recursive_objects = {}
+        raise _InvalidMapKey(loader.construct_object(key, deep=True)) from None
+
+
 def _pyyaml_load(loader_cls, text, multi):
     """``yaml.load_all``, or for a single load the first document only (go-yaml's
     ``Unmarshal`` decodes the first document of a stream and never reads the
@@ -1022,14 +1131,14 @@ def _pyyaml_load(loader_cls, text, multi):
             while loader.check_node():
                 node = loader.get_node()
                 dups.extend(_duplicate_keys(node))
-                docs.append(loader.construct_document(node))
+                docs.append(_construct(loader, node))
         else:
             docs = None
             if loader.check_node():
                 node = loader.get_node()
                 if node is not None:
                     dups = _duplicate_keys(node)
-                    docs = loader.construct_document(node)
+                    docs = _construct(loader, node)
     finally:
         loader.dispose()
     return docs, dups
@@ -1068,6 +1177,37 @@ def _go_error_texts(e, text):
     return fmt(v3), fmt(v2)
 
 
+def _go_utf8_problem(text):
+    """The first problem readerc.go ``yaml_parser_update_buffer`` finds in the
+    bytes of ``text`` (surrogate-escaped where they are not UTF-8)."""
+    raw = text.encode("utf-8", errors="surrogateescape") if isinstance(text, str) else bytes(text)
+    i, n = 0, len(raw)
+    while i < n:
+        b = raw[i]
+        width = 1 if b & 0x80 == 0 else 2 if b & 0xE0 == 0xC0 else 3 if b & 0xF0 == 0xE0 else \
+            4 if b & 0xF8 == 0xF0 else 0
+        if width == 0:
+            return "invalid leading UTF-8 octet"
+        if i + width > n:
+            return "incomplete UTF-8 octet sequence"
+        value = b & (0x7F if width == 1 else 0x1F if width == 2 else 0x0F if width == 3 else 0x07)
+        for k in range(1, width):
+            c = raw[i + k]
+            if c & 0xC0 != 0x80:
+                return "invalid trailing UTF-8 octet"
+            value = (value << 6) + (c & 0x3F)
+        if not (width == 1 or (width == 2 and value >= 0x80) or (width == 3 and value >= 0x800) or
+                (width == 4 and value >= 0x10000)):
+            return "invalid length of a UTF-8 sequence"
+        if 0xD800 <= value <= 0xDFFF or value > 0x10FFFF:
+            return "invalid Unicode character"
+        if not (value in (0x09, 0x0A, 0x0D, 0x85) or 0x20 <= value <= 0x7E or 0xA0 <= value <= 0xD7FF or
+                0xE000 <= value <= 0xFFFD or 0x10000 <= value <= 0x10FFFF):
+            return "control characters are not allowed"
+        i += width
+    return "invalid leading UTF-8 octet"
+
+
 def _parse(text, mode, multi):
     """-> (document(s), go-yaml v3 duplicate-key errors).  Only the v3 entry
     points raise on the second part: go-yaml v2 (compose files, and Kubernetes
@@ -1099,11 +1239,23 @@ def _parse(text, mode, multi):
         err = lz.yaml.YAMLError(texts[1] if mode == _V2 else texts[0])
         err.go_v2 = texts[1]
         raise err from None
-    except UnicodeError as e:
+    except _InvalidMapKey as e:
+        # decode.go mapping(): failf("invalid map key: %#v", k.Interface())
+        v3, v2 = ("yaml: invalid map key: " + _go_sharp_v(e.key, flavour) for flavour in (False, True))
+        err = lz.yaml.YAMLError(v2 if mode == _V2 else v3)
+        err.go_v2 = v2
+        raise err from None
+    except _GoDecodeError as e:
+        raise lz.yaml.YAMLError("yaml: %s" % e) from None
+    except lz.yaml.reader.ReaderError as e:
+        # readerc.go yaml_parser_set_reader_error: no mark, so parser.fail()
+        # prints the problem alone
+        raise lz.yaml.YAMLError("yaml: " + (e.reason or "unknown problem parsing YAML content")) from None
+    except UnicodeError:
         # bytes that are not UTF-8 (kept as surrogates by read_text): a parse
-        # error of this document, as go-yaml reports "invalid leading UTF-8
-        # octet" - callers skip the file instead of losing the whole planner
-        raise lz.yaml.YAMLError("invalid UTF-8 in document: %s" % e) from None
+        # error of this document worded as go-yaml's reader - callers skip the
+        # file instead of losing the whole planner
+        raise lz.yaml.YAMLError("yaml: " + _go_utf8_problem(text)) from None
 
 
 def _v3(result):

@@ -18,6 +18,14 @@ from move2kube_amd.utils import yamlio
     ("key: 'unterminated\n", "yaml: line 2: found unexpected end of stream",
      "yaml: line 2: found unexpected end of stream"),
     ("a: &x 1\nb: *y\n", "yaml: unknown anchor 'y' referenced", "yaml: unknown anchor 'y' referenced"),
+    # decode.go mapping(): a sequence or mapping key is failf("invalid map key: %#v");
+    # v3 decodes an all-string mapping into map[string]interface{}, v2 never does
+    ("a:\n  ? [1, 'x', 1.5, true, null, 2.0]\n  : 2\n",
+     'yaml: invalid map key: []interface {}{1, "x", 1.5, true, interface {}(nil), 2}',
+     'yaml: invalid map key: []interface {}{1, "x", 1.5, true, interface {}(nil), 2}'),
+    ("? {b: 1, a: [yes]}\n: x\n", 'yaml: invalid map key: map[string]interface {}{"a":[]interface {}{"yes"}, "b":1}',
+     'yaml: invalid map key: map[interface {}]interface {}{"a":[]interface {}{true}, "b":1}'),
+    ("x: {? {[1]: 2} : 3}\n", "yaml: invalid map key: []interface {}{1}", "yaml: invalid map key: []interface {}{1}"),
 ])
 def test_parse_errors_read_like_go_yaml(text, v3, v2):
     with pytest.raises(yamlio.YAMLError) as ei:
@@ -47,3 +55,36 @@ def test_plan_read_error_is_worded_like_the_reference(tmp_path):
     with pytest.raises(Exception) as ei:
         plantypes.read_plan(str(p))
     assert str(ei.value) == "yaml: line 5: mapping values are not allowed in this context"
+
+
+@pytest.mark.parametrize("text,want", [
+    # resolve.go resolvableTag: a tag go-yaml does not resolve decodes by node kind
+    ("a: !foo bar\n", {"a": "bar"}),
+    ("a: !!foo 12\n", {"a": "12"}),
+    ("a: !foo [1, {b: 2}]\n", {"a": [1, {"b": 2}]}),
+    ("a: !!set {x}\n", {"a": {"x": None}}),
+    ("a: !!omap [x: 1]\n", {"a": [{"x": 1}]}),
+    ("a: !!python/tuple [1]\n", {"a": [1]}),
+    # decode.go scalar(): !!binary is decoded into a string
+    ("a: !!binary aGVsbG8=\n", {"a": "hello"}),
+])
+def test_tags_decode_like_go_yaml(text, want):
+    assert yamlio.load(text) == want
+    assert yamlio.load_v2(text) == want
+
+
+@pytest.mark.parametrize("text,want", [
+    ("a: !!binary aGVsbG8\n", "yaml: !!binary value contains invalid base64 data"),
+    # readerc.go: reader errors carry no mark, so no line number
+    ("a: b\x01\n", "yaml: control characters are not allowed"),
+    ("a: b\udcff\n", "yaml: invalid leading UTF-8 octet"),          # a lone 0xff byte
+    ("a: b\udce9\udc80\n", "yaml: invalid trailing UTF-8 octet"),   # 0xe9 0x80 then a newline
+    ("a: b\udce9\udc80", "yaml: incomplete UTF-8 octet sequence"),
+    ("a: \udcc0\udc80\n", "yaml: invalid length of a UTF-8 sequence"),   # overlong NUL
+    ("a: \udced\udca0\udc80\n", "yaml: invalid Unicode character"),      # an encoded surrogate
+])
+def test_decode_failures_read_like_go_yaml(text, want):
+    for load in (yamlio.load, yamlio.load_v2, yamlio.load_raw):
+        with pytest.raises(yamlio.YAMLError) as ei:
+            load(text)
+        assert str(ei.value) == want
