@@ -28,12 +28,12 @@ def get_loaders():
 
 def _read_cluster_metadata(path):
     """``getClusterMetadata`` (clustermdloader.go:121-133)."""
+    from ..models.base import read_document
     try:
-        data = common.read_move2kube_yaml(path)
+        cm = read_document(path, collection.ClusterMetadata.from_yaml, "CLUSTER_METADATA")
     except Exception as e:  # noqa: BLE001
         log.debug("Failed to read the cluster metadata at path %r Error: %r", path, common.go_error_text(e))
         raise
-    cm = collection.ClusterMetadata.from_yaml(data)
     if cm.kind != collection.CLUSTER_METADATA_KIND:
         err = ValueError("The file at path %s is not a valid cluster metadata. Expected kind: %s Actual kind: %s"
                          % (log.go_quote(path), collection.CLUSTER_METADATA_KIND, cm.kind))

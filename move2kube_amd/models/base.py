@@ -7,10 +7,12 @@ Go struct-field order and wraps Go maps in :class:`GoMap` so the emitter sorts
 them like go-yaml.
 """
 
-from ..utils.yamlio import GoMap
+import math
+
+from ..utils.yamlio import GoMap, go_resolve_number
 
 __all__ = ["GoMap", "as_str", "as_bool", "as_int", "as_str_list", "as_str_map",
-           "as_str_list_map", "as_list", "as_map", "DecodeError"]
+           "as_str_list_map", "as_list", "as_map", "DecodeError", "read_document", "decode_loaded"]
 
 
 class DecodeError(ValueError):
@@ -43,23 +45,21 @@ def as_bool(v, default=False):
 
 
 def as_int(v, default=0):
+    """A scalar into a Go int field: decode.go ``scalar()`` takes a resolved
+    int, or a float64 truncated toward zero (resolve.go numbers: ``0x``,
+    ``0o``, ``0b``, a leading-zero octal, underscores)."""
     if v is None:
         return default
     if isinstance(v, bool):
         raise DecodeError("cannot unmarshal bool into int")
     if isinstance(v, int):
         return v
-    s = str(v).replace("_", "")
-    try:
-        return int(s, 0)
-    except ValueError:
-        try:
-            f = float(s)
-            if f == int(f):
-                return int(f)
-        except ValueError:
-            pass
-        raise DecodeError("cannot unmarshal %r into int" % (v,))
+    r = v if isinstance(v, float) else go_resolve_number(str(v))
+    if isinstance(r, int) and not isinstance(r, bool):
+        return r
+    if isinstance(r, float) and not math.isnan(r) and -2.0 ** 63 <= r <= 2 ** 63 - 1:
+        return int(r)
+    raise DecodeError("cannot unmarshal %r into int" % (v,))
 
 
 def as_list(v):
@@ -88,3 +88,27 @@ def as_str_map(v):
 
 def as_str_list_map(v):
     return {as_str(k): as_str_list(x) for k, x in as_map(v).items()}
+
+
+def read_document(path, decode, gotype):
+    """``common.ReadMove2KubeYaml(path, &out)`` (utils.go:210-251) for the Go
+    type named ``gotype`` in :mod:`.gotypes`: the move2kube group checks of
+    ``common.read_move2kube_yaml``, then ``decode`` of the loaded document."""
+    from ..utils import common
+    text, data = common.read_move2kube_yaml_text(path)
+    return decode_loaded(path, text, data, decode, gotype)
+
+
+def decode_loaded(path, text, data, decode, gotype):
+    """The typed half of :func:`read_document` for a document already read: a
+    shape ``decode`` rejects fails with go-yaml's full list of type errors
+    (:func:`.gotypes.error_text`), logged at debug level as utils.go:246-248
+    does.  The Go types are only loaded on that path."""
+    try:
+        return decode(data)
+    except DecodeError as e:
+        from ..utils import log
+        from . import gotypes
+        msg = gotypes.error_text(text, getattr(gotypes, gotype)) or str(e)
+        log.debug("Error occurred while unmarshalling yaml file at path %s Error: %r", path, msg)
+        raise DecodeError(msg) from None

@@ -17,7 +17,7 @@ import os
 from ..utils import common, log, yamlio
 from ..utils.constants import (ASSETS_DIR, DEFAULT_CLUSTER_TYPE, DEFAULT_PROJECT_NAME,
                                SCHEME_GROUP_VERSION, settings)
-from .base import (GoMap, as_bool, as_list, as_map, as_str, as_str_list,
+from .base import (GoMap, as_bool, as_list, as_map, as_str, as_str_list, read_document,
                    as_str_list_map)
 
 PLAN_KIND = "Plan"
@@ -467,7 +467,7 @@ def new_plan():
 def read_plan(path):
     """Read a plan converting relative paths to absolute (planutils.go:165-178)."""
     try:
-        plan = Plan.from_yaml(common.read_move2kube_yaml(path))
+        plan = read_document(path, Plan.from_yaml, "PLAN")
     except Exception as e:  # noqa: BLE001 - logged like ReadPlan, then returned to the caller
         log.error("Failed to load the plan file at path %r Error %r", path, common.go_error_text(e))
         raise

@@ -540,12 +540,12 @@ class Cache:
 
     def load(self):
         """Load and merge the cache file (cache.go:45-60)."""
+        from .base import read_document
         try:
-            data = common.read_move2kube_yaml(self.file)
+            other = read_document(self.file, lambda d: Cache.from_yaml(d, self.file), "QA_CACHE")
         except Exception as e:  # noqa: BLE001 - logged, then returned to StartEngine
-            log.error("Unable to load cache : %s", e)
+            log.error("Unable to load cache : %s", common.go_error_text(e))
             raise
-        other = Cache.from_yaml(data, self.file)
         self._merge(other)
         for p in self.problems:
             p.resolved = True

@@ -31,7 +31,8 @@ def _get_cf_instance_app(file_apps, name):
 
 
 def _get_cf_app_instance(path, appname):
-    c = collection.CfInstanceApps.from_yaml(common.read_move2kube_yaml(path))
+    from ..models.base import read_document
+    c = read_document(path, collection.CfInstanceApps.from_yaml, "CF_INSTANCE_APPS")
     for app in c.applications:
         if app.name == appname:
             return app
@@ -69,38 +70,32 @@ class CfManifestTranslator(Translator):
         if settings.fixed:
             containerizers = [collection.BuildpackContainerizer(b["buildpackName"], b["containerBuildType"], b["targetOptions"])
                               for b in assets.builtin_cf_buildpacks()]
+        from ..models.base import decode_loaded
         docs = {}
         for f in files:   # every move2kube-group YAML counts: there is no kind check (cfmanifest2kube.go:67-76)
             try:
-                docs[f] = data = common.read_move2kube_yaml(f)
+                docs[f] = text, data = common.read_move2kube_yaml_text(f)
+                found = decode_loaded(f, text, data, collection.CfContainerizers.from_yaml, "CF_CONTAINERIZERS")
             except Exception as e:  # noqa: BLE001
-                log.debug("Not a valid containerizer option file at path %r Error: %r", f, str(e))
+                log.debug("Not a valid containerizer option file at path %r Error: %r", f, common.go_error_text(e))
                 continue
-            try:
-                containerizers.extend(collection.CfContainerizers.from_yaml(data).buildpack_containerizers)
-            except ValueError:
-                continue
+            containerizers.extend(found.buildpack_containerizers)
         if log.debug_enabled():
             log.debug("Containerizers %s", "{TypeMeta:{APIVersion: Kind:cfcontainerizers} ObjectMeta:{Name:} "
                       "Spec:{BuildpackContainerizers:[%s]}}" % " ".join(b.go_plus_v() for b in containerizers))
         instance_apps = {}
         for f in files:
-            data = docs.get(f)
-            if data is None:
-                try:
-                    data = common.read_move2kube_yaml(f)
-                except Exception as e:  # noqa: BLE001
-                    log.debug("Failed to read the yaml file at path %r Error: %r", f, common.go_error_text(e))
-                    continue
-            kind = data.get("kind") if isinstance(data, dict) else None
-            if kind != collection.CF_INSTANCE_APPS_KIND:
-                log.debug("%s is not a valid apps file. Expected kind: %s Actual Kind: %s", log.go_quote(f),
-                          collection.CF_INSTANCE_APPS_KIND, kind if isinstance(kind, str) else "")
-                continue
             try:
-                instance_apps.setdefault(f, []).extend(collection.CfInstanceApps.from_yaml(data).applications)
-            except ValueError:
+                text, data = docs.get(f) or common.read_move2kube_yaml_text(f)
+                apps = decode_loaded(f, text, data, collection.CfInstanceApps.from_yaml, "CF_INSTANCE_APPS")
+            except Exception as e:  # noqa: BLE001
+                log.debug("Failed to read the yaml file at path %r Error: %r", f, common.go_error_text(e))
                 continue
+            if apps.kind != collection.CF_INSTANCE_APPS_KIND:
+                log.debug("%s is not a valid apps file. Expected kind: %s Actual Kind: %s", log.go_quote(f),
+                          collection.CF_INSTANCE_APPS_KIND, apps.kind)
+                continue
+            instance_apps.setdefault(f, []).extend(apps.applications)
         if log.debug_enabled():
             log.debug("Cf Instances %s", "map[" + " ".join(
                 "%s:[%s]" % (k, " ".join(a.go_plus_v() for a in instance_apps[k])) for k in sorted(instance_apps)) + "]")

@@ -17,8 +17,8 @@ from .translator import Translator
 
 
 def _read_image_info(path):
-    data = common.read_move2kube_yaml(path)
-    return collection.ImageInfo.from_yaml(data)
+    from ..models.base import read_document
+    return read_document(path, collection.ImageInfo.from_yaml, "IMAGE_INFO")
 
 
 class ComposeTranslator(Translator):

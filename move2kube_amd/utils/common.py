@@ -221,6 +221,11 @@ def read_move2kube_yaml(path, raw=True):
     Checks that ``apiVersion``'s group is ``move2kube.konveyor.io`` and warns on a
     version mismatch (``internal/common/utils.go:210-251``).  Returns the decoded
     document (scalars kept as raw strings when ``raw``)."""
+    return read_move2kube_yaml_text(path, raw)[1]
+
+
+def read_move2kube_yaml_text(path, raw=True):
+    """:func:`read_move2kube_yaml` -> (file text, document)."""
     try:
         text = read_text(path)
     except OSError as e:
@@ -259,7 +264,7 @@ def read_move2kube_yaml(path, raw=True):
     if version != SCHEME_VERSION:
         log.warning("The file at path %s was generated using a different version. File version is %s and move2kube version is %s",
                     path, version, SCHEME_VERSION)
-    return yamlio.load_raw(text) if raw else data
+    return text, (yamlio.load_raw(text) if raw else data)
 
 
 def write_json(output_path, data):

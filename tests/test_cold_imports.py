@@ -18,6 +18,8 @@ sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
 
 STALE_ON_BOX = ("argparse", "gettext", "locale", "json", "base64", "copy",
                 "queue", "heapq")  # queue + heapq: 1.9 ms per process there (profiles/r05_perf2/cold_importtime.jsonl)
+# package modules only error paths need (Go type tables for decode errors, fmt's printer for printf)
+ERROR_PATH_ONLY = ("move2kube_amd.models.gotypes", "move2kube_amd.utils.gofmt_printer")
 
 _CHILD = """
 import sys
@@ -42,7 +44,7 @@ def test_cold_translate_skips_stale_stdlib_modules(tmp_path, config):
             subprocess.run([sys.executable, "-m", "move2kube_amd"] + argv0, env=env, cwd=str(tmp_path),
                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True, timeout=120)
         shutil.copytree(os.path.join(str(tmp_path), "collect", "m2k_collect"), os.path.join(run.src, "m2k_collect"))
-    p = subprocess.run([sys.executable, "-c", _CHILD % (ROOT, argv, STALE_ON_BOX)], env=env, cwd=str(tmp_path),
+    p = subprocess.run([sys.executable, "-c", _CHILD % (ROOT, argv, STALE_ON_BOX + ERROR_PATH_ONLY)], env=env, cwd=str(tmp_path),
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     assert p.stdout.decode().strip().splitlines()[-1:] in ([], [""]), p.stdout.decode()
