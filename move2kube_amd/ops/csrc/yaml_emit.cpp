@@ -136,6 +136,18 @@ static Analysis analyze(const char* s, size_t n) {
   return {line_breaks, block_plain, single_ok, block_ok};
 }
 
+// A null, a bool (YAML 1.1 words included) or the merge key: never plain.
+static bool reserved_word(const char* s, size_t n) {
+  switch (s[0]) {  // every such word starts with one of these
+    case '~': case 'n': case 'N': case 't': case 'T': case 'f': case 'F':
+    case 'y': case 'Y': case 'o': case 'O': case '<':
+      break;
+    default:
+      return false;
+  }
+  return in_list(s, n, kNulls) || in_list(s, n, kBools) || in_list(s, n, kOldBools) || eq(s, n, "<<");
+}
+
 // Style for an ASCII string; -1 with a Python error set on failure.
 static int string_style(Ctx& c, PyObject* str, const char* s, size_t n, bool key) {
   bool can_plain;
@@ -148,8 +160,7 @@ static int string_style(Ctx& c, PyObject* str, const char* s, size_t n, bool key
     if (v == -1 && PyErr_Occurred()) return -1;
     return static_cast<int>(v);
   }
-  can_plain = n > 0 && !in_list(s, n, kNulls) && !in_list(s, n, kBools) && !in_list(s, n, kOldBools) &&
-              !eq(s, n, "<<");
+  can_plain = n > 0 && !reserved_word(s, n);
   int style;
   if (std::memchr(s, '\n', n))
     style = LITERAL;
@@ -357,9 +368,17 @@ struct Entry {
   size_t n;
 };
 
+// A line's lead-in is `indent` columns: spaces, or - for the first entry of a
+// mapping or sequence that is itself a sequence item - spaces followed by
+// `marks` "- " pairs (a sequence item's dash(es) on the same line).
 static bool emit_value_tail(Ctx& c, PyObject* v, int indent);
-static bool emit_map(Ctx& c, PyObject* d, int indent, const std::string* first_prefix);
-static bool emit_seq(Ctx& c, PyObject* seq, int indent, const std::string* first_prefix);
+static bool emit_map(Ctx& c, PyObject* d, int indent, int first_marks);
+static bool emit_seq(Ctx& c, PyObject* seq, int indent, int first_marks);
+
+static inline void put_lead(Ctx& c, int indent, int marks) {
+  c.out.append(static_cast<size_t>(indent - 2 * marks), ' ');
+  for (int i = 0; i < marks; ++i) c.out += "- ";
+}
 
 static inline bool is_seq(PyObject* v) { return PyList_Check(v) || PyTuple_Check(v); }
 static inline Py_ssize_t seq_len(PyObject* v) { return PyList_Check(v) ? PyList_GET_SIZE(v) : PyTuple_GET_SIZE(v); }
@@ -367,17 +386,14 @@ static inline PyObject* seq_item(PyObject* v, Py_ssize_t i) {
   return PyList_Check(v) ? PyList_GET_ITEM(v, i) : PyTuple_GET_ITEM(v, i);
 }
 
-static bool emit_entry(Ctx& c, PyObject* k, PyObject* v, int indent, const std::string* prefix, int pad) {
-  if (prefix)
-    c.out += *prefix;
-  else
-    c.out.append(static_cast<size_t>(pad), ' ');
+static bool emit_entry(Ctx& c, PyObject* k, PyObject* v, int indent, int marks) {
+  put_lead(c, indent, marks);
   if (!put_scalar(c, k, indent, true)) return false;
   c.out.push_back(':');
   return emit_value_tail(c, v, indent);
 }
 
-static bool emit_map(Ctx& c, PyObject* d, int indent, const std::string* first_prefix) {
+static bool emit_map(Ctx& c, PyObject* d, int indent, int first_marks) {
   int sorted = c.sort_maps;
   if (!sorted) {
     sorted = PyObject_IsInstance(d, c.gomap);
@@ -389,14 +405,22 @@ static bool emit_map(Ctx& c, PyObject* d, int indent, const std::string* first_p
     PyObject *k, *v;
     bool first = true;
     while (PyDict_Next(d, &pos, &k, &v)) {
-      if (!emit_entry(c, k, v, indent, first ? first_prefix : nullptr, indent)) return false;
+      if (!emit_entry(c, k, v, indent, first ? first_marks : 0)) return false;
       first = false;
     }
     return true;
   }
   if (plain_dict) {
-    std::vector<Entry> es;
-    es.reserve(static_cast<size_t>(PyDict_GET_SIZE(d)));
+    // small maps (nearly all of a manifest's) sort on the stack by insertion
+    const size_t size = static_cast<size_t>(PyDict_GET_SIZE(d));
+    Entry small[32];
+    std::vector<Entry> big;
+    Entry* es = small;
+    if (size > 32) {
+      big.resize(size);
+      es = big.data();
+    }
+    size_t n = 0;
     Py_ssize_t pos = 0;
     PyObject *k, *v;
     bool native_keys = true;
@@ -405,19 +429,23 @@ static bool emit_map(Ctx& c, PyObject* d, int indent, const std::string* first_p
         native_keys = false;
         break;
       }
-      Py_ssize_t len;
-      const char* s = PyUnicode_AsUTF8AndSize(k, &len);
-      if (!s) return false;
-      es.push_back({k, v, s, static_cast<size_t>(len)});
+      // compact ASCII: the UTF-8 form is the string's own data
+      es[n++] = {k, v, static_cast<const char*>(PyUnicode_DATA(k)), static_cast<size_t>(PyUnicode_GET_LENGTH(k))};
     }
     if (native_keys) {
-      std::stable_sort(es.begin(), es.end(),
-                       [](const Entry& x, const Entry& y) { return go_key_cmp(x.s, x.n, y.s, y.n) < 0; });
-      bool first = true;
-      for (const Entry& e : es) {
-        if (!emit_entry(c, e.key, e.val, indent, first ? first_prefix : nullptr, indent)) return false;
-        first = false;
+      auto less = [](const Entry& x, const Entry& y) { return go_key_cmp(x.s, x.n, y.s, y.n) < 0; };
+      if (n > 32) {
+        std::stable_sort(es, es + n, less);
+      } else {
+        for (size_t i = 1; i < n; ++i) {   // stable: an entry moves only past strictly greater ones
+          Entry e = es[i];
+          size_t j = i;
+          for (; j > 0 && less(e, es[j - 1]); --j) es[j] = es[j - 1];
+          es[j] = e;
+        }
       }
+      for (size_t i = 0; i < n; ++i)
+        if (!emit_entry(c, es[i].key, es[i].val, indent, i == 0 ? first_marks : 0)) return false;
       return true;
     }
   }
@@ -441,7 +469,7 @@ static bool emit_map(Ctx& c, PyObject* d, int indent, const std::string* first_p
       Py_DECREF(list);
       return false;
     }
-    bool ok = emit_entry(c, k, v, indent, i == 0 ? first_prefix : nullptr, indent);
+    bool ok = emit_entry(c, k, v, indent, i == 0 ? first_marks : 0);
     Py_DECREF(v);
     if (!ok) {
       Py_DECREF(list);
@@ -452,30 +480,27 @@ static bool emit_map(Ctx& c, PyObject* d, int indent, const std::string* first_p
   return true;
 }
 
-static bool emit_seq(Ctx& c, PyObject* seq, int indent, const std::string* first_prefix) {
+static bool emit_seq(Ctx& c, PyObject* seq, int indent, int first_marks) {
   Py_ssize_t n = seq_len(seq);
-  std::string pad(static_cast<size_t>(indent), ' ');
   for (Py_ssize_t i = 0; i < n; ++i) {
     PyObject* item = seq_item(seq, i);
-    const std::string& prefix = (i == 0 && first_prefix) ? *first_prefix : pad;
+    const int marks = i == 0 ? first_marks : 0;   // this item's lead-in, then its own "- "
     if (PyDict_Check(item)) {
       if (PyDict_GET_SIZE(item) > 0) {
-        std::string p = prefix + "- ";
-        if (!emit_map(c, item, indent + 2, &p)) return false;
+        if (!emit_map(c, item, indent + 2, marks + 1)) return false;
       } else {
-        c.out += prefix;
+        put_lead(c, indent, marks);
         c.out += "- {}\n";
       }
     } else if (is_seq(item)) {
       if (seq_len(item) > 0) {
-        std::string p = prefix + "- ";
-        if (!emit_seq(c, item, indent + 2, &p)) return false;
+        if (!emit_seq(c, item, indent + 2, marks + 1)) return false;
       } else {
-        c.out += prefix;
+        put_lead(c, indent, marks);
         c.out += "- []\n";
       }
     } else {
-      c.out += prefix;
+      put_lead(c, indent, marks);
       c.out += "- ";
       if (!put_scalar(c, item, indent + 2, false)) return false;
       c.out.push_back('\n');
@@ -492,7 +517,7 @@ static bool emit_value_tail(Ctx& c, PyObject* v, int indent) {
       return true;
     }
     c.out.push_back('\n');
-    return emit_map(c, v, indent + 2, nullptr);
+    return emit_map(c, v, indent + 2, 0);
   }
   if (is_seq(v)) {
     if (seq_len(v) == 0) {
@@ -500,7 +525,7 @@ static bool emit_value_tail(Ctx& c, PyObject* v, int indent) {
       return true;
     }
     c.out.push_back('\n');
-    return emit_seq(c, v, indent + 2, nullptr);
+    return emit_seq(c, v, indent + 2, 0);
   }
   c.out.push_back(' ');
   if (!put_scalar(c, v, indent + 2, false)) return false;
@@ -522,14 +547,14 @@ extern "C" PyObject* m2k_yaml_dump(PyObject* data, int sort_maps, PyObject* goma
       c.out += "{}\n";
       ok = true;
     } else {
-      ok = emit_map(c, data, 0, nullptr);
+      ok = emit_map(c, data, 0, 0);
     }
   } else if (is_seq(data)) {
     if (seq_len(data) == 0) {
       c.out += "[]\n";
       ok = true;
     } else {
-      ok = emit_seq(c, data, 0, nullptr);
+      ok = emit_seq(c, data, 0, 0);
     }
   } else {
     ok = put_scalar(c, data, 2, false);
