@@ -46,7 +46,8 @@ def test_single_rank():
     d = _last_json(p.stdout.decode())
     assert KEYS <= set(d)
     assert d["n_gpus"] == 1 and d["steps"] == 1 and d["value"] > 0
-    assert d["manifest_diff_vs_ref"] == 0 and d["manifest_diff_vs_ref_headline"] == 0
+    assert d["manifest_diff_vs_ref"] == 0 and d["manifest_diff_vs_ref_headline"] == 0, \
+        (d["manifest_diff_vs_ref_headline"], {k: v.get("manifest_diff_vs_ref") for k, v in d["per_config"].items()})
     assert sorted(d["per_config"]) == ["cf", "docker-compose", "golang", "helm-openshift", "java-cnb", "large-tree"]
     lt = d["per_config"]["large-tree"]
     assert sorted(lt["large_tree_translate_ms_per_service"]) == ["20", "60"] and lt["ratio_largest_vs_smallest"] > 0
