@@ -16,7 +16,11 @@ class GitError(Exception):
 
 
 def find_repo(path):
-    """Walk up from ``path`` to the directory containing ``.git``.
+    """Walk up from ``path`` to the first directory holding a ``.git`` entry
+    (go-git ``dotGitToOSFilesystems`` with ``DetectDotGit``): a ``.git``
+    directory is the repository, a ``.git`` file must point at one with
+    ``gitdir: ``; either way the walk stops there, and a repository without
+    ``HEAD`` does not exist (``Open``: ``ErrRepositoryNotExists``).
 
     Returns (worktree_root, git_dir).  Inside an ``fsindex.scope()`` every
     directory visited remembers the answer, so the per-service lookups of one
@@ -31,21 +35,11 @@ def find_repo(path):
         visited.append(p)
         dotgit = os.path.join(p, ".git")
         if os.path.isdir(dotgit):
-            if os.path.exists(os.path.join(dotgit, "HEAD")):
-                result = (p, dotgit)
-                break
-        elif os.path.isfile(dotgit):
-            try:
-                with open(dotgit) as f:
-                    line = f.read().strip()
-            except OSError as e:
-                raise GitError(str(e))
-            if line.startswith("gitdir:"):
-                gd = line[len("gitdir:"):].strip()
-                if not os.path.isabs(gd):
-                    gd = os.path.normpath(os.path.join(p, gd))
-                result = (p, gd)
-                break
+            result = (p, dotgit)
+            break
+        if os.path.lexists(dotgit):
+            result = (p, _gitdir_file(p, dotgit))
+            break
         parent = os.path.dirname(p)
         if parent == p:
             result = None
@@ -54,37 +48,172 @@ def find_repo(path):
     if cache is not None:
         for v in visited:
             cache[v] = result
-    if result is None:
+    if result is None or isinstance(result[1], GitError):
+        raise result[1] if result is not None else GitError("repository does not exist")
+    if not os.path.exists(os.path.join(result[1], "HEAD")):
         raise GitError("repository does not exist")
     return result
 
 
-_REMOTE_RE = _lazy_re(r'^remote\s+"(.*)"$')
+def _gitdir_file(root, dotgit):
+    """``dotGitFileToOSFilesystem``: the first line after ``gitdir: ``,
+    relative to the work tree; a GitError (kept in the cache) otherwise."""
+    try:
+        with open(dotgit, encoding="utf-8", errors="surrogateescape") as f:
+            line = f.read()
+    except OSError as e:
+        from .common import go_path_error
+        return GitError(go_path_error(e, "open"))
+    prefix = "gitdir: "
+    if not line.startswith(prefix):
+        return GitError(".git file has no %s prefix" % prefix)
+    gd = line[len(prefix):].split("\n")[0].strip()
+    return gd if os.path.isabs(gd) else os.path.join(root, gd)
+
+
+class GitConfigError(GitError):
+    pass
+
+
+def parse_config(text):
+    """``git-config`` syntax as go-git's decoder (``gcfg``) reads it: ``[section]``
+    and ``[section "subsection"]`` headers (section and variable names are
+    case-insensitive, subsections are not; ``[section.sub]`` is the old form of a
+    lower-cased subsection), ``name = value`` with double quotes, the escapes
+    ``\\ \" \n \t \b``, backslash-newline continuations and ``;``/``#``
+    comments outside quotes, and a bare ``name`` (no ``=``).  Returns
+    ``[(section, subsection, name, value)]`` in file order."""
+    out = []
+    section = subsection = None
+    i, n, line = 0, len(text), 1
+
+    def fail(what):
+        raise GitConfigError("bad config line %d in file config: %s" % (line, what))
+
+    while i < n:
+        ch = text[i]
+        if ch == "\n":
+            line += 1
+            i += 1
+            continue
+        if ch in " \t\r":
+            i += 1
+            continue
+        if ch in "#;":
+            while i < n and text[i] != "\n":
+                i += 1
+            continue
+        if ch == "[":
+            j = i + 1
+            while j < n and (text[j].isalnum() or text[j] in "-."):
+                j += 1
+            name = text[i + 1:j]
+            k = j
+            while k < n and text[k] in " \t":
+                k += 1
+            sub = None
+            if k < n and text[k] == '"':
+                buf = []
+                k += 1
+                while k < n and text[k] != '"':
+                    if text[k] == "\n":
+                        fail("unterminated subsection name")
+                    if text[k] == "\\" and k + 1 < n and text[k + 1] != "\n":
+                        k += 1
+                    buf.append(text[k])
+                    k += 1
+                if k >= n:
+                    fail("unterminated subsection name")
+                sub = "".join(buf)
+                k += 1
+            elif "." in name:
+                name, sub = name.split(".", 1)
+                sub = sub.lower()
+            if k >= n or text[k] != "]" or not name:
+                fail("bad section header")
+            section, subsection = name.lower(), sub
+            i = k + 1
+            continue
+        if not ch.isalpha():
+            fail("bad variable name")
+        j = i
+        while j < n and (text[j].isalnum() or text[j] == "-"):
+            j += 1
+        name = text[i:j].lower()
+        while j < n and text[j] in " \t":
+            j += 1
+        if section is None:
+            fail("variable outside a section")
+        if j >= n or text[j] in "\r\n#;":
+            out.append((section, subsection, name, None))
+            i = j
+            continue
+        if text[j] != "=":
+            fail("bad variable")
+        j += 1
+        while j < n and text[j] in " \t":
+            j += 1
+        buf, keep, quoted = [], 0, False
+        while j < n:
+            c = text[j]
+            if c == "\n" and not quoted:
+                break
+            if c == "\n":
+                fail("unterminated quoted value")
+            if c == "\r" and not quoted and text[j + 1:j + 2] == "\n":
+                j += 1
+                continue
+            if c == '"':
+                quoted = not quoted
+                keep = len(buf)
+                j += 1
+                continue
+            if c in "#;" and not quoted:
+                while j < n and text[j] != "\n":
+                    j += 1
+                break
+            if c == "\\":
+                e = text[j + 1:j + 2]
+                if e == "\n":
+                    line += 1
+                    j += 2
+                    continue
+                esc = {"\\": "\\", '"': '"', "n": "\n", "t": "\t", "b": "\b"}.get(e)
+                if esc is None:
+                    fail("bad escape")
+                buf.append(esc)
+                keep = len(buf)
+                j += 2
+                continue
+            buf.append(c)
+            if c not in " \t" or quoted:
+                keep = len(buf)
+            j += 1
+        if quoted:
+            fail("unterminated quoted value")
+        out.append((section, subsection, name, "".join(buf[:keep])))
+        i = j
+    return out
 
 
 def _read_config(git_dir):
+    """Remote name -> URLs (in file order; ``remote.Config().URLs``) from the
+    repository's config (the common dir's for a linked work tree).  A config
+    go-git cannot parse raises :class:`GitConfigError`."""
     cfg = os.path.join(git_dir, "config")
-    # worktrees keep the shared config in the common dir
-    common_file = os.path.join(git_dir, "commondir")
-    if not os.path.exists(cfg) and os.path.exists(common_file):
-        with open(common_file) as f:
-            cfg = os.path.join(os.path.normpath(os.path.join(git_dir, f.read().strip())), "config")
-    import configparser
-    parser = configparser.RawConfigParser(strict=False, allow_no_value=True)
+    if not os.path.exists(cfg):
+        cfg = os.path.join(_common_dir(git_dir), "config")
     try:
-        with open(cfg) as f:
-            parser.read_string(f.read())
-    except (OSError, configparser.Error):
+        with open(cfg, encoding="utf-8", errors="surrogateescape") as f:
+            text = f.read()
+    except OSError:
         return {}
     remotes = {}
-    for sect in parser.sections():
-        m = _REMOTE_RE.match(sect.strip())
-        if m:
-            urls = []
-            for k, v in parser.items(sect):
-                if k == "url" and v:
-                    urls.append(v.strip())
-            remotes[m.group(1)] = urls
+    for section, sub, name, value in parse_config(text):
+        if section == "remote" and sub is not None:
+            urls = remotes.setdefault(sub, [])
+            if name == "url":
+                urls.append(value if value is not None else "")
     return remotes
 
 
@@ -148,7 +277,11 @@ def repo_details(path, remote_name):
     branch = head_branch(git_dir)
     if branch == "":
         log.debug("Unable to get the current branch. Error: %r", "reference not found")
-    remotes = _read_config(git_dir)
+    try:
+        remotes = _read_config(git_dir)
+    except GitConfigError as e:
+        log.debug("Unable to get remote named %s Error: %r", remote_name, str(e))
+        return [], branch, root
     if remote_name not in remotes:
         log.debug("Unable to get remote named %s Error: %r", remote_name, "remote not found")
     urls = remotes.get(remote_name, [])
@@ -230,7 +363,11 @@ def repo_name(path):
     except GitError as e:
         log.debug("Unable to open %s as a git repo : %s", path, e)
         return "", ""
-    remotes = _read_config(git_dir)
+    try:
+        remotes = _read_config(git_dir)
+    except GitConfigError as e:
+        log.debug("Unable to get origin remote : %s", e)
+        return "", ""
     if "origin" not in remotes:
         log.debug("Unable to get origin remote : %s", "remote not found")
         return "", ""

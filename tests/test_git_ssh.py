@@ -132,6 +132,49 @@ def test_gather_git_info_prefers_upstream_then_origin(tmp_path):
     assert s2.repo_info.git_repo_url == "https://a/o.git"
 
 
+def test_config_is_read_as_git_config(tmp_path):
+    """go-git's config decoder: section names case-insensitive, quotes and
+    escapes removed, comments dropped, every ``url`` kept in order (the first
+    is the one GetGitRepoDetails' callers use)."""
+    cfg = ('[Remote "origin"]\n\tURL = "https://a/o.git" ; the fork\n\turl = https://b/o.git # mirror\n'
+           '[remote.Upstream]\n\turl = git@u:x/y.git\n')
+    _repo(tmp_path / "r", cfg)
+    assert git.remote_names(str(tmp_path / "r")) == ["origin", "upstream"]
+    assert git.repo_details(str(tmp_path / "r"), "origin")[0] == ["https://a/o.git", "https://b/o.git"]
+    assert git.parse_config('[a "s\\"q"]\n x = "p q" r\\\n  s\n y\n') == [("a", 's"q', "x", "p q r  s"), ("a", 's"q', "y", None)]
+
+
+def test_unparsable_config_has_no_remotes(tmp_path, capsys):
+    from move2kube_amd.utils import log
+    _repo(tmp_path / "r", '[remote "origin"]\n\turl = "https://a/o.git\n')
+    with pytest.raises(git.GitConfigError):
+        git.remote_names(str(tmp_path / "r"))
+    log.set_verbose(True)
+    try:
+        assert git.repo_details(str(tmp_path / "r"), "origin") == ([], "main", str(tmp_path / "r"))
+    finally:
+        log.set_verbose(False)
+    assert "Unable to get remote named origin Error: " in capsys.readouterr().err
+
+
+def test_dot_git_discovery_stops_at_the_first_entry(tmp_path):
+    """dotGitToOSFilesystems: the walk up stops at the first ``.git``, file or
+    directory; a ``.git`` file needs the ``gitdir: `` prefix, and a ``.git``
+    directory without HEAD is no repository (the walk does not go on)."""
+    _repo(tmp_path, _remote("https://a/top.git"))
+    bad_file = tmp_path / "sub1"
+    bad_file.mkdir()
+    (bad_file / ".git").write_text("nonsense\n")
+    with pytest.raises(git.GitError, match="^.git file has no gitdir:  prefix$"):
+        git.remote_names(str(bad_file))
+    empty = tmp_path / "sub2"
+    (empty / ".git").mkdir(parents=True)
+    with pytest.raises(git.GitError, match="^repository does not exist$"):
+        git.repo_details(str(empty), "origin")
+    (tmp_path / "sub3").mkdir()
+    assert git.repo_details(str(tmp_path / "sub3"), "origin")[2] == str(tmp_path)
+
+
 # -- known_hosts ---------------------------------------------------------------
 
 def _blob(algo):
