@@ -150,6 +150,27 @@ def read_bytes(path):
         os.close(fd)
 
 
+def go_scan_lines(data):
+    """``bufio.Scanner`` with ``ScanLines`` over ``data`` (bytes): lines split at
+    LF with one CR before it dropped, a last line without LF kept; a line of
+    64 KiB or more stops the scan (``ErrTooLong``).  -> (lines, too_long)."""
+    lines = []
+    start, n = 0, len(data)
+    while start < n:
+        end = data.find(b"\n", start)
+        stop = n if end < 0 else end
+        if stop - start >= 64 * 1024 or (end < 0 and n - start >= 64 * 1024):
+            return lines, True
+        line = data[start:stop]
+        if line.endswith(b"\r"):
+            line = line[:-1]
+        lines.append(line)
+        if end < 0:
+            break
+        start = end + 1
+    return lines, False
+
+
 def read_text(path):
     return read_bytes(path).decode("utf-8", errors="surrogateescape")
 

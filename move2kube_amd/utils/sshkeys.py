@@ -57,7 +57,8 @@ def load_known_hosts_of_current_user():
     try:
         keys = parse_known_hosts(path)
     except (OSError, KnownHostsError) as e:
-        log.warning("Failed to get public keys from the known_hosts file at path %r Error: %r", path, str(e))
+        log.warning("Failed to get public keys from the known_hosts file at path %r Error: %r", path,
+                    common.go_error_text(e))
         return
     for domain, lines in keys.items():
         DOMAIN_TO_PUBLIC_KEYS.setdefault(domain, lines)

@@ -177,40 +177,83 @@ def test_dot_git_discovery_stops_at_the_first_entry(tmp_path):
 
 # -- known_hosts ---------------------------------------------------------------
 
-def _blob(algo):
-    body = len(algo).to_bytes(4, "big") + algo.encode() + b"\x00\x00\x00\x01\x23"
-    return base64.b64encode(body).decode()
+def _keys():
+    """Public keys made with ssh-keygen (tests/fixtures/sshkeys/public_keys.txt)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "sshkeys", "public_keys.txt")
+    with open(path) as f:
+        return dict(ln.split()[0:2] for ln in f if ln.strip())
+
+
+def _wire(*fields):
+    return b"".join(len(f).to_bytes(4, "big") + f for f in fields)
+
+
+def _b64(raw):
+    return base64.b64encode(raw).decode()
 
 
 def test_parse_known_hosts(tmp_path):
+    k = _keys()
     kh = tmp_path / "known_hosts"
-    kh.write_text("\n".join([
+    kh.write_bytes(("\n".join([
         "# comment",
         "",
-        "github.com,140.82.121.3 ssh-rsa %s" % _blob("ssh-rsa"),
-        "gitlab.example.com ssh-ed25519 %s comment here" % _blob("ssh-ed25519"),
-        "@cert-authority *.example.com ssh-rsa %s" % _blob("ssh-rsa"),
-        "@revoked old.example.com ssh-rsa %s" % _blob("ssh-rsa"),
-        "|1|abc=|def= ecdsa-sha2-nistp256 %s" % _blob("ecdsa-sha2-nistp256"),
-        "github.com ecdsa-sha2-nistp256 %s" % _blob("ecdsa-sha2-nistp256"),
-    ]) + "\n")
+        "github.com,140.82.121.3 ssh-rsa %s" % k["ssh-rsa"],
+        "gitlab.example.com\tssh-ed25519   %s comment here\r" % k["ssh-ed25519"],
+        "@cert-authority *.example.com ssh-rsa %s" % k["ssh-rsa"],
+        "@revoked old.example.com ssh-dss %s" % k["ssh-dss"],
+        "|1|abc=|def= ecdsa-sha2-nistp256 %s" % k["ecdsa-sha2-nistp256"],
+        "github.com ecdsa-sha2-nistp384 %s" % k["ecdsa-sha2-nistp384"],
+        "  p521.example.com ecdsa-sha2-nistp521 %s  " % k["ecdsa-sha2-nistp521"],
+    ]) + "\n# caf\xe9\n").encode("latin-1"))   # a byte that is not UTF-8, in a comment
     got = knownhosts.parse_known_hosts(str(kh))
-    assert sorted(got) == ["140.82.121.3", "github.com", "gitlab.example.com"]
+    assert sorted(got) == ["140.82.121.3", "github.com", "gitlab.example.com", "p521.example.com"]
     assert len(got["github.com"]) == 2 and got["github.com"][0].startswith("github.com,140.82.121.3 ssh-rsa ")
-    assert got["gitlab.example.com"] == ["gitlab.example.com ssh-ed25519 %s comment here" % _blob("ssh-ed25519")]
+    assert got["gitlab.example.com"] == ["gitlab.example.com\tssh-ed25519   %s comment here" % k["ssh-ed25519"]]
+
+
+@pytest.mark.parametrize("blob,err", [
+    # ssh.ParsePublicKey (x/crypto/ssh keys.go) and base64.StdEncoding texts
+    ("!!notbase64!!", "illegal base64 data at input byte 0"),
+    ("AAAAB3NzaC1yc2E=x", "illegal base64 data at input byte 16"),
+    (_b64(_wire(b"ssh-foo")), "ssh: unknown key algorithm: ssh-foo"),
+    (_b64(b"\x00\x00\x00\x07ssh-rsa\x00\x00\x00\x01\x23"), "ssh: short read"),
+    (_b64(_wire(b"ssh-rsa", b"\x01\x00\x00\x01", b"\x00\xc3")), "ssh: exponent too large"),
+    (_b64(_wire(b"ssh-rsa", b"\x01\x00", b"\x00\xc3")), "ssh: incorrect exponent"),
+    (_b64(_wire(b"ssh-rsa", b"\x01\x00\x01", b"\x00\xc3", b"x")), "ssh: trailing junk in public key"),
+    (_b64(_wire(b"ssh-ed25519", b"\x01" * 31)), "invalid size 31 for Ed25519 public key"),
+    (_b64(_wire(b"ecdsa-sha2-nistp256", b"nistp999", b"\x04")), "ssh: unsupported curve"),
+    (_b64(_wire(b"ecdsa-sha2-nistp256", b"nistp256", b"\x04" + b"\x01" * 64)), "ssh: invalid curve point"),
+])
+def test_key_blob_errors_read_like_x_crypto_ssh(tmp_path, blob, err):
+    kh = tmp_path / "known_hosts"
+    kh.write_text("# first\nok ssh-rsa %s\nhost ssh-rsa %s\n" % (_keys()["ssh-rsa"], blob))
+    with pytest.raises(knownhosts.KnownHostsError) as ei:
+        knownhosts.parse_known_hosts(str(kh))
+    assert str(ei.value) == 'Error occurred parsing known_hosts file at path "%s" on line no. 3 Error: "%s"' % (kh, err)
 
 
 @pytest.mark.parametrize("line,err", [
     ("lonelyhost", "missing host pattern"),
+    ("@revoked", "missing host pattern"),
     ("host ssh-rsa", "missing key type pattern"),
-    ("host ssh-rsa !!notbase64!!", "invalid key blob"),
-    ("host ssh-rsa %s" % base64.b64encode(b"\x00\x00\x00\x07ssh-foo").decode(), "invalid key blob"),
 ])
 def test_parse_known_hosts_errors_name_the_line(tmp_path, line, err):
     kh = tmp_path / "known_hosts"
-    kh.write_text("# first\nok ssh-rsa %s\n%s\n" % (_blob("ssh-rsa"), line))
+    kh.write_text("# first\nok ssh-rsa %s\n%s\n" % (_keys()["ssh-rsa"], line))
     with pytest.raises(knownhosts.KnownHostsError, match="on line no. 3 .*%s" % err):
         knownhosts.parse_known_hosts(str(kh))
+
+
+def test_known_hosts_lines_split_like_bufio_scanner(tmp_path):
+    """A line of 64 KiB or more ends bufio.Scanner's scan: ParseKnownHosts
+    returns scanner.Err()."""
+    kh = tmp_path / "known_hosts"
+    kh.write_text("ok ssh-rsa %s\n# %s\n" % (_keys()["ssh-rsa"], "x" * 70000))
+    with pytest.raises(knownhosts.KnownHostsError, match="^bufio.Scanner: token too long$"):
+        knownhosts.parse_known_hosts(str(kh))
+    from move2kube_amd.utils.common import go_scan_lines
+    assert go_scan_lines(b"a\r\nb\rc\n\nd") == ([b"a", b"b\rc", b"", b"d"], False)
 
 
 def test_host_key_line_follows_go_client_preference():
@@ -283,7 +326,7 @@ def _keygen(path, kind, passphrase="", fmt=None):
 
 
 def test_known_hosts_of_user_are_added_after_confirm(qa_home):
-    (qa_home / ".ssh" / "known_hosts").write_text("git.corp.example ssh-rsa %s\n" % _blob("ssh-rsa"))
+    (qa_home / ".ssh" / "known_hosts").write_text("git.corp.example ssh-rsa %s\n" % _keys()["ssh-rsa"])
     eng = _Answers({"The CI/CD pipeline needs access": ["true"]})
     qaengine.add_engine(eng)
     sshkeys.load_known_hosts_of_current_user()
@@ -294,7 +337,7 @@ def test_known_hosts_of_user_are_added_after_confirm(qa_home):
 
 
 def test_known_hosts_not_read_when_declined(qa_home):
-    (qa_home / ".ssh" / "known_hosts").write_text("declined.example ssh-rsa %s\n" % _blob("ssh-rsa"))
+    (qa_home / ".ssh" / "known_hosts").write_text("declined.example ssh-rsa %s\n" % _keys()["ssh-rsa"])
     qaengine.add_engine(_Answers({}))                    # the default is "no"
     sshkeys.load_known_hosts_of_current_user()
     assert "declined.example" not in sshkeys.DOMAIN_TO_PUBLIC_KEYS
