@@ -255,8 +255,10 @@ def _subprocess_errors(name):
     then no such error can have been raised (the tools run through
     ``utils.proc``, which loads it only to raise a timeout), and naming it in
     an ``except`` would import it into a cold CLI process."""
-    sp = sys.modules.get("subprocess")
-    return (getattr(sp, name),) if sp is not None else ()
+    # another thread may be importing it right now: a partly initialised
+    # module lacks the name, and nothing it has not defined can be raised yet
+    err = getattr(sys.modules.get("subprocess"), name, None)
+    return (err,) if err is not None else ()
 
 
 def _chain_errors():

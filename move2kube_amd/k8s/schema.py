@@ -17,6 +17,8 @@ a struct name, ``*T`` (pointer), ``[]T`` (slice), ``map:T`` (map of T) or
 ``inline:T`` (embedded struct).
 """
 
+import _thread
+
 _STRUCTS = {}  # struct name -> its field DSL string (parsed on use: _fields)
 _parsed = {}
 
@@ -681,6 +683,7 @@ def _marshal_fields(d, typ):
 
 
 _native_fn = None
+_native_lock = _thread.RLock()
 
 
 def _native_marshal():
@@ -688,15 +691,21 @@ def _native_marshal():
     compiled from the ``_STRUCTS`` field strings on first use; False when it is unavailable or
     ``M2K_NATIVE_MARSHAL=0``.  This module stays its specification."""
     global _native_fn
-    if _native_fn is None:
-        _native_fn = False
-        import os
-        if os.environ.get("M2K_NATIVE_MARSHAL", "1") != "0":
-            from ..ops import native
-            m = native.module()
-            if m is not None and hasattr(m, "schema_marshal"):
-                m.schema_init(_STRUCTS, _marshal_value)
-                _native_fn = m.schema_marshal
+    if _native_fn is not None:
+        return _native_fn
+    with _native_lock:   # threads asking at once wait for one initialisation
+        if _native_fn is None:
+            fn = False
+            import os
+            try:
+                if os.environ.get("M2K_NATIVE_MARSHAL", "1") != "0":
+                    from ..ops import native
+                    m = native.module()
+                    if m is not None and hasattr(m, "schema_marshal"):
+                        m.schema_init(_STRUCTS, _marshal_value)
+                        fn = m.schema_marshal
+            finally:
+                _native_fn = fn
     return _native_fn
 
 

@@ -6,6 +6,7 @@ machine that exposes an AMD GPU (``/dev/kfd``) a missing library is an error
 callers use the native CPU path.
 """
 
+import _thread
 import ctypes
 import os
 
@@ -16,6 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libm2k_ed_hip.so")
 
 _lib = None
 _state = None  # None=untried, True=ok, False=unavailable
+_lock = _thread.RLock()
 
 
 class GpuUnavailable(RuntimeError):
@@ -37,6 +39,13 @@ def gpu_host():
 
 
 def _load():
+    if _state is not None:
+        return _lib
+    with _lock:   # one thread loads; the others wait for it
+        return _load_locked()
+
+
+def _load_locked():
     global _lib, _state
     if _state is not None:
         return _lib

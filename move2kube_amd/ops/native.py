@@ -6,26 +6,33 @@ fallback so the framework still runs where the extension was not built; set
 ``M2K_REQUIRE_NATIVE=1`` to make a missing extension an error.
 """
 
+import _thread
 import os
 
 _mod = None
 _tried = False
+_lock = _thread.RLock()
 
 
 def _load():
+    """The extension module, or None.  Loaded once under a lock: a second
+    thread asking while the first is still importing waits for it instead of
+    being told there is none (collector and probe threads start together)."""
     global _mod, _tried
     if _tried:
         return _mod
-    _tried = True
-    if os.environ.get("M2K_DISABLE_NATIVE"):
-        return None
-    try:
-        from . import _m2k_native as m  # noqa: F401
-        _mod = m
-    except ImportError:
-        if os.environ.get("M2K_REQUIRE_NATIVE"):
-            raise
-        _mod = None
+    with _lock:
+        if not _tried:
+            mod = None
+            if not os.environ.get("M2K_DISABLE_NATIVE"):
+                try:
+                    from . import _m2k_native as mod  # noqa: F811
+                except ImportError:
+                    if os.environ.get("M2K_REQUIRE_NATIVE"):
+                        raise
+                    mod = None
+            _mod = mod
+            _tried = True
     return _mod
 
 

@@ -77,10 +77,10 @@ class Any2KubeTranslator(Translator):
                 for d, o in zip(candidates, opts):
                     if o:
                         matched[d] = o
-                    elif not common.is_string_present(ignore_contents, d):
+                        continue
+                    log.debug("No known containerization approach is supported for directory %r", d)
+                    if not common.is_string_present(ignore_contents, d):
                         nxt.extend(children.get(d, []))
-                    else:
-                        log.debug("No known containerization approach is supported for directory %r", d)
             frontier = nxt
         for path in sorted(matched, key=lambda p: p.split("/")):
             for cop in matched[path]:
@@ -130,13 +130,15 @@ class Any2KubeTranslator(Translator):
             return ignore_dirs, ignore_contents
         for fp in files:
             try:
-                text = common.read_text(fp)
+                data = common.read_bytes(fp)
             except OSError as e:
                 log.warning("Failed to open the .m2kignore file at path %r Error: %r", fp, common.go_path_error(e, "open"))
                 continue
             base = os.path.dirname(fp)
-            for raw in text.splitlines():
-                line = raw.strip()
+            # bufio.Scanner lines: LF only, a CR before it dropped, the scan
+            # silently ending at a line of 64 KiB or more (any2kube.go:165-178)
+            for raw in common.go_scan_lines(data)[0]:
+                line = common.go_trim_space(raw.decode("utf-8", errors="surrogateescape"))
                 if line.endswith("*"):
                     ignore_contents.append(common.go_join(base, line[:-1]))
                 else:

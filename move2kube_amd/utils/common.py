@@ -150,6 +150,16 @@ def read_bytes(path):
         os.close(fd)
 
 
+_GO_SPACE = ("\t\n\v\f\r \x85\xa0\u1680\u2000\u2001\u2002\u2003\u2004\u2005\u2006\u2007\u2008\u2009"
+             "\u200a\u2028\u2029\u202f\u205f\u3000")
+
+
+def go_trim_space(s):
+    """``strings.TrimSpace`` / ``bytes.TrimSpace``: Unicode white space
+    (``unicode.IsSpace``), not Python's wider ``str.strip()`` set."""
+    return s.strip(_GO_SPACE)
+
+
 def go_scan_lines(data):
     """``bufio.Scanner`` with ``ScanLines`` over ``data`` (bytes): lines split at
     LF with one CR before it dropped, a last line without LF kept; a line of

@@ -13,6 +13,7 @@ import os
 import shutil
 
 from . import log
+from .common import go_scan_lines, go_trim_space
 
 MARKER_CERT = "@cert-authority"
 MARKER_REVOKED = "@revoked"
@@ -159,15 +160,6 @@ def parse_public_key(raw):
         raise KnownHostsError("ssh: trailing junk in public key")
 
 
-_GO_SPACE = ("\t\n\v\f\r \x85\xa0\u1680\u2000\u2001\u2002\u2003\u2004\u2005\u2006\u2007\u2008\u2009"
-             "\u200a\u2028\u2029\u202f\u205f\u3000")
-
-
-def go_trim_space(s):
-    """``bytes.TrimSpace``: Unicode white space (not Python's wider set)."""
-    return s.strip(_GO_SPACE)
-
-
 def _next_word(line):
     """``nextWord``: up to the first space or tab, and the trimmed rest."""
     cut = [k for k in (line.find(" "), line.find("\t")) if k >= 0]
@@ -200,7 +192,6 @@ def parse_known_hosts(path):
     """``ParseKnownHosts`` (knownhosts.go:84-121): host -> key lines.  Lines
     are split as ``bufio.Scanner`` splits them (LF; a CR before it dropped; a
     line of 64 KiB or more ends the scan with ``token too long``)."""
-    from .common import go_scan_lines
     with open(path, "rb") as f:
         data = f.read()
     out = {}

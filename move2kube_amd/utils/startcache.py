@@ -24,6 +24,8 @@ A missing, unreadable or foreign file disables the cache; nothing else
 changes.  ``M2K_STARTCACHE=0`` turns it off.
 """
 
+import _thread
+
 import marshal
 import os
 import sys
@@ -39,6 +41,7 @@ def parser_sources():
     return (GOTEMPLATE_SRC, GOTEMPLATE_PARSE_SRC)
 
 _state = None  # None: not read yet; False: unusable; else (templates, regexes)
+_lock = _thread.RLock()
 
 
 def interpreter_tag():
@@ -62,6 +65,11 @@ def source_digest(paths):
 
 
 def _load():
+    with _lock:   # threads asking at once read the file once; none sees it half read
+        return _state if _state is not None else _read()
+
+
+def _read():
     global _state
     _state = False
     if os.environ.get("M2K_STARTCACHE", "1") == "0":

@@ -5,6 +5,7 @@ import itertools
 import json
 import os
 import socketserver
+import sys
 import threading
 from http.server import BaseHTTPRequestHandler
 
@@ -485,3 +486,14 @@ def test_no_background_probes_when_the_docker_socket_exists(monkeypatch, tmp_pat
     providers.start_runtime_prefetch(["b"])
     assert all(getattr(p, "_pending", None) is None for p in providers.providers())
     providers.reset_providers()
+
+
+def test_error_tuples_tolerate_a_partly_imported_subprocess(monkeypatch):
+    """Another thread importing ``subprocess`` leaves a partly initialised
+    module in sys.modules for a moment (a collector thread did, and the
+    container-types collector failed with "partially initialized module
+    'subprocess' has no attribute 'SubprocessError'" once in ~30 runs)."""
+    import types
+    monkeypatch.setitem(sys.modules, "subprocess", types.ModuleType("subprocess"))
+    assert providers._chain_errors() == (providers.ProviderError, OSError, ValueError, KeyError)
+    assert providers._start_errors() == (OSError,)

@@ -151,3 +151,30 @@ def test_sniff_dockerfiles_undecodable_from_line(tmp_path):
     want = dockerfile_parser.sniff_first_from(str(p))
     assert native.sniff_dockerfiles([str(p)]) == [want]
     assert native.sniff_dockerfiles([str(p)] * 100) == [want] * 100
+
+
+def test_native_module_load_waits_for_a_loading_thread(monkeypatch):
+    """Threads asking for the extension while another thread is still loading
+    it get the module, not None (a collector thread once fell back to the
+    Python process runner this way and imported subprocess half-way under
+    another thread's feet)."""
+    import threading
+    import time
+    import types
+    from move2kube_amd.ops import native
+    real = native.module()
+
+    class SlowEnviron(dict):
+        def get(self, key, default=None):
+            time.sleep(0.05)   # widen the loading window
+            return os.environ.get(key, default)
+    monkeypatch.setattr(native, "os", types.SimpleNamespace(environ=SlowEnviron()))
+    monkeypatch.setattr(native, "_tried", False)
+    monkeypatch.setattr(native, "_mod", None)
+    got = []
+    threads = [threading.Thread(target=lambda: got.append(native.module())) for _ in range(8)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert got == [real] * 8
