@@ -160,10 +160,14 @@ std::string ltrim(const std::string &s) {
   return s.substr(i);
 }
 
+// the instruction word of a logical line (buildkit splitCommand trims the line
+// first: a line continued from an empty first line keeps its leading blanks)
 std::string lower_word(const std::string &s) {
-  size_t i = 0;
+  size_t b = 0;
+  while (b < s.size() && is_space((unsigned char)s[b])) b++;
+  size_t i = b;
   while (i < s.size() && !is_space((unsigned char)s[i])) i++;
-  std::string w = s.substr(0, i);
+  std::string w = s.substr(b, i - b);
   for (auto &c : w) c = (char)tolower((unsigned char)c);
   return w;
 }

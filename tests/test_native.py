@@ -178,3 +178,44 @@ def test_native_module_load_waits_for_a_loading_thread(monkeypatch):
     for t in threads:
         t.join()
     assert got == [real] * 8
+
+
+def test_dockerfile_sniff_native_matches_python_on_mutated_dockerfiles(tmp_path):
+    """Differential fuzz of ops/csrc/m2k_native.cpp:sniff_one against
+    source/dockerfile_parser.py:sniff_first_from over mutated Dockerfiles
+    (directives, continuations with either escape, comments, CRLF, BOMs, bytes
+    that are not UTF-8).  It found a first line holding only a continuation:
+    buildkit trims the joined line before reading the instruction, so
+    '\\\\\\n  FROM x' is a FROM."""
+    import glob
+    import random
+    from move2kube_amd.ops import native
+    from move2kube_amd.source.dockerfile_parser import sniff_first_from
+    m = native.module()
+    if m is None:
+        pytest.skip("native extension not built")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    seeds = [open(p, "rb").read() for p in sorted(glob.glob(os.path.join(root, "samples", "**", "Dockerfile*"),
+                                                            recursive=True))]
+    toks = [b"\n", b"\r\n", b"\\\n", b"`\n", b"# escape=`\n", b"# escape=\\\n", b"#syntax=x\n", b"ARG X=1\n",
+            b"FROM ", b"from ", b" AS ", b"--platform=linux ", b"# c\n", b"\t", b"  ", b"\xff", b"\xef\xbb\xbf",
+            b"\\", b"`", b"#", b"ARG\n", b"FROM\n", b"\r"]
+    rnd = random.Random(7)
+    path = str(tmp_path / "Dockerfile")
+    assert seeds
+    for _ in range(3000):
+        s = bytearray(rnd.choice(seeds))
+        for _ in range(rnd.randint(1, 6)):
+            i = rnd.randrange(len(s) + 1)
+            if rnd.random() < 0.3 and i < len(s):
+                del s[i:i + rnd.randint(1, 8)]
+            else:
+                s[i:i] = rnd.choice(toks)
+        if rnd.random() < 0.2:
+            s[0:0] = rnd.choice(toks)
+        with open(path, "wb") as f:
+            f.write(bytes(s))
+        assert m.sniff_dockerfiles([os.fsencode(path)], 1)[0] == sniff_first_from(path), bytes(s)[:200]
+    with open(path, "wb") as f:
+        f.write(b"\\\n  FROM node:14\n")
+    assert m.sniff_dockerfiles([os.fsencode(path)], 1)[0] == sniff_first_from(path) == "  FROM node:14"
