@@ -70,7 +70,32 @@ def loads(s, parse_int=int):
     except (StopIteration, ValueError, _GoRejects, RecursionError):
         raw = s if isinstance(s, (bytes, bytearray)) else s.encode("utf-8", "surrogatepass")
         raise ValueError(go_syntax_error(bytes(raw)) or "invalid JSON") from None
+    if "\\u" in text or (text is s and not _valid_utf8(text)):
+        obj = _no_lone_surrogates(obj)
     return obj
+
+
+def _valid_utf8(t):
+    try:
+        t.encode("utf-8")
+        return True
+    except UnicodeEncodeError:
+        return False
+
+
+def _no_lone_surrogates(o):
+    """decode.go unquote: a ``\\uD800``-range escape that is not half of a
+    pair, like a byte that is not UTF-8, becomes U+FFFD (the scanner has
+    already joined the pairs, so every surrogate left is a lone one)."""
+    if isinstance(o, str):
+        if _valid_utf8(o):
+            return o
+        return "".join("\ufffd" if "\ud800" <= c <= "\udfff" else c for c in o)
+    if isinstance(o, list):
+        return [_no_lone_surrogates(x) for x in o]
+    if isinstance(o, dict):
+        return {_no_lone_surrogates(k): _no_lone_surrogates(v) for k, v in o.items()}
+    return o
 
 
 def load(f, parse_int=int):

@@ -59,3 +59,17 @@ def test_loads_errors_are_go_texts(text, err):
     with pytest.raises(ValueError) as ei:
         fastjson.loads(text)
     assert str(ei.value) == err
+
+
+@pytest.mark.parametrize("text,want", [
+    # encoding/json decode.go unquote: a surrogate escape that is not half of a
+    # pair decodes to U+FFFD, as a byte that is not UTF-8 does
+    ('"\\ud800"', "�"),
+    ('"\\udc80x"', "�x"),
+    ('"\\ud83d\\ude00"', "\U0001F600"),
+    ('{"\\ude00\\ud83d": ["a", "\\ud801"]}', {"��": ["a", "�"]}),
+    ('"\udcff"', "�"),          # a surrogate-escaped byte of a file read as text
+    (b'"\xff"', "�"),
+])
+def test_lone_surrogates_decode_to_the_replacement_character(text, want):
+    assert fastjson.loads(text) == want
