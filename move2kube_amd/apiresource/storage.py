@@ -89,7 +89,7 @@ def convert_cfgmap_to_secret(cm):
     if m.get("labels"):
         md["labels"] = dict(m["labels"])
     return {"kind": SECRET_KIND, "apiVersion": "v1", "metadata": md, "type": "Opaque",
-            "data": {k: (v.encode() if isinstance(v, str) else v) for k, v in (cm.get("data") or {}).items()}}
+            "data": {k: (common.go_bytes(v) if isinstance(v, str) else v) for k, v in (cm.get("data") or {}).items()}}
 
 
 def convert_secret_to_cfgmap(s):

@@ -36,7 +36,7 @@ import threading
 import time
 import urllib.parse
 
-from ..utils import log, yamlio
+from ..utils import common, log, yamlio
 
 DISCOVERY_TIMEOUT = 32.0  # client-go's default discovery timeout
 MAX_PARALLEL = 8
@@ -227,7 +227,7 @@ class KubeconfigClient(_HTTPClient):
             headers["Authorization"] = "Bearer " + token
         elif user.get("username") or user.get("password"):
             cred = "%s:%s" % (user.get("username", ""), user.get("password", ""))
-            headers["Authorization"] = "Basic " + base64.b64encode(cred.encode()).decode()
+            headers["Authorization"] = "Basic " + base64.b64encode(common.go_bytes(cred)).decode()
         ctx = None
         if u.scheme == "https":
             ctx = self._ssl_context(cluster, user)
@@ -241,7 +241,7 @@ class KubeconfigClient(_HTTPClient):
             ctx.check_hostname = False
             ctx.verify_mode = ssl.CERT_NONE
         elif cluster.get("certificate-authority-data"):
-            ctx.load_verify_locations(cadata=base64.b64decode(cluster["certificate-authority-data"]).decode())
+            ctx.load_verify_locations(cadata=base64.b64decode(cluster["certificate-authority-data"]).decode("utf-8", "replace"))
         elif cluster.get("certificate-authority"):
             ctx.load_verify_locations(cafile=cluster["certificate-authority"])
         cert, key = user.get("client-certificate-data"), user.get("client-key-data")

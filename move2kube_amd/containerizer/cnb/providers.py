@@ -116,7 +116,7 @@ class DockerAPIProvider:
             raise ProviderError("docker API %s %s: %d %s" % (method, path, resp.status, data[:200]))
         if raw:
             return data
-        return fastjson.loads(data.decode() or "null") if data else None
+        return fastjson.loads(data) if data else None
 
     def pull_image(self, image):
         name, tag = (image.rsplit(":", 1) + ["latest"])[:2] if ":" in image.rsplit("/", 1)[-1] else (image, "latest")
@@ -567,7 +567,7 @@ class ContainerRuntimeProvider:
             if p.returncode != 0:
                 log.debug("Unable to inspect image %s : %s, %s", b, _go_err(p, rt), _out(p))
                 continue
-            out[b] = get_builders_from_label(p.stdout.decode())
+            out[b] = get_builders_from_label(p.stdout.decode("utf-8", "replace"))
         return out
 
 
@@ -690,7 +690,7 @@ class RuncProvider:
             if p.returncode != 0:
                 continue
             try:
-                labels = fastjson.loads(p.stdout.decode()).get("Labels") or {}
+                labels = fastjson.loads(p.stdout).get("Labels") or {}
             except ValueError:
                 continue
             if ORDER_LABEL in labels:

@@ -47,9 +47,9 @@ def _gpu_warm():
 
 def wagner_fischer_py(a, b, icost=1, dcost=1, scost=2):
     if isinstance(a, str):
-        a = a.encode()
+        a = a.encode("utf-8", "surrogateescape")
     if isinstance(b, str):
-        b = b.encode()
+        b = b.encode("utf-8", "surrogateescape")
     row1 = [j * icost for j in range(len(b) + 1)]
     for i in range(1, len(a) + 1):
         row2 = [i * dcost] + [0] * len(b)
@@ -77,7 +77,7 @@ def _use_gpu(pairs, device, queries):
     if device != "gpu" and pairs < GPU_MIN_PAIRS:
         return False
     gpu = _gpu()
-    fits = all(len(q.encode() if isinstance(q, str) else q) <= 64 for q in queries)
+    fits = all(len(q.encode("utf-8", "surrogateescape") if isinstance(q, str) else q) <= 64 for q in queries)
     if device == "gpu":
         if not fits:
             raise gpu.GpuUnavailable("queries longer than 64 bytes are not supported on the GPU path")

@@ -107,7 +107,7 @@ def _pack(strings):
     if m is not None and isinstance(strings, list):
         data, off, maxlen = m.pack_strings(strings)
         return data, off, int(maxlen)
-    bs = [s.encode() if isinstance(s, str) else bytes(s) for s in strings]
+    bs = [s.encode("utf-8", "surrogateescape") if isinstance(s, str) else bytes(s) for s in strings]
     lens = np.fromiter((len(b) for b in bs), dtype=np.int64, count=len(bs))
     off = np.zeros(len(bs) + 1, dtype=np.int64)
     np.cumsum(lens, out=off[1:])

@@ -94,7 +94,7 @@ def _find_main(d):
 
 
 def _ok(s):
-    return 0, s.encode()
+    return 0, s.encode("utf-8", "surrogateescape")
 
 
 _FAIL = (1, b"")

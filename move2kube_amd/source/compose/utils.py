@@ -36,7 +36,7 @@ def is_path(s):
 
 
 def get_hash(data):
-    return common.fnv64a(data.encode() if isinstance(data, str) else data)
+    return common.fnv64a(data)
 
 
 # ---------------------------------------------------------------------------

@@ -84,17 +84,27 @@ def fnv64a_py(data):
     return h
 
 
+def go_bytes(s):
+    """The bytes of a Go string held as ``str``: UTF-8, with the
+    surrogate-escaped bytes of a name or file that is not UTF-8 given back as
+    they were read (``str.encode()`` would fail on them)."""
+    try:
+        return s.encode("utf-8", "surrogateescape")
+    except UnicodeEncodeError:   # a lone surrogate from elsewhere: keep it encodable
+        return s.encode("utf-8", "surrogatepass")
+
+
 def crc64_ecma(data):
     from ..ops import native
     if isinstance(data, str):
-        data = data.encode()
+        data = go_bytes(data)
     return native.crc64_ecma(data)
 
 
 def fnv64a(data):
     from ..ops import native
     if isinstance(data, str):
-        data = data.encode()
+        data = go_bytes(data)
     return native.fnv64a(data)
 
 
@@ -325,7 +335,7 @@ def normalize_for_filename(name):
     processed = make_file_name_compliant(name)
     if len(processed) > 15:
         processed = processed[:15]
-    return processed + "-" + format(crc64_ecma(name.encode()), "x")
+    return processed + "-" + format(crc64_ecma(go_bytes(name)), "x")
 
 
 def go_lower(s):

@@ -130,3 +130,21 @@ def test_a_yaml_bomb_only_loses_itself(tmp_path):
     with api.Session(qaskip=True) as s:
         out = _bounded(lambda: s.translate(str(src), str(tmp_path / "out")), 60)
     assert "web-deployment.yaml" in os.listdir(os.path.join(out, "myproject"))
+
+
+def test_compose_service_in_a_non_utf8_directory(tmp_path):
+    """A compose file under a directory whose name is not UTF-8: the volume
+    hash is taken over the name's bytes, as Go hashes its string, instead of
+    failing the whole compose translation on the undecodable byte."""
+    bsrc = os.fsencode(str(tmp_path / "src"))
+    d = os.path.join(bsrc, b"caf\xe9")
+    os.makedirs(os.path.join(d, b"data"))
+    with open(os.path.join(d, b"docker-compose.yaml"), "wb") as f:
+        f.write(b'version: "3"\nservices:\n  web:\n    image: nginx\n    volumes:\n      - ./data:/data\n'
+                b'    ports:\n      - "80:80"\n')
+    with api.Session(qaskip=True) as s:
+        out = _bounded(lambda: s.translate(str(tmp_path / "src"), str(tmp_path / "out")), 60)
+    assert sorted(os.listdir(os.path.join(out, "myproject"))) == ["web-deployment.yaml", "web-ingress.yaml",
+                                                                  "web-service.yaml"]
+    assert common.fnv64a(os.fsdecode(b"caf\xe9")) == common.fnv64a(b"caf\xe9")
+    assert common.normalize_for_filename(os.fsdecode(b"\xff")) == "--" + format(common.crc64_ecma(b"\xff"), "x")
