@@ -155,3 +155,44 @@ def test_packaged_assets_used_in_place_and_never_removed(tmp_path):
         assert not os.path.exists(scratch)
     finally:
         settings.temp_path, settings.assets_path = saved
+
+
+def test_builtin_matches_scripts_on_random_trees(tmp_path, assets_dir, monkeypatch):
+    """Random trees of detector marker files (nested, hidden, dangling
+    symlinks, directories named like markers, contents that are not UTF-8):
+    every built-in detector answers as its shell script does."""
+    import random
+    names = ["package.json", "pom.xml", "build.gradle", "requirements.txt", "setup.py", "Pipfile", "Gemfile", "go.mod",
+             "main.go", ".h.go", "a.war", "a b.war", "A.java", "index.php", "build.xml", "composer.json", "manage.py",
+             "main.py", "app.py", "Gemfile.lock", "config.ru", "x.GO", "X.WAR", "package.JSON", "sub", "src"]
+    contents = ["", "{}", '{"scripts": {"start": "node x"}}', "if __name__ == '__main__':\n  run()\n",
+                "module example.com/x\n", "package main\n", "flask\n", "\xff\xfe"]
+    rnd = random.Random(11)
+    for it in range(40):
+        targets = []
+        for t in range(6):
+            d = tmp_path / ("i%d" % it) / ("t%d" % t)
+            d.mkdir(parents=True)
+            for _ in range(rnd.randint(0, 5)):
+                p = d / rnd.choice(["", "sub/", "src/main/", ".hidden/"]) / rnd.choice(names)
+                try:
+                    p.parent.mkdir(parents=True, exist_ok=True)
+                except (FileExistsError, NotADirectoryError):
+                    continue
+                if os.path.lexists(p):
+                    continue
+                if rnd.random() < 0.1:
+                    p.mkdir()
+                else:
+                    p.write_text(rnd.choice(contents), encoding="latin-1")
+            if rnd.random() < 0.1:
+                os.symlink("/nonexistent", str(d / rnd.choice(names)))
+            targets.append(str(d))
+        jobs = [(os.path.join(assets_dir, rel), script, t) for rel, script in sorted(builtin_detect.DETECTORS)
+                for t in targets]
+        monkeypatch.delenv("M2K_NATIVE_DETECT", raising=False)
+        ours = detect_pool.run_detect_jobs(jobs)
+        monkeypatch.setenv("M2K_NATIVE_DETECT", "0")
+        scripts = detect_pool.run_detect_jobs(jobs)
+        assert [(j, a.code == 0, a.stdout if a.code == 0 else None) for j, a in zip(jobs, ours)] == \
+            [(j, b.code == 0, b.stdout if b.code == 0 else None) for j, b in zip(jobs, scripts)]
