@@ -82,7 +82,7 @@ class Any2KubeTranslator(Translator):
                     if not common.is_string_present(ignore_contents, d):
                         nxt.extend(children.get(d, []))
             frontier = nxt
-        for path in sorted(matched, key=lambda p: p.split("/")):
+        for path in sorted(matched, key=lambda p: os.fsencode(p).split(b"/")):   # the walk's order: bytes
             for cop in matched[path]:
                 s = self.new_service(os.path.basename(path))
                 s.container_build_type = cop.containerization_type

@@ -313,7 +313,7 @@ def _walk_py(root):
         kinds.append(DIR)
         try:
             with os.scandir(d) as it:
-                entries = sorted((e.name, e) for e in it)
+                entries = sorted(((e.name, e) for e in it), key=lambda ne: os.fsencode(ne[0]))   # Go: byte order
         except OSError as e:
             errors.append((d, "open %s: %s" % (d, _go_errno_text(e.errno))))
             return

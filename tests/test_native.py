@@ -219,3 +219,20 @@ def test_dockerfile_sniff_native_matches_python_on_mutated_dockerfiles(tmp_path)
     with open(path, "wb") as f:
         f.write(b"\\\n  FROM node:14\n")
     assert m.sniff_dockerfiles([os.fsencode(path)], 1)[0] == sniff_first_from(path) == "  FROM node:14"
+
+
+def test_walk_order_is_byte_order_in_both_walkers(tmp_path):
+    """filepath.Walk visits names in byte order (sort.Strings); the Python
+    walker sorted str, which puts a surrogate-escaped byte (0xf5 ->
+    U+DCF5) before U+E000 (bytes ee 80 80)."""
+    from move2kube_amd.utils import fsindex
+    base = os.fsencode(str(tmp_path))
+    for name in (b"\xf5x", b"\xee\x80\x80", b"\xf0\x9f\x98\x80", b"a", b"\xff"):
+        os.makedirs(os.path.join(base, name, b"sub"))
+    want = sorted(os.listdir(base))       # bytes sort
+    ppaths, _, _ = fsindex._walk_py(str(tmp_path))
+    top = [p for p in ppaths if os.path.dirname(p) == str(tmp_path)]
+    assert [os.fsencode(os.path.basename(p)) for p in top] == want
+    if native.available():
+        npaths, _, _ = native.module().walk(base)
+        assert list(npaths) == list(ppaths)
