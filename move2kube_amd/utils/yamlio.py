@@ -220,8 +220,11 @@ def _is_space(ch):
 
 
 def _is_printable(ch):
+    """yamlprivateh.go is_printable: NEL (U+0085) is not printable for the
+    emitter (PyYAML's emitter counts it), so a string holding one is written
+    double-quoted with ``\\N`` and reads back unchanged."""
     o = ord(ch)
-    return (o == 0x0A or 0x20 <= o <= 0x7E or o == 0x85 or 0xA0 <= o <= 0xD7FF
+    return (o == 0x0A or 0x20 <= o <= 0x7E or 0xA0 <= o <= 0xD7FF
             or 0xE000 <= o <= 0xFFFD and o != 0xFEFF or 0x10000 <= o <= 0x10FFFF)
 
 

@@ -88,3 +88,13 @@ def test_decode_failures_read_like_go_yaml(text, want):
         with pytest.raises(yamlio.YAMLError) as ei:
             load(text)
         assert str(ei.value) == want
+
+
+def test_nel_is_not_printable_for_the_emitter():
+    """yamlprivateh.go is_printable leaves out NEL (U+0085): a string holding
+    one is written double-quoted with the \\N escape (PyYAML's emitter would
+    write it raw, and the reader turns a raw NEL into a line break)."""
+    for v in ("a\x85b", "\x85", "a\nb\x85c"):
+        text = yamlio.dump({"k": [v]})
+        assert "\x85" not in text and "\\N" in text
+        assert yamlio.load(text) == {"k": [v]}
