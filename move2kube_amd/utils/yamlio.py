@@ -406,9 +406,15 @@ def _literal(s, indent):
     buf = []
     breaks = True
     for ch in s:
-        if _is_break(ch):
+        if ch == "\n":
             lines.append("".join(buf))
             buf = []
+            breaks = True
+        elif _is_break(ch):
+            # emitterc.go write_break: a break other than LF (LS, PS: the
+            # printable ones that reach a literal) is written as itself, and
+            # the next line's indentation follows it on the same output line
+            buf.append(ch)
             breaks = True
         else:
             if breaks:

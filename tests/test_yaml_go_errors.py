@@ -98,3 +98,13 @@ def test_nel_is_not_printable_for_the_emitter():
         text = yamlio.dump({"k": [v]})
         assert "\x85" not in text and "\\N" in text
         assert yamlio.load(text) == {"k": [v]}
+
+
+def test_line_and_paragraph_separators_in_a_literal_scalar():
+    """emitterc.go write_break writes a break other than LF as itself and the
+    next line's indentation follows it, so LS/PS inside a literal block read
+    back unchanged (splitting lines there turned them into LF)."""
+    for v in ("a\u2028b\nc", "x\u2029y\nz", "a\nb\u2028c"):
+        text = yamlio.dump({"k": [v]})
+        assert text.startswith("k:\n  - |-\n") and ("\u2028" in text or "\u2029" in text)
+        assert yamlio.load(text) == {"k": [v]}
