@@ -335,8 +335,25 @@ def _double_quoted(s):
     return "".join(out)
 
 
-def _single_quoted(s):
-    return "'" + s.replace("'", "''") + "'"
+def _single_quoted(s, indent=0):
+    """emitterc.go write_single_quoted_scalar: quotes doubled; a break (LS or
+    PS: LF and the unprintable ones never get this style) is written as
+    itself and the next character starts after the indentation."""
+    if "\u2028" not in s and "\u2029" not in s:
+        return "'" + s.replace("'", "''") + "'"
+    out = ["'"]
+    breaks = False
+    for ch in s:
+        if ch in "\u2028\u2029":
+            out.append(ch)
+            breaks = True
+            continue
+        if breaks:
+            out.append(" " * indent)
+            breaks = False
+        out.append("''" if ch == "'" else ch)
+    out.append("'")
+    return "".join(out)
 
 
 PLAIN, SINGLE, DOUBLE, LITERAL = range(4)
@@ -498,7 +515,7 @@ class _Emitter:
         if style == PLAIN:
             return [s]
         if style == SINGLE:
-            return [_single_quoted(s)]
+            return [_single_quoted(s, indent)]
         if style == DOUBLE:
             return [_double_quoted(s)]
         return _literal(s, indent)

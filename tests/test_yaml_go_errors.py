@@ -108,3 +108,13 @@ def test_line_and_paragraph_separators_in_a_literal_scalar():
         text = yamlio.dump({"k": [v]})
         assert text.startswith("k:\n  - |-\n") and ("\u2028" in text or "\u2029" in text)
         assert yamlio.load(text) == {"k": [v]}
+
+
+def test_line_separator_in_a_single_quoted_scalar():
+    """write_single_quoted_scalar: LS/PS are written as themselves and the next
+    character follows the indentation, so '--- x' after one is not read as a
+    document marker at column 0."""
+    for doc in ({"k": ["true --- x"]}, {"k": "a b"}, {"a": {"b": ["x  y"]}}):
+        text = yamlio.dump(doc)
+        assert "'" in text and " \n" not in text
+        assert yamlio.load(text) == doc
