@@ -114,7 +114,7 @@ def test_line_separator_in_a_single_quoted_scalar():
     """write_single_quoted_scalar: LS/PS are written as themselves and the next
     character follows the indentation, so '--- x' after one is not read as a
     document marker at column 0."""
-    for doc in ({"k": ["true --- x"]}, {"k": "a b"}, {"a": {"b": ["x  y"]}}):
+    for doc in ({"k": ["true\u2028--- x"]}, {"k": "a\u2029b"}, {"a": {"b": ["x\u2028\u2028y"]}}):
         text = yamlio.dump(doc)
-        assert "'" in text and " \n" not in text
+        assert "'" in text and "\u2028\n" not in text
         assert yamlio.load(text) == doc
