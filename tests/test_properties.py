@@ -167,3 +167,37 @@ def test_translate_never_crashes_on_arbitrary_manifests(tmp_path, monkeypatch):
         except log.FatalError as e:
             assert "No containerization technique was selected" in str(e), str(e)
     assert done > 0
+
+
+_qa_atoms = st.sampled_from(["a", "b c", "", " lead", "trail ", "x:y", "- d", "#h", "'q'", '"dq"', "\\", "é", "中", "1",
+                             "1.5", "true", "null", "~", "yes", "0x1f", "a\nb", "*a", "&b", "!t", "%p", "@", "`", "{}",
+                             "[]", "a, b", "?", "--- x", "...", "<<", " x", "\x85", "\x7f", "\x01"])
+_qa_text = st.lists(_qa_atoms, min_size=1, max_size=3).map("".join)
+
+
+@settings(max_examples=int(os.environ.get("M2K_PROP_EXAMPLES", "300")), deadline=None)
+@given(st.lists(st.tuples(_qa_text, _qa_text, _qa_text), min_size=1, max_size=4))
+def test_qa_cache_answers_survive_a_write_and_read(tmp_path_factory, answers):
+    """A QA cache written by this emitter reads back with the same
+    descriptions, contexts and answers (go-yaml's emitter and reader agree on
+    these strings: NEL double-quoted, LS kept raw with the indentation after)."""
+    from move2kube_amd.models import qa
+    path = str(tmp_path_factory.mktemp("qa") / "cache.yaml")
+    c = qa.Cache(path)
+    seen = set()
+    for desc, ctx, ans in answers:
+        if desc in seen:
+            continue
+        try:
+            p = qa.new_input_problem(desc, [ctx], "d")
+            p.set_answer([ans])
+        except qa.ProblemError:   # not a problem the engine would accept
+            continue
+        seen.add(desc)
+        c.add_problem_solution(p)
+    if not seen:
+        return
+    c.write()
+    back = qa.Cache(path)
+    back.load()
+    assert [p.to_yaml() for p in back.problems] == [p.to_yaml() for p in c.problems]
