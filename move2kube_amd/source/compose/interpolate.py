@@ -70,20 +70,45 @@ def os_env_mapping(env=None):
     return env.get
 
 
+class EnvFileError(ValueError):
+    """A line docker/cli's ``opts.ParseEnvFile`` refuses."""
+
+
 def parse_env_file(path):
-    """Parse a docker env file (``KEY=VAL`` lines, ``#`` comments, bare ``KEY``
-    inherits from the OS environment)."""
+    """docker/cli ``opts.ParseEnvFile`` (``parseKeyValueFile``): lines as
+    ``bufio.Scanner`` splits them, a UTF-8 BOM dropped from the first,
+    leading white space trimmed, ``#`` comments; ``KEY=VAL`` keeps the value
+    as written (trailing blanks too), a bare ``KEY`` takes the OS
+    environment's value when there is one.  A key with blanks, an empty key,
+    bytes that are not UTF-8 or a 64 KiB line raise :class:`EnvFileError`
+    with docker/cli's text; an unreadable file raises OSError."""
+    from ...utils import common
+    data = common.read_bytes(path)
+    lines, too_long = common.go_scan_lines(data)
     out = {}
-    with open(path, encoding="utf-8", errors="replace") as f:
-        for raw in f:
-            line = raw.strip()
-            if not line or line.startswith("#"):
-                continue
-            if "=" in line:
-                k, v = line.split("=", 1)
-                out[k.strip()] = v
-            else:
-                v = os.environ.get(line)
-                if v is not None:
-                    out[line] = v
+    for n, raw in enumerate(lines):
+        try:
+            text = raw.decode("utf-8")
+        except UnicodeDecodeError:
+            raise EnvFileError("env file %s contains invalid utf8 bytes at line %d: [%s]"
+                               % (path, n + 1, " ".join(str(b) for b in raw))) from None
+        if n == 0 and text.startswith("\ufeff"):
+            text = text[1:]
+        line = text.lstrip(common._GO_SPACE)
+        if not line or line.startswith("#"):
+            continue
+        key, eq, value = line.partition("=")
+        variable = key.lstrip(" \t")
+        if " " in variable or "\t" in variable:
+            raise EnvFileError("poorly formatted environment: variable '%s' contains whitespaces" % variable)
+        if not variable:
+            raise EnvFileError("poorly formatted environment: no variable name on line '%s'" % line)
+        if eq:
+            out[variable] = value
+        else:
+            v = os.environ.get(line)
+            if v is not None:
+                out[common.go_trim_space(line)] = v
+    if too_long:
+        raise EnvFileError("bufio.Scanner: token too long")
     return out

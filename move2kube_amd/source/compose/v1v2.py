@@ -20,7 +20,7 @@ from ...utils import common, log, yamlio
 from ...utils.constants import VOLUME_PREFIX, settings
 from . import schema as cschema
 from . import utils as cu
-from .interpolate import InterpolationError, interpolate, parse_env_file
+from .interpolate import EnvFileError, InterpolationError, interpolate, parse_env_file
 from .v3 import ComposeError, _as_list_of_str, _labels, _scalar_str
 
 V1_SERVICE_KEYS = {
@@ -86,7 +86,7 @@ def _env_lookup():
     if os.path.isfile(env_path):
         try:
             dotenv = parse_env_file(env_path)
-        except OSError:
+        except (OSError, EnvFileError):   # libcompose EnvfileLookup: an unparsable .env is empty
             dotenv = {}
 
     def lookup(k):

@@ -17,7 +17,7 @@ from ...utils import common, log, yamlio
 from ...utils.constants import VOLUME_PREFIX
 from . import schema as cschema
 from . import utils as cu
-from .interpolate import InterpolationError, interpolate, parse_env_file
+from .interpolate import EnvFileError, InterpolationError, interpolate, parse_env_file
 
 SUPPORTED_V3 = {"3", "3.0", "3.1", "3.2", "3.3", "3.4", "3.5", "3.6", "3.7", "3.8", "3.9"}
 
@@ -287,6 +287,8 @@ def _load_service(name, d, wd, env):
                 environment[k] = v
         except OSError:
             pass
+        except EnvFileError as e:   # resolveEnvironment returns it: the file does not load
+            raise ComposeError(str(e)) from None
     for k, v in _mapping_with_equals(d.get("environment")).items():
         environment[k] = v
     for k, v in list(environment.items()):

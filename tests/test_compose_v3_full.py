@@ -156,3 +156,25 @@ def test_deploy_cpus_parse_like_cast_to_float64(tmp_path, monkeypatch, capsys, c
                                 'to float64', "warning")
     if warning:
         assert logparse.logged(err, warning, "warning")
+
+
+@pytest.mark.parametrize("content,want", [
+    # docker/cli opts.ParseEnvFile: values kept as written, keys trimmed on the left only
+    (b"A=1  \n  B=two words \n#C=3\n\xef\xbb\xbfD=4\n", None),
+    (b"\xef\xbb\xbfA=1\nB=\n", {"A": "1", "B": ""}),
+    (b"A =1\n", "poorly formatted environment: variable 'A ' contains whitespaces"),
+    (b"=1\n", "poorly formatted environment: no variable name on line '=1'"),
+    (b"A=\xff\n", "contains invalid utf8 bytes at line 1: [65 61 255]"),
+])
+def test_env_file_lines_parse_like_docker_cli(tmp_path, content, want):
+    from move2kube_amd.source.compose.interpolate import EnvFileError, parse_env_file
+    p = tmp_path / "app.env"
+    p.write_bytes(content)
+    if want is None:
+        assert parse_env_file(str(p)) == {"A": "1  ", "B": "two words ", "\ufeffD": "4"}
+    elif isinstance(want, dict):
+        assert parse_env_file(str(p)) == want
+    else:
+        with pytest.raises(EnvFileError) as ei:
+            parse_env_file(str(p))
+        assert want in str(ei.value)
