@@ -233,6 +233,8 @@ def parse_v3(path):
     for sname in services:
         try:
             cfg["services"].append(_load_service(sname, services[sname] or {}, wd, env))
+        except EnvFileError as e:   # resolveEnvironment's error comes back as it is
+            raise ComposeError(str(e)) from None
         except (ValueError, TypeError) as e:  # bad port spec, duration, size, ...
             raise ComposeError("Failed to load service %s in %s: %s" % (sname, path, e))
     cfg["services"].sort(key=lambda s: s["name"])
@@ -287,8 +289,6 @@ def _load_service(name, d, wd, env):
                 environment[k] = v
         except OSError:
             pass
-        except EnvFileError as e:   # resolveEnvironment returns it: the file does not load
-            raise ComposeError(str(e)) from None
     for k, v in _mapping_with_equals(d.get("environment")).items():
         environment[k] = v
     for k, v in list(environment.items()):
