@@ -13,7 +13,7 @@ ARG ROCM_IMAGE=rocm/dev-ubuntu-22.04:7.2
 ARG RUNTIME_IMAGE=python:3.10-slim-bookworm
 
 FROM ${ROCM_IMAGE} AS builder
-RUN apt-get update && apt-get install -y --no-install-recommends python3 python3-pip g++ make git curl ca-certificates \
+RUN apt-get update && apt-get install -y --no-install-recommends python3 python3-pip g++ make git curl ca-certificates libssl-dev \
  && python3 -m pip install --no-cache-dir pybind11 pyyaml numpy pytest hypothesis \
  && rm -rf /var/lib/apt/lists/*
 WORKDIR /src

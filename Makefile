@@ -1,6 +1,8 @@
 # move2kube_amd developer entry points.
 #   make build      native host extension + gfx950 HIP library (in-tree)
 #   make test       CPU test suite (what CI runs)
+#   make stress     race/stress harness (scripts/stress.py, 20 seeds)
+#   make coverage   line coverage of the CPU suite (scripts/coverage.py)
 #   make test-gpu   GPU tests (needs an MI355X)
 #   make bench      headline benchmark (translate throughput on samples/)
 #   make dist       sdist/wheel-style tarballs + sha256 sums under dist/
@@ -32,13 +34,24 @@ generate: ## Regenerate embedded asset modules
 test: build ## Run the CPU test suite
 	$(PYTHON) -m pytest tests -q -m "not gpu"
 
+.PHONY: stress
+stress: build ## Race/stress harness: 20 seeded CLI runs per configuration under a 1 us switch interval
+	$(PYTHON) scripts/stress.py --seeds 20
+
+.PHONY: test-twins
+test-twins: build ## Golden trees through every implementation twin (M2K_DISABLE_NATIVE=1 etc.)
+	$(PYTHON) -m pytest tests/test_twin_matrix.py -q
+
 .PHONY: test-gpu
 test-gpu: build ## Run the GPU tests (MI355X)
 	$(PYTHON) -m pytest tests -q -m gpu
 
 .PHONY: test-coverage
-test-coverage: build ## CPU tests with coverage (needs pytest-cov)
-	$(PYTHON) -m pytest tests -q -m "not gpu" --cov=move2kube_amd --cov-report=xml
+test-coverage: build ## CPU tests with line coverage, checked against scripts/coverage_floor.json
+	$(PYTHON) scripts/coverage.py run --floor scripts/coverage_floor.json
+
+.PHONY: coverage
+coverage: test-coverage
 
 .PHONY: test-style
 test-style: ## Syntax/byte-compile check and license-free header check

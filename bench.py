@@ -26,13 +26,23 @@ available (``--workdir``, reported as ``workdir_fs``): every step rewrites the
 output tree, and on the hosts' discard-mounted scratch disks that churn slows
 every later run (see README "Why tmpfs").
 
+Host accounting (``host``): CPU ms per step over all ranks, context switches,
+and ``per_rank`` user / sys CPU, step p50 / p90 and context switches per step,
+so that a CPU-share limit on a shared node can be told from a code change.
+``--pin-cores`` (rehearsal only) pins each rank to its own physical cores and
+``M2K_HOST_THREADS=1`` sizes every host pool to one thread
+(``scripts/scale_rehearsal.sh`` runs the three variants).
+
 Correctness (untimed, rank 0): ``manifest_diff_vs_ref`` is the number of
 files that differ from the reference-derived expected trees
 (``tests/golden/reference/<config>``) over all five configurations, and
 ``per_config`` gives each configuration's diff plus its warm in-process and
-cold CLI-process p50.  The reference's execution model
-is only emulated in Python (``benchmarks/baseline_configs.py``), so nothing
-here is a measured comparison with the Go tool and ``vs_baseline`` is null.
+cold CLI-process p50 and interquartile range over ``--check-runs`` (default 9)
+runs; ``per_config_vs_prev`` divides them by the
+previous round's driver line (``benchmarks/prev_round_bench.json``).  The
+reference's execution model is only emulated in Python
+(``benchmarks/baseline_configs.py``), so nothing here is a measured
+comparison with the Go tool and ``vs_baseline`` is null.
 """
 
 import argparse
@@ -63,16 +73,47 @@ def tree_files(root):
 
 def per_config_checks(runs):
     """Untimed: every configuration's diff vs the reference-derived tree and its
-    warm / cold p50 (``benchmarks/baseline_configs.py``)."""
+    warm / cold p50 and interquartile range (``benchmarks/baseline_configs.py``)."""
     import baseline_configs
     out = {}
     for name in refconfigs.CONFIGS:
         r = baseline_configs.warm_runs(name, runs)
         cold, cold_diff = baseline_configs.cold_runs(name, runs)
-        out[name] = {"manifest_diff_vs_ref": r["manifest_diff_vs_ref"] + cold_diff,
-                     "warm_p50_ms": r["warm_p50_ms"], "cold_p50_ms": cold["cold_p50_ms"],
+        out[name] = {"manifest_diff_vs_ref": r["manifest_diff_vs_ref"] + cold_diff, "runs": runs,
+                     "warm_p50_ms": r["warm_p50_ms"], "warm_iqr_ms": r["warm_iqr_ms"],
+                     "cold_p50_ms": cold["cold_p50_ms"], "cold_iqr_ms": cold["cold_iqr_ms"],
                      "cold_over_floor_p50_ms": cold["cold_over_floor_p50_ms"],
+                     "cold_over_floor_iqr_ms": cold["cold_over_floor_iqr_ms"],
                      "cold_launcher_p50_ms": cold["cold_launcher_p50_ms"]}
+    return out
+
+
+# the previous round's driver line (BENCH_r05.json, stdout verbatim; kept out
+# of profiles/, which does not travel to the GPU box)
+PREV_BENCH = os.path.join(HERE, "benchmarks", "prev_round_bench.json")
+
+
+def per_config_vs_prev(per_config, prev_path):
+    """Ratio now / previous round for each configuration's warm p50 and cold
+    p50 over the interpreter floor (> 1 = slower), next to the previous
+    values, so that a shifted median shows in the bench line itself; compare
+    a ratio with ``*_iqr_ms`` / p50 before calling it a regression."""
+    try:
+        with open(prev_path) as f:
+            prev = json.load(f)
+    except (OSError, ValueError):
+        return None
+    out = {"prev": os.path.relpath(prev_path, HERE), "prev_ms_per_step": prev.get("ms_per_step")}
+    for name, now in (per_config or {}).items():
+        was = (prev.get("per_config") or {}).get(name)
+        if not was or "warm_p50_ms" not in now:
+            continue
+        row = {}
+        for k in ("warm", "cold_over_floor"):
+            if was.get(k + "_p50_ms") and now.get(k + "_p50_ms") is not None:
+                row[k + "_ratio"] = round(now[k + "_p50_ms"] / was[k + "_p50_ms"], 3)
+                row[k + "_prev_p50_ms"] = was[k + "_p50_ms"]
+        out[name] = row
     return out
 
 
@@ -110,10 +151,42 @@ def step_spread(step_s):
 
 def _cpu_s():
     """(user, system) CPU seconds of this process and its reaped children
-    (the operator-sdk stand-in, detector scripts)."""
+    (the operator-sdk stand-in, detector scripts), and their (voluntary,
+    involuntary) context switches."""
     import resource
     a, b = resource.getrusage(resource.RUSAGE_SELF), resource.getrusage(resource.RUSAGE_CHILDREN)
-    return a.ru_utime + b.ru_utime, a.ru_stime + b.ru_stime
+    return (a.ru_utime + b.ru_utime, a.ru_stime + b.ru_stime,
+            a.ru_nvcsw + b.ru_nvcsw, a.ru_nivcsw + b.ru_nivcsw)
+
+
+def pin_to_cores(local_rank, local_world):
+    """Weak-scaling rehearsal knob (``--pin-cores``): restrict this rank to its
+    own physical cores - the CPUs of this job's affinity mask grouped by
+    (package, core id) from sysfs, cores dealt round-robin to the local ranks,
+    every SMT sibling of a dealt core kept.  Runs before anything touches the
+    GPU.  Returns the CPU list, or None where the topology cannot be read."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+    cores = {}
+    for c in allowed:
+        base = "/sys/devices/system/cpu/cpu%d/topology/" % c
+        try:
+            with open(base + "physical_package_id") as f:
+                pkg = f.read().strip()
+            with open(base + "core_id") as f:
+                core = f.read().strip()
+        except OSError:
+            return None
+        cores.setdefault((pkg, core), []).append(c)
+    keys = sorted(cores, key=lambda k: min(cores[k]))
+    mine = [c for i, k in enumerate(keys) if i % max(1, local_world) == local_rank % max(1, local_world)
+            for c in cores[k]]
+    if not mine:   # more ranks than cores: share by rank modulo core count
+        mine = cores[keys[local_rank % len(keys)]]
+    os.sched_setaffinity(0, mine)
+    return mine
 
 
 def _cgroup_throttled_us():
@@ -131,8 +204,13 @@ def _cgroup_throttled_us():
 
 def _host_cpus():
     """CPUs this job may use: the affinity mask within the cgroup quota."""
-    from move2kube_amd.utils.constants import host_threads
-    return host_threads(1 << 20, local=1)
+    from move2kube_amd.utils.constants import _cgroup_cpu_limit
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    limit = _cgroup_cpu_limit()
+    return n if limit is None else min(n, limit)
 
 
 def main():
@@ -142,8 +220,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=refconfigs.HEADLINE,
                     choices=sorted(refconfigs.CONFIGS) + sorted(refconfigs.EXTRA_CONFIGS))
-    ap.add_argument("--check-runs", type=int, default=3,
+    ap.add_argument("--check-runs", type=int, default=9,
                     help="warm/cold runs per configuration in the untimed per-config check (0 = skip)")
+    ap.add_argument("--prev", default=PREV_BENCH,
+                    help="previous round's bench line (JSON) for per_config_vs_prev; empty = skip")
+    ap.add_argument("--pin-cores", action="store_true",
+                    help="rehearsal knob: pin each rank to its own physical cores (LOCAL_RANK) before any GPU call")
     ap.add_argument("--large-tree", default="100,1000,5000",
                     help="untimed: translate synthetic trees of these app counts and report ms per service "
                          "(benchmarks/translate_large_tree.py); empty = skip")
@@ -153,6 +235,9 @@ def main():
     args = ap.parse_args()
 
     world, rank, local_rank = _dist_env()
+    pinned = None
+    if args.pin_cores:
+        pinned = pin_to_cores(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world) or world))
     import torch
     dist = None
     have_cuda = torch.cuda.is_available()
@@ -203,7 +288,7 @@ def main():
             barrier()
             elapsed = time.perf_counter() - t0
             cpu1, thr1 = _cpu_s(), _cgroup_throttled_us()
-            cpu_s = (cpu1[0] - cpu0[0], cpu1[1] - cpu0[1])
+            cpu_s = tuple(b - a for a, b in zip(cpu0, cpu1))
             if rank == 0:
                 # untimed: one traced step for the per-phase breakdown (utils/trace.py)
                 from move2kube_amd.utils import trace
@@ -227,6 +312,12 @@ def main():
 
     spread = step_spread(step_s)
     slowest_p50 = spread["p50"] if spread else 0.0
+    k = max(1, args.steps)
+    # this rank's accounting per timed step: user / sys CPU ms, step p50 / p90,
+    # voluntary / involuntary context switches, CPUs it may run on
+    mine = [cpu_s[0] * 1e3 / k, cpu_s[1] * 1e3 / k, slowest_p50, spread["p90"] if spread else 0.0,
+            cpu_s[2] / k, cpu_s[3] / k, float(_host_cpus() if pinned is None else len(pinned))]
+    per_rank = [mine]
     if dist is not None:
         dev = torch.device("cuda", torch.cuda.current_device()) if have_cuda else torch.device("cpu")
         t = torch.tensor([elapsed, slowest_p50], dtype=torch.float64, device=dev)
@@ -234,7 +325,10 @@ def main():
         elapsed, slowest_p50 = float(t[0].item()), float(t[1].item())
         c = torch.tensor(list(cpu_s), dtype=torch.float64, device=dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        cpu_s = (float(c[0].item()), float(c[1].item()))
+        cpu_s = tuple(float(x) for x in c.tolist())
+        rows = [torch.zeros(len(mine), dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(rows, torch.tensor(mine, dtype=torch.float64, device=dev))
+        per_rank = [r.tolist() for r in rows]
     ms = elapsed * 1000.0 / max(1, args.steps)
     value = world * n_services * args.steps / elapsed if elapsed > 0 else 0.0
     if rank == 0:
@@ -258,7 +352,12 @@ def main():
                      "cpu_ms_per_step_all_ranks": round(sum(cpu_s) * 1000.0 / max(1, args.steps), 3),
                      "cpu_sys_ms_per_step_all_ranks": round(cpu_s[1] * 1000.0 / max(1, args.steps), 3),
                      "slowest_rank_step_p50_ms": round(slowest_p50, 3),
-                     "cgroup_throttled_ms": None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1000.0, 3)},
+                     "cgroup_throttled_ms": None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1000.0, 3),
+                     "ctx_switches_per_step_all_ranks": {"voluntary": round(cpu_s[2] / k, 2),
+                                                         "involuntary": round(cpu_s[3] / k, 2)},
+                     "pinned": pinned is not None,
+                     "per_rank": [dict(zip(("user_ms", "sys_ms", "step_p50_ms", "step_p90_ms", "nvcsw", "nivcsw",
+                                            "cpus"), (round(x, 3) for x in r))) for r in per_rank]},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -270,6 +369,7 @@ def main():
             "manifest_diff_vs_ref": total_diff,
             "manifest_diff_vs_ref_headline": diff_headline,
             "per_config": per_config,
+            "per_config_vs_prev": per_config_vs_prev(per_config, args.prev) if per_config and args.prev else None,
             "phase_ms_one_step": phase_ms,
             "config": {"model": BASELINE_CONFIG, "command": "move2kube translate -s samples --qaskip -q "
                        "helm-openshift-qacache.yaml" if args.config == refconfigs.HEADLINE else args.config,

@@ -8,13 +8,15 @@ CNB disabled (the java-cnb and cf configurations probe CNB through a
 ``podman`` stand-in instead of a container engine).  For every configuration
 this reports:
 
-* ``warm_p50_ms``  - p50 of ``--runs`` in-process runs of the configuration's
-  commands (assets unpacked once; nothing else reused between runs: fresh file
-  index, detectors, QA engines, output directory);
+* ``warm_p50_ms`` / ``warm_iqr_ms`` - p50 and interquartile range of
+  ``--runs`` in-process runs of the configuration's commands (assets
+  unpacked once; nothing else reused between runs: fresh file index,
+  detectors, QA engines, output directory);
 * ``cold_p50_ms``  - p50 of ``--runs`` sets of complete CLI processes
   (``python -m move2kube_amd collect|translate ...``: interpreter start,
   imports, asset unpack, the command, cleanup) - what a user of the Go binary
-  compares against; byte-compiled modules cached as in an installed package;
+  compares against; byte-compiled modules cached as in an installed package
+  (``cold_iqr_ms`` / ``cold_over_floor_iqr_ms``: the interquartile ranges);
   ``cold_cpu_p50_ms`` is their CPU time and ``cold_over_floor_p50_ms`` the
   time above a bare ``python -c pass`` per process, paired run by run;
 * ``cold_launcher_p50_ms`` / ``cold_launcher_over_floor_p50_ms`` - the same
@@ -62,6 +64,14 @@ def _p50(xs):
     return round(statistics.median(xs), 3)
 
 
+def _iqr(xs):
+    """Interquartile range (q75 - q25, linear interpolation); 0 for one run."""
+    if len(xs) < 2:
+        return 0.0
+    q = statistics.quantiles(xs, n=4, method="inclusive")
+    return round(q[2] - q[0], 3)
+
+
 def warm_runs(name, runs, emulation_runs=0):
     """In-process timings of one configuration; returns a result dict."""
     from move2kube_amd.utils import log
@@ -81,6 +91,7 @@ def warm_runs(name, runs, emulation_runs=0):
                 run.step(s)
                 times.append((time.perf_counter() - t0) * 1e3)
             res["warm_p50_ms"] = _p50(times)
+            res["warm_iqr_ms"] = _iqr(times)
             res["warm_min_ms"] = round(min(times), 3)
             if emulation_runs > 0:
                 saved = (os.environ.get("M2K_NATIVE_DETECT"), settings.workers)
@@ -154,7 +165,8 @@ def cold_stats(name, runs):
                 lwalls.append(wall)
                 lover.append(wall - floor * ncmd)
             diff += refconfigs.manifest_diff_vs_ref(name, out) or 0
-        return {"cold_p50_ms": _p50(walls), "cold_cpu_p50_ms": _p50(cpus), "cold_over_floor_p50_ms": _p50(over),
+        return {"cold_p50_ms": _p50(walls), "cold_iqr_ms": _iqr(walls), "cold_cpu_p50_ms": _p50(cpus),
+                "cold_over_floor_p50_ms": _p50(over), "cold_over_floor_iqr_ms": _iqr(over),
                 "cold_launcher_p50_ms": _p50(lwalls), "cold_launcher_over_floor_p50_ms": _p50(lover),
                 "manifest_diff_vs_ref": diff}
     finally:

@@ -114,6 +114,9 @@ def curate_plan(p):
                         except ValueError as e:
                             log.error("Failed to make the option path %r relative to the root directory. Error: %r",
                                       o, str(e))
+                if not opts:   # options[0] panics in the reference (planner.go:169): keep the options
+                    services[sn] = [so]
+                    break
                 mode = _ask(qa.new_select_problem("Select containerization technique's mode for service " + sn + ":",
                                                   ["Choose the containerization technique mode of interest."], opts[0],
                                                   opts)).get_string_answer()
@@ -268,10 +271,10 @@ def _emit(p, ir, outpath, qadisablecli):
 
 def _emit_artifacts(p, ir, outpath, qadisablecli, join_remover=None):
     # For a Helm chart the main transformer starts operator-sdk once the chart
-    # is written and waits for it at the end; the compose file, the CI/CD
-    # objects (built and written) and the QA cache do not feed the chart, so
-    # they are done in that wait (same bytes, same files, same questions in
-    # the same order: the Kubernetes transform asks none).
+    # is written and waits for it at the end; the writes of the compose file,
+    # the CI/CD objects and the QA cache do not feed the chart, so they are
+    # done in that wait (same bytes, same files; every question is still asked
+    # in the reference's order, before the chart is written).
     overlap = [] if p.kubernetes.artifact_type == plantypes.HELM else None
 
     def later(fn):
@@ -306,28 +309,28 @@ def _emit_artifacts(p, ir, outpath, qadisablecli, join_remover=None):
             ir = parameterizer.parameterize(ir)
 
         if any(c.new for c in ir.containers):
+            # translator.go:92-102: the CI/CD transform (the git secrets ask
+            # for known hosts and SSH keys) runs before the main transformer,
+            # so its questions, and a fatal error among them, come before
+            # anything of the chart is written; only the write of the Tekton
+            # objects, which the chart does not read, waits for operator-sdk
             cicd = transformer.CICDTransformer()
-
-            def transform_and_write_cicd():
-                try:
-                    with trace.span("CICDTransformer", "transform"):
-                        cicd.transform(ir)
-                except Exception as e:  # noqa: BLE001
-                    if isinstance(e, log.FatalError):
-                        raise
-                    log.error("Error while genrationg CI/CD resource fomr the IR. Error: %r", str(e))  # sic
-                    return
-                try:
-                    cicd.write_objects(outpath)
-                except Exception as e:  # noqa: BLE001
-                    if isinstance(e, log.FatalError):
-                        raise
-                    log.error("Unable to write the CI/CD artifacts to files. Error: %r", str(e))
-            # the Tekton objects read the final IR but feed nothing the
-            # Kubernetes transform or the chart reads, and the Kubernetes
-            # transform asks no question: for a Helm chart they are built
-            # while operator-sdk runs, with their questions in the same order
-            later(transform_and_write_cicd)
+            try:
+                with trace.span("CICDTransformer", "transform"):
+                    cicd.transform(ir)
+            except Exception as e:  # noqa: BLE001
+                if isinstance(e, log.FatalError):
+                    raise
+                log.error("Error while genrationg CI/CD resource fomr the IR. Error: %r", str(e))  # sic
+            else:
+                def write_cicd():
+                    try:
+                        cicd.write_objects(outpath)
+                    except Exception as e:  # noqa: BLE001
+                        if isinstance(e, log.FatalError):
+                            raise
+                        log.error("Unable to write the CI/CD artifacts to files. Error: %r", str(e))
+                later(write_cicd)
 
         ir.add_copy_sources_warning = qadisablecli
         t = transformer.get_transformer(ir)

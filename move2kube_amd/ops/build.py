@@ -143,9 +143,25 @@ def build_startcache(force=False):
     return startcache_build.write()
 
 
+def have_openssl_headers():
+    """Whether ``<openssl/evp.h>`` is on the compiler's include path (the
+    ``libssl-dev`` package): ``_m2k_sshkey`` needs it to build."""
+    cxx = os.environ.get("CXX", "g++")
+    try:
+        p = subprocess.run([cxx, "-E", "-x", "c++", "-"], input=b"#include <openssl/evp.h>\n",
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    except OSError:
+        return False
+    return p.returncode == 0
+
+
 def build_all(force=False):
     outs = [build_native(force)]
-    outs.append(build_sshkey(force))
+    if have_openssl_headers():
+        outs.append(build_sshkey(force))
+    else:   # utils/sshkeys.py then parses keys through ssh-keygen
+        sys.stderr.write("warning: OpenSSL headers not found (install libssl-dev); _m2k_sshkey not built, "
+                         "encrypted SSH keys go through ssh-keygen\n")
     outs.append(build_hip(force))
     outs.append(build_bytecode(force))
     outs.append(build_startcache(force))
@@ -166,6 +182,9 @@ def build_report(force=True):
                               os.path.join(os.path.dirname(HERE), "_bytecode.bin")),
                              ("_startcache.bin (parsed templates, compiled regexes)", build_startcache,
                               os.path.join(os.path.dirname(HERE), "_startcache.bin"))):
+        if fn is build_sshkey and not have_openssl_headers():
+            report.append({"target": name, "skipped": "OpenSSL headers not found (libssl-dev)"})
+            continue
         before = os.path.getmtime(target) if os.path.exists(target) else None
         t0 = time.perf_counter()
         out = fn(force)

@@ -46,14 +46,27 @@ def _load():
 
 
 def _load_locked():
-    global _lib, _state
+    """Load the library (under ``_lock``).  ``_lib`` is set before ``_state``
+    and ``_state`` only when the outcome is known, so the lock-free check in
+    :func:`_load` never hands a thread a provisional None while another
+    thread is still loading (the round-4 race of ``ops/native.py``)."""
+    global _state
     if _state is not None:
         return _lib
-    _state = False
+    ok = False
+    try:
+        ok = _open_library()
+    finally:
+        _state = ok
+    return _lib
+
+
+def _open_library():
+    global _lib
     if not os.path.exists(LIB_PATH):
         if gpu_host():
             raise GpuUnavailable("HIP library %s not built (run __graft_entry__.build())" % LIB_PATH)
-        return None
+        return False
     lib = ctypes.CDLL(LIB_PATH)
     i64p = ctypes.POINTER(ctypes.c_int64)
     i32p = ctypes.POINTER(ctypes.c_int32)
@@ -67,8 +80,7 @@ def _load_locked():
     lib.m2k_gpu_device_count.restype = ctypes.c_int
     lib.m2k_gpu_arch.restype = ctypes.c_char_p
     _lib = lib
-    _state = True
-    return _lib
+    return True
 
 
 def available():

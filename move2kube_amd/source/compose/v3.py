@@ -54,6 +54,21 @@ def _version(d):
     return v
 
 
+def _env_file_missing(p):
+    """``os.IsNotExist(err) || finfo.IsDir()`` of ``removeNonExistentEnvFilesV3``
+    (v3.go:61-65): only a path that does not exist, or a directory, is dropped.
+    Any other stat error (permission denied on a parent, ENOTDIR, a loop)
+    panics there on the nil FileInfo; here the file is kept, and reading it
+    fails the load (:func:`_read_env_file`)."""
+    import stat
+    try:
+        return stat.S_ISDIR(os.stat(p).st_mode)
+    except FileNotFoundError:
+        return True
+    except OSError:
+        return False
+
+
 def remove_non_existent_env_files(path, parsed):
     base = os.path.dirname(path)
     services = parsed.get("services") if isinstance(parsed, dict) else None
@@ -65,7 +80,7 @@ def remove_non_existent_env_files(path, parsed):
         ef = vals[cu.ENV_FILE]
         if isinstance(ef, str):
             p = ef if os.path.isabs(ef) else os.path.join(base, ef)
-            if not os.path.isfile(p):
+            if _env_file_missing(p):
                 log.warning("Unable to find env config file %s referred in service %s in file %s. Ignoring it.", p, sname, path)
                 del vals[cu.ENV_FILE]
         elif isinstance(ef, list):
@@ -73,12 +88,26 @@ def remove_non_existent_env_files(path, parsed):
             for e in ef:
                 if isinstance(e, str):
                     p = e if os.path.isabs(e) else os.path.join(base, e)
-                    if not os.path.isfile(p):
+                    if _env_file_missing(p):
                         log.warning("Unable to find env config file %s referred in service %s in file %s. Ignoring it.", p, sname, path)
                         continue
                     kept.append(e)
             vals[cu.ENV_FILE] = kept
     return parsed
+
+
+def _read_env_file(p):
+    """docker/cli ``opts.ParseEnvFile`` on an env file the removal kept: an
+    error opening or reading it is the load's error as it is
+    (``open <path>: permission denied``).  A FIFO, socket or device is an
+    error too, where ``os.Open`` in the reference would block on it forever."""
+    try:
+        return parse_env_file(p)
+    except FileNotFoundError:   # removed between the removal pass and here
+        return {}
+    except OSError as e:
+        from ...utils import common
+        raise EnvFileError(common.go_path_error(e, getattr(e, "go_op", "open"))) from None
 
 
 def _as_list_of_str(v):
@@ -284,11 +313,8 @@ def _load_service(name, d, wd, env):
     environment = {}
     for ef in _as_list_of_str(d.get(cu.ENV_FILE)):
         p = ef if os.path.isabs(ef) else os.path.join(wd, ef)
-        try:
-            for k, v in parse_env_file(p).items():
-                environment[k] = v
-        except OSError:
-            pass
+        for k, v in _read_env_file(p).items():
+            environment[k] = v
     for k, v in _mapping_with_equals(d.get("environment")).items():
         environment[k] = v
     for k, v in list(environment.items()):

@@ -77,6 +77,9 @@ def host_threads(cap, local=None):
             local = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
         except ValueError:
             local = 1
+    forced = os.environ.get("M2K_HOST_THREADS", "")
+    if forced.isdigit() and int(forced) > 0:   # scaling-rehearsal knob: every pool this size
+        return min(cap, int(forced))
     return max(1, min(cap, n // max(1, local)))
 
 

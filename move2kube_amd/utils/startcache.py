@@ -70,21 +70,32 @@ def _load():
 
 
 def _read():
+    """Read the file (under ``_lock``).  ``_state`` is assigned once, when the
+    outcome is known: the lock-free readers in :func:`template` and
+    :func:`regex` must never see a provisional value (a thread that saw
+    ``False`` while another was still reading would parse from source)."""
     global _state
-    _state = False
+    st = False
+    try:
+        st = _read_file()
+    finally:
+        _state = st
+    return _state
+
+
+def _read_file():
     if os.environ.get("M2K_STARTCACHE", "1") == "0":
-        return _state
+        return False
     try:
         with open(PATH, "rb") as f:
             tag, stamp, templates, regexes = marshal.loads(f.read())
     except (OSError, ValueError, EOFError, TypeError):
-        return _state
+        return False
     if tag != interpreter_tag():
-        return _state
+        return False
     if not _same_parser(stamp):
         templates = {}
-    _state = (templates, regexes)
-    return _state
+    return (templates, regexes)
 
 
 def _same_parser(stamp):

@@ -17,6 +17,10 @@ except ImportError:
     _HAVE_TORCH = False
 needs_torch = pytest.mark.skipif(not _HAVE_TORCH, reason="bench.py needs torch")
 
+def refconfigs_names():
+    return ["cf", "docker-compose", "golang", "helm-openshift", "java-cnb"]
+
+
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
 
@@ -52,6 +56,16 @@ def test_single_rank():
     lt = d["per_config"]["large-tree"]
     assert sorted(lt["large_tree_translate_ms_per_service"]) == ["20", "60"] and lt["ratio_largest_vs_smallest"] > 0
     assert all(v["manifest_diff_vs_ref"] == 0 for k, v in d["per_config"].items() if k != "large-tree")
+    # p50 and interquartile range per configuration, and the ratio to the
+    # previous round's driver line (benchmarks/prev_round_bench.json)
+    for name in refconfigs_names():
+        row = d["per_config"][name]
+        assert row["runs"] == 1 and row["warm_iqr_ms"] == 0 and row["cold_iqr_ms"] == 0
+        assert row["cold_over_floor_iqr_ms"] == 0
+        vs = d["per_config_vs_prev"][name]
+        assert vs["warm_ratio"] > 0 and vs["warm_prev_p50_ms"] > 0 and vs["cold_over_floor_prev_p50_ms"] > 0
+    assert d["per_config_vs_prev"]["prev"] == os.path.join("benchmarks", "prev_round_bench.json")
+    assert len(d["host"]["per_rank"]) == 1 and d["host"]["pinned"] is False
     # the headline names BASELINE.json configuration 5 verbatim
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         assert d["config"]["model"] in json.load(f)["configs"]
@@ -75,6 +89,12 @@ def test_two_ranks_gloo():
     assert h["cpus"] >= 1 and h["cpu_ms_per_step_all_ranks"] > 0
     assert 0 <= h["cpu_sys_ms_per_step_all_ranks"] <= h["cpu_ms_per_step_all_ranks"]
     assert h["slowest_rank_step_p50_ms"] > 0
+    # each rank's own accounting: user / sys CPU, step p50 / p90, context switches
+    assert len(h["per_rank"]) == 2
+    for r in h["per_rank"]:
+        assert set(r) == {"user_ms", "sys_ms", "step_p50_ms", "step_p90_ms", "nvcsw", "nivcsw", "cpus"}
+        assert r["user_ms"] > 0 and r["step_p50_ms"] > 0 and r["cpus"] >= 1
+    assert set(h["ctx_switches_per_step_all_ranks"]) == {"voluntary", "involuntary"}
 
 
 @needs_torch
@@ -136,3 +156,57 @@ def test_cold_diagnostics_scripts_run():
     assert p.returncode == 0, p.stderr.decode()[-3000:]
     d = _last_json(p.stdout.decode())
     assert set(d["median_ms"]) == {"0", "1"}
+
+
+def test_default_check_runs_can_see_a_shift():
+    """The untimed per-configuration check takes 9 runs by default (3 could
+    not tell a 30 % regression from box noise)."""
+    import ast
+    with open(os.path.join(ROOT, "bench.py")) as f:
+        tree = ast.parse(f.read())
+    for node in ast.walk(tree):
+        if isinstance(node, ast.Call) and getattr(node.func, "attr", "") == "add_argument" and \
+                node.args and getattr(node.args[0], "value", None) == "--check-runs":
+            default = [k.value.value for k in node.keywords if k.arg == "default"][0]
+            assert default >= 9
+            return
+    raise AssertionError("--check-runs not found")
+
+
+def test_per_config_vs_prev_ratios(tmp_path):
+    sys.path.insert(0, ROOT)
+    import bench
+    prev = tmp_path / "prev.json"
+    prev.write_text(json.dumps({"ms_per_step": 7.0, "per_config": {
+        "golang": {"warm_p50_ms": 2.0, "cold_over_floor_p50_ms": 8.0}}}))
+    now = {"golang": {"warm_p50_ms": 3.0, "cold_over_floor_p50_ms": 6.0}, "cf": {"warm_p50_ms": 1.0},
+           "large-tree": {"ratio_largest_vs_smallest": 1.0}}
+    out = bench.per_config_vs_prev(now, str(prev))
+    assert out["golang"] == {"warm_ratio": 1.5, "warm_prev_p50_ms": 2.0, "cold_over_floor_ratio": 0.75,
+                             "cold_over_floor_prev_p50_ms": 8.0}
+    assert "cf" not in out and "large-tree" not in out and out["prev_ms_per_step"] == 7.0
+    assert bench.per_config_vs_prev(now, str(tmp_path / "missing.json")) is None
+
+
+def test_pin_to_cores_deals_physical_cores(monkeypatch):
+    """--pin-cores: the job's CPUs grouped by (package, core id), cores dealt
+    round-robin to the local ranks, SMT siblings kept together."""
+    sys.path.insert(0, ROOT)
+    import bench
+    topo = {0: ("0", "0"), 1: ("0", "1"), 2: ("0", "0"), 3: ("0", "1"), 4: ("0", "2"), 5: ("0", "2")}
+    set_to = []
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(topo))
+    monkeypatch.setattr(bench.os, "sched_setaffinity", lambda pid, cpus: set_to.append(sorted(cpus)))
+    real_open = open
+
+    def fake_open(path, *a, **k):
+        if path.startswith("/sys/devices/system/cpu/cpu"):
+            import io
+            cpu = int(path.split("/cpu/cpu")[1].split("/")[0])
+            return io.StringIO(topo[cpu][0] if path.endswith("physical_package_id") else topo[cpu][1])
+        return real_open(path, *a, **k)
+    monkeypatch.setattr("builtins.open", fake_open)
+    assert bench.pin_to_cores(0, 2) == [0, 2, 4, 5]   # cores 0 and 2 with their siblings
+    assert bench.pin_to_cores(1, 2) == [1, 3]
+    assert bench.pin_to_cores(3, 8) == [0, 2]          # more ranks than cores: shared modulo
+    assert set_to == [[0, 2, 4, 5], [1, 3], [0, 2]]

@@ -178,3 +178,44 @@ def test_env_file_lines_parse_like_docker_cli(tmp_path, content, want):
         with pytest.raises(EnvFileError) as ei:
             parse_env_file(str(p))
         assert want in str(ei.value)
+
+
+def test_env_files_dropped_only_when_missing_or_a_directory(tmp_path, capsys):
+    """removeNonExistentEnvFilesV3 (v3.go:46-95): a missing env file or a
+    directory is dropped with a warning; every other entry reaches docker/cli's
+    opts.ParseEnvFile."""
+    from move2kube_amd.source.compose import v3
+    from move2kube_amd.utils import log
+    (tmp_path / "dir.env").mkdir()
+    (tmp_path / "ok.env").write_text("A=1\n")
+    p = tmp_path / "docker-compose.yaml"
+    p.write_text("version: '3'\nservices:\n  s:\n    image: busybox\n    env_file: [gone.env, dir.env, ok.env]\n")
+    log.set_verbose(False)
+    cfg = v3.parse_v3(str(p))
+    assert cfg["services"][0]["environment"] == {"A": "1"}
+    err = capsys.readouterr().err
+    for name in ("gone.env", "dir.env"):
+        assert logparse.logged(err, "Unable to find env config file %s referred in service s in file %s. Ignoring it."
+                               % (tmp_path / name, p), "warning")
+
+
+@pytest.mark.parametrize("kind", ["fifo", "enotdir"])
+def test_an_env_file_that_exists_but_cannot_be_read_fails_the_load(tmp_path, kind):
+    """An env file that stat finds but ParseEnvFile cannot read fails the whole
+    compose load with the open error, as docker/cli returns it (wrapped by
+    ParseV3, v3.go:112-118).  The reference
+    blocks forever opening a FIFO, and panics on the nil FileInfo of a stat
+    error other than ENOENT (v3.go:61): here both are that error."""
+    from move2kube_amd.source.compose import v3
+    if kind == "fifo":
+        target = tmp_path / "pipe.env"
+        os.mkfifo(str(target))
+        ref, want = "pipe.env", "open %s: invalid argument" % target
+    else:
+        (tmp_path / "plain").write_text("x")
+        ref, want = "plain/app.env", "open %s: not a directory" % (tmp_path / "plain" / "app.env")
+    p = tmp_path / "docker-compose.yaml"
+    p.write_text("version: '3'\nservices:\n  s:\n    image: busybox\n    env_file: %s\n" % ref)
+    with pytest.raises(v3.ComposeError) as ei:
+        v3.parse_v3(str(p))
+    assert str(ei.value) == 'Unable to load Compose file at path %s Error: "%s"' % (p, want)   # ParseV3's %q

@@ -117,7 +117,7 @@ def test_release_workflow_follows_the_reference():
     assert wf["on"] == {"push": {"tags": ["v*"]}}
     jobs = wf["jobs"]
     assert set(jobs) == {"build", "image-build", "create-release-draft", "upload-release-assets"}
-    assert "pytest tests" in _runs(jobs["build"])
+    assert "scripts/coverage.py run" in _runs(jobs["build"]) and "tests -q -m \"not gpu\"" in _runs(jobs["build"])
     img = jobs["image-build"]
     assert img["needs"] == ["build"]
     runs = _runs(img)
@@ -144,10 +144,47 @@ def test_release_workflow_follows_the_reference():
 def test_tag_and_ci_workflows():
     tag = _workflow("tag.yml")
     assert "workflow_dispatch" in tag["on"] and "git push origin" in _runs(tag["jobs"]["tag"])
+    # the dispatch input reaches the script through the environment, validated
+    step = [s for s in tag["jobs"]["tag"]["steps"] if "run" in s][0]
+    assert "${{" not in step["run"] and step["env"] == {"TAG": "${{ github.event.inputs.tag }}"}
+    assert "^v[0-9A-Za-z.+-]+$" in step["run"]
     ci = _workflow("ci.yml")
     assert ci["on"]["push"] == {"branches": ["main"]}          # tags: release.yml
     runs = _runs(ci["jobs"]["image"])
     assert "move2kube-amd:latest" in runs and "refs/heads/main" in str(ci["jobs"]["image"]["steps"])
+    # the race harness, the twin matrix and the coverage floor run on every push
+    assert "scripts/stress.py" in _runs(ci["jobs"]["stress"])
+    assert "tests/test_twin_matrix.py" in _runs(ci["jobs"]["twins"])
+    cov = _runs(ci["jobs"]["coverage"])
+    assert "scripts/coverage.py run" in cov and "--floor scripts/coverage_floor.json" in cov
+    assert os.path.exists(os.path.join(ROOT, "scripts", "coverage_floor.json"))
+
+
+def test_every_sshkey_build_has_the_openssl_headers():
+    """``_m2k_sshkey`` includes <openssl/*.h>: every job and image stage that
+    builds it installs libssl-dev (or lets ``build_all`` skip it)."""
+    for name in ("ci.yml", "release.yml"):
+        for job_name, job in _workflow(name)["jobs"].items():
+            runs = _runs(job)
+            if "build_sshkey" in runs or "move2kube_amd.ops.build" in runs or "make cbuild" in runs:
+                assert "libssl-dev" in runs or "make cbuild" in runs, (name, job_name)
+    with open(os.path.join(ROOT, "Dockerfile")) as f:
+        builder = f.read().split("FROM ${RUNTIME_IMAGE}")[0]
+    assert "libssl-dev" in builder and "move2kube_amd.ops.build" in builder
+
+
+def test_build_all_skips_the_key_parser_without_openssl_headers(monkeypatch):
+    from move2kube_amd.ops import build
+    called = []
+    for fn in ("build_native", "build_sshkey", "build_hip", "build_bytecode", "build_startcache"):
+        monkeypatch.setattr(build, fn, lambda force=False, fn=fn: called.append(fn) or fn)
+    monkeypatch.setattr(build, "have_openssl_headers", lambda: False)
+    build.build_all()
+    assert "build_sshkey" not in called and "build_native" in called
+    monkeypatch.setattr(build, "have_openssl_headers", lambda: True)
+    called.clear()
+    build.build_all()
+    assert "build_sshkey" in called
 
 
 def test_image_build_installs_every_tool_it_copies():
