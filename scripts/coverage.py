@@ -14,7 +14,8 @@ How it measures:
   placed first on ``PYTHONPATH`` - pytest itself and the CLI processes the
   tests start (``python -m move2kube_amd``, the stress and twin scripts), in
   every thread (``threading.settrace``) - and each process writes its lines
-  at exit (the CLI's ``_cli_exit`` runs the ``atexit`` handlers too);
+  at exit (``atexit``, and ``os._exit``, which the CLI's fast exit and forked
+  test helpers use, is wrapped to write them first);
   processes started with ``-S``/``-I`` or a scrubbed environment are not
   counted;
 * the executable lines of a module are the line numbers its compiled code
@@ -23,7 +24,7 @@ How it measures:
 Usage::
 
     python scripts/coverage.py run [--out DIR] [-- PYTEST ARGS]   # default: tests -m "not gpu"
-    python scripts/coverage.py report --data DIR [--out DIR] [--floor scripts/coverage_floor.json]
+    python scripts/coverage.py report --data DIR [--data DIR2 ...] [--out DIR] [--floor scripts/coverage_floor.json]
 
 ``run`` also reports.  The report is ``coverage.txt`` (a per-module table,
 lowest first) and ``coverage.json`` (per-module statements, hits, percent and
@@ -101,6 +102,17 @@ if _d:
             _json.dump(_data(), f)
         _os.replace(path + ".tmp", path)
     _atexit.register(_dump)
+    # a forked child (the tests' unprivileged helpers) or the CLI's fast exit
+    # leaves through os._exit, which skips atexit: write the lines first
+    _real_exit = _os._exit
+
+    def _exit_after_dump(code, _real=_real_exit):
+        try:
+            _dump()
+        except Exception:  # noqa: BLE001
+            pass
+        _real(code)
+    _os._exit = _exit_after_dump
 '''
 
 
@@ -151,18 +163,34 @@ def product_modules():
     return out
 
 
-def merge(data_dir):
+def _data_files(data_dirs):
+    for d in [data_dirs] if isinstance(data_dirs, str) else data_dirs:
+        for fn in sorted(os.listdir(d)):
+            if fn.endswith(".json"):
+                yield os.path.join(d, fn)
+
+
+def _package_path(path):
+    """The file under this tree that ``path`` names: line files written on
+    another machine (the GPU box runs the snapshot at another root) are
+    matched by their path below the package directory."""
+    marker = os.sep + "move2kube_amd" + os.sep
+    i = path.rfind(marker)
+    return os.path.realpath(os.path.join(ROOT, path[i + 1:]) if i >= 0 else path)
+
+
+def merge(data_dirs):
+    """{file: lines that ran} over every process's line file in ``data_dirs``
+    (one directory or a list, e.g. the CPU suite's and the GPU tests')."""
     hits = {}
-    for fn in sorted(os.listdir(data_dir)):
-        if not fn.endswith(".json"):
-            continue
-        with open(os.path.join(data_dir, fn)) as f:
+    for fn in _data_files(data_dirs):
+        with open(fn) as f:
             try:
                 d = json.load(f)
             except ValueError:
                 continue
         for path, lines in d.items():
-            hits.setdefault(os.path.realpath(path), set()).update(lines)
+            hits.setdefault(_package_path(path), set()).update(lines)
     return hits
 
 
@@ -183,6 +211,7 @@ def _ranges(lines):
 
 def report(data_dir, out_dir):
     hits = merge(data_dir)
+    nproc = sum(1 for _ in _data_files(data_dir))
     rows = {}
     tot_s = tot_h = 0
     for rel, path in product_modules().items():
@@ -195,7 +224,7 @@ def report(data_dir, out_dir):
         rows[rel] = {"statements": len(ex), "hit": len(ran), "percent": round(100.0 * len(ran) / len(ex), 1),
                      "missed": _ranges(ex - ran)}
     res = {"total": {"statements": tot_s, "hit": tot_h, "percent": round(100.0 * tot_h / max(1, tot_s), 1)},
-           "processes": len([f for f in os.listdir(data_dir) if f.endswith(".json")]), "modules": rows}
+           "processes": nproc, "modules": rows}
     os.makedirs(out_dir, exist_ok=True)
     with open(os.path.join(out_dir, "coverage.json"), "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
@@ -264,7 +293,8 @@ def main(argv=None):
     r.add_argument("--write-floor", default=None)
     r.add_argument("pytest_args", nargs="*")
     p = sub.add_parser("report")
-    p.add_argument("--data", required=True)
+    p.add_argument("--data", required=True, action="append",
+                   help="a directory of per-process line files (repeat to merge, e.g. CPU and GPU runs)")
     p.add_argument("--out", default=DEFAULT_OUT)
     p.add_argument("--floor", default=None)
     p.add_argument("--write-floor", default=None)
