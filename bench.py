@@ -349,7 +349,7 @@ def main():
             # CPU ms per step summed over ranks (children included), the
             # slowest rank's median step, and the cgroup's quota throttling
             "host": {"cpus": _host_cpus(),
-                     "cpu_ms_per_step_all_ranks": round(sum(cpu_s) * 1000.0 / max(1, args.steps), 3),
+                     "cpu_ms_per_step_all_ranks": round((cpu_s[0] + cpu_s[1]) * 1000.0 / max(1, args.steps), 3),
                      "cpu_sys_ms_per_step_all_ranks": round(cpu_s[1] * 1000.0 / max(1, args.steps), 3),
                      "slowest_rank_step_p50_ms": round(slowest_p50, 3),
                      "cgroup_throttled_ms": None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1000.0, 3),

@@ -8,6 +8,8 @@
 #   PHASES=1 the per-configuration cold phase split (scripts/cold_phases.py),
 #   TRACE=1 the traced spans of cold CLI runs (benchmarks/cold_trace.py),
 #   BUDGET=1 the whole-process cold budget split (benchmarks/cold_budget.py),
+#   COV=1 the line coverage of `pytest -m gpu` (scripts/coverage.py; merge its
+#         cov_gpu_data/ with the CPU suite's: coverage.py report --data A --data B),
 #   SKIP_BENCH=1 leaves out the GPU tests, smoke, bench and rocprof steps.
 #   RUN=r04_x AB=r03 gpurun --timeout 1200 -- bash scripts/gpu_pass.sh
 set -eo pipefail
@@ -28,6 +30,12 @@ grep '^{' "$OUT/bench.log" > "$OUT/bench.json"
 python -c 'import json,sys; d=json.load(open(sys.argv[1])); print(d["ms_per_step"], d["step_ms"], d["manifest_diff_vs_ref"], d["per_config"]["large-tree"]["ratio_largest_vs_smallest"])' "$OUT/bench.json"
 echo "rocprof smoke"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof" -o smoke -- python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/rocprof_smoke.log" 2>&1
+fi
+if [ -n "$COV" ]; then
+  echo "gpu test coverage"
+  timeout -k 10 400 python -u scripts/coverage.py run --out "$OUT/cov_gpu" --data "$OUT/cov_gpu_data" \
+    -- tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > "$OUT/cov_gpu.log" 2>&1
+  tail -1 "$OUT/cov_gpu.log"
 fi
 if [ -n "$AB" ]; then
   echo "A/B vs $AB"

@@ -95,6 +95,9 @@ def test_two_ranks_gloo():
         assert set(r) == {"user_ms", "sys_ms", "step_p50_ms", "step_p90_ms", "nvcsw", "nivcsw", "cpus"}
         assert r["user_ms"] > 0 and r["step_p50_ms"] > 0 and r["cpus"] >= 1
     assert set(h["ctx_switches_per_step_all_ranks"]) == {"voluntary", "involuntary"}
+    # CPU over ranks is user + sys of every rank (not the switch counts)
+    total = sum(r["user_ms"] + r["sys_ms"] for r in h["per_rank"])
+    assert abs(h["cpu_ms_per_step_all_ranks"] - total) < 0.01 * max(1.0, total) + 0.01
 
 
 @needs_torch
