@@ -65,6 +65,14 @@ class Problem:
             self.id, self.desc, lst(self.context), self.type, lst(self.default), lst(self.options),
             lst(self.answer), "true" if self.resolved else "false")
 
+    def go_plus_v(self):
+        """fmt ``%+v`` of the Go struct: field names, nil slices as ``[]``."""
+        def lst(xs):
+            return "[" + " ".join(xs or ()) + "]"
+        return "{ID:%d Desc:%s Context:%s Solution:{Type:%s Default:%s Options:%s Answer:%s} Resolved:%s}" % (
+            self.id, self.desc, lst(self.context), self.type, lst(self.default), lst(self.options),
+            lst(self.answer), "true" if self.resolved else "false")
+
     def copy(self):
         return Problem(self.id, self.desc, list(self.context), self.type, list(self.default),
                        list(self.options), None if self.answer is None else list(self.answer), self.resolved)
@@ -634,7 +642,7 @@ class Cache:
         if i >= 0:
             p.set_answer(self.problems[i].answer)
             return p
-        raise ProblemError("The problem %r was not found in the cache" % (p.desc,))
+        raise ProblemError("The problem %s was not found in the cache" % p.go_plus_v())   # cache.go:125 (%+v)
 
     def _index(self):
         idx = self.__dict__.get("_desc_index")

@@ -43,35 +43,81 @@ def get_hash(data):
 # Go value parsers
 # ---------------------------------------------------------------------------
 
-_DUR_UNITS = {"ns": 1, "us": 1000, "µs": 1000, "μs": 1000, "ms": 10 ** 6, "s": 10 ** 9,
+_DUR_UNITS = {"ns": 1, "us": 1000, "\u00b5s": 1000, "\u03bcs": 1000, "ms": 10 ** 6, "s": 10 ** 9,
               "m": 60 * 10 ** 9, "h": 3600 * 10 ** 9}
-_DUR_RE = _lazy_re(r"(\d+\.?\d*|\.\d+)(ns|us|µs|μs|ms|s|m|h)")
+_INT64_MAX = (1 << 63) - 1
 
 
 def parse_duration(s):
-    """Go ``time.ParseDuration`` -> nanoseconds."""
+    """Go 1.15 ``time.ParseDuration`` -> nanoseconds: ``[-+]?([0-9]*(\\.[0-9]*)?[a-z]+)+``
+    with its integer arithmetic, overflow checks and error texts
+    (``time: invalid duration "x"``, ``time: missing unit in duration "1"``,
+    ``time: unknown unit "d" in duration "1d"``)."""
+    from ...utils.log import go_quote
     if s is None:
-        raise ValueError("time: invalid duration")
-    s = str(s)
-    orig = s
+        raise ValueError("time: invalid duration " + go_quote(""))
+    orig = s = str(s)
+
+    def invalid():
+        return ValueError("time: invalid duration " + go_quote(orig))
     neg = False
-    if s[:1] in "+-":
+    if s and s[0] in "+-":
         neg = s[0] == "-"
         s = s[1:]
     if s == "0":
         return 0
     if not s:
-        raise ValueError("time: invalid duration %r" % orig)
-    total = 0.0
-    pos = 0
-    while pos < len(s):
-        m = _DUR_RE.match(s, pos)
-        if not m:
-            raise ValueError("time: invalid duration %r" % orig)
-        total += float(m.group(1)) * _DUR_UNITS[m.group(2)]
-        pos = m.end()
-    v = int(total)
-    return -v if neg else v
+        raise invalid()
+    d = 0
+    while s:
+        if not (s[0] == "." or "0" <= s[0] <= "9"):
+            raise invalid()
+        i = 0
+        while i < len(s) and "0" <= s[i] <= "9":
+            i += 1
+        pre = i > 0
+        v = int(s[:i]) if pre else 0
+        if v > _INT64_MAX:                      # leadingInt overflow
+            raise invalid()
+        s = s[i:]
+        f, scale, post = 0, 1.0, False
+        if s and s[0] == ".":
+            s = s[1:]
+            i = 0
+            overflow = False
+            while i < len(s) and "0" <= s[i] <= "9":
+                if not overflow:
+                    y = f * 10 + int(s[i])
+                    if f > _INT64_MAX // 10 or y > _INT64_MAX:   # leadingFraction stops accumulating
+                        overflow = True
+                    else:
+                        f = y
+                        scale *= 10
+                i += 1
+            post = i > 0
+            s = s[i:]
+        if not pre and not post:
+            raise invalid()
+        i = 0
+        while i < len(s) and not (s[i] == "." or "0" <= s[i] <= "9"):
+            i += 1
+        if i == 0:
+            raise ValueError("time: missing unit in duration " + go_quote(orig))
+        u, s = s[:i], s[i:]
+        unit = _DUR_UNITS.get(u)
+        if unit is None:
+            raise ValueError("time: unknown unit " + go_quote(u) + " in duration " + go_quote(orig))
+        if v > _INT64_MAX // unit:
+            raise invalid()
+        v *= unit
+        if f > 0:
+            v += int(float(f) * (float(unit) / scale))
+            if v > _INT64_MAX:
+                raise invalid()
+        d += v
+        if d > _INT64_MAX:
+            raise invalid()
+    return -d if neg else d
 
 
 _BRACKETED_HOST_RE = _lazy_re(r"^\[([^\]]+)\]:(.*)$")

@@ -9,7 +9,10 @@ which instruments every goroutine: the CNB providers
 Each run is one configuration of ``benchmarks/refconfigs.py`` as the user's
 CLI commands (``collect`` then ``translate`` for cf; ``rest:<config>`` answers
 every question over the QA REST engine from one client while three others
-poll the current problem, instead of ``--qaskip``), each command a fresh
+poll the current problem, instead of ``--qaskip``; ``collect:k8s`` collects
+cluster metadata through the stand-in ``kubectl proxy`` and inspects 13
+images concurrently, and must reproduce a plain sequential run's tree), each
+command a fresh
 ``python scripts/m2k_switchy.py ...`` process whose thread switch interval is
 1 us, so every thread is preempted between almost every pair of bytecodes.
 Runs vary, by seed:
@@ -52,7 +55,7 @@ sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
 import refconfigs  # noqa: E402
 
 DEFAULT_CONFIGS = (sorted(refconfigs.CONFIGS) + ["coverage/git-repos", "coverage/carried-over/Openshift"]
-                   + ["rest:" + c for c in sorted(refconfigs.CONFIGS)])
+                   + ["rest:" + c for c in sorted(refconfigs.CONFIGS)] + ["collect:k8s"])
 WORKERS = ("1", "2", "16")
 CNB_PARALLEL = ("1", "4")
 NATIVE_DETECT = ("1", "0")
@@ -178,6 +181,82 @@ def _run_rest(run, env, seed):
     return run.out, stats
 
 
+STUBBIN = os.path.join(ROOT, "tests", "fixtures", "stubbin")
+_COLLECT_IMAGES = ["stress/app%d:1.%d" % (i, i) for i in range(12)] + ["redis:6"]
+_DOCKER_STUB = """#!/bin/sh
+# scripts/stress.py: docker for `collect -a k8s` (inspect of the compose images)
+if [ -n "$M2K_STUB_DELAY_SEED" ]; then
+  _d=$(printf '%s %s' "$M2K_STUB_DELAY_SEED" "$*" | cksum); _d=${_d%% *}
+  sleep "$(printf '0.%03d' $((_d % 25)))"
+fi
+case "$1 $2" in
+  "inspect stress/"*) printf '[{"RepoTags":["%s"],"ContainerConfig":{"ExposedPorts":{"80/tcp":{},"8443/tcp":{}},'\\
+'"User":"1001","WorkingDir":"/srv/%s"}}]' "$2" "$2" ;;
+  "inspect redis:6") echo "Error: No such object: redis:6"; exit 1 ;;
+  *) echo "unexpected: $*" >&2; exit 1 ;;
+esac
+"""
+
+
+def _collect_k8s(work, env, launcher):
+    """``collect -a k8s`` of a compose tree: cluster discovery through the
+    stand-in ``kubectl proxy`` (``tests/fixtures/fake_apiserver.py``) and the
+    concurrent ``docker inspect`` of 13 images (one missing).  Returns the
+    collect output directory."""
+    import subprocess
+    src = os.path.join(work, "src")
+    os.makedirs(src)
+    with open(os.path.join(src, "docker-compose.yaml"), "w") as f:
+        f.write("version: '3'\nservices:\n" + "".join("  s%d:\n    image: %s\n" % (i, img)
+                                                        for i, img in enumerate(_COLLECT_IMAGES)))
+    bindir = os.path.join(work, "bin")
+    os.makedirs(bindir)
+    with open(os.path.join(bindir, "docker"), "w") as f:
+        f.write(_DOCKER_STUB)
+    os.chmod(os.path.join(bindir, "docker"), 0o755)
+    full = dict(os.environ)
+    full.update(env)
+    full["PATH"] = os.pathsep.join([bindir, STUBBIN, "/usr/bin", "/bin"])
+    full["KUBECONFIG"] = os.path.join(work, "no-kubeconfig")
+    full["HOME"] = os.path.join(work, "home")
+    full["PYTHONPATH"] = ROOT + os.pathsep + full.get("PYTHONPATH", "")
+    out = os.path.join(work, "collect")
+    p = subprocess.run(launcher + ["collect", "-a", "k8s", "-s", src, "-o", out], env=full, cwd=work,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=300)
+    if p.returncode != 0:
+        raise RuntimeError("collect failed: %s" % p.stderr.decode(errors="replace")[-2000:])
+    return os.path.join(out, "m2k_collect")
+
+
+_COLLECT_EXPECTED = {}
+
+
+def _collect_expected():
+    """The tree of one plain, sequential ``collect -a k8s`` (no switch
+    interval, one worker): what every stressed run must reproduce."""
+    if "tree" not in _COLLECT_EXPECTED:
+        work = tempfile.mkdtemp(prefix="m2k-stress-ref-")
+        out = _collect_k8s(work, {"M2K_WORKERS": "1"}, [sys.executable, "-m", "move2kube_amd"])
+        tree = {}
+        for rel, path in refconfigs.tree_files(out).items():
+            with open(path, "rb") as f:
+                tree[rel] = f.read()
+        shutil.rmtree(work, ignore_errors=True)
+        _COLLECT_EXPECTED["tree"] = tree
+    return _COLLECT_EXPECTED["tree"]
+
+
+def _diff_collect(out):
+    want = _collect_expected()
+    have = refconfigs.tree_files(out)
+    bad = sorted(set(want) ^ set(have))
+    for rel in sorted(set(want) & set(have)):
+        with open(have[rel], "rb") as f:
+            if f.read() != want[rel]:
+                bad.append(rel)
+    return sorted(bad)
+
+
 UI_NOTE_HEAD = "\nIMPORTANT!!: If you used the UI for translation"
 UI_NOTE_TAIL = "in order to get it right.\n"
 
@@ -204,6 +283,18 @@ def run_one(config, seed, switch="1e-6", keep_on_failure=None):
     work = tempfile.mkdtemp(prefix="m2k-stress-")
     row = {"config": config, "seed": seed, "knobs": knobs(seed)}
     t0 = time.perf_counter()
+    if config == "collect:k8s":
+        try:
+            out = _collect_k8s(work, dict(row["knobs"], M2K_SWITCH_INTERVAL=switch), [sys.executable, ENTRY])
+            row["diff"] = _diff_collect(out)
+        except RuntimeError as e:
+            row["error"] = str(e)[-1500:]
+            row["diff"] = None
+        finally:
+            shutil.rmtree(work, ignore_errors=True)
+        row["wall_s"] = round(time.perf_counter() - t0, 3)
+        row["ok"] = not row.get("error") and row["diff"] == []
+        return row
     try:
         run = refconfigs.Run(name, work).prepare()
         env = dict(row["knobs"], M2K_SWITCH_INTERVAL=switch)
@@ -273,7 +364,8 @@ def main(argv=None):
     args = ap.parse_args(argv)
     configs = [c for c in args.configs.split(",") if c]
     for c in configs:
-        refconfigs._lookup(_name(c[len("rest:"):] if c.startswith("rest:") else c))   # unknown names fail here
+        if c != "collect:k8s":
+            refconfigs._lookup(_name(c[len("rest:"):] if c.startswith("rest:") else c))   # unknown names fail here
     sink_f = open(args.json, "a") if args.json else None
 
     def sink(r):

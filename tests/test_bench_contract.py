@@ -213,3 +213,18 @@ def test_pin_to_cores_deals_physical_cores(monkeypatch):
     assert bench.pin_to_cores(1, 2) == [1, 3]
     assert bench.pin_to_cores(3, 8) == [0, 2]          # more ranks than cores: shared modulo
     assert set_to == [[0, 2, 4, 5], [1, 3], [0, 2]]
+
+
+def test_host_contention_control_runs():
+    """benchmarks/host_contention.py (the control experiment for the scaling
+    rehearsal) reports per-process CPU of each phase and its ratio to N=1."""
+    p = subprocess.run([sys.executable, os.path.join("benchmarks", "host_contention.py"), "--ranks", "1,2",
+                        "--iters", "3"], cwd=ROOT, env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    rows = [json.loads(l) for l in p.stdout.decode().splitlines() if l.startswith("{")]
+    assert [r["n"] for r in rows] == [1, 2]
+    for r in rows:
+        assert set(r["per_process"]) == {"cpu", "fs", "spawn"}
+        assert r["per_process"]["cpu"]["user_ms"] > 0 and r["per_process"]["fs"]["wall_ms"] > 0
+    assert rows[0]["ratio_to_first"]["cpu"]["user_ms"] == 1.0

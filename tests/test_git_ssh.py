@@ -17,9 +17,11 @@ import subprocess
 
 import pytest
 
+import logparse
+
 from move2kube_amd import qaengine
 from move2kube_amd.qaengine.engine import Engine
-from move2kube_amd.utils import git, knownhosts, sshkeys
+from move2kube_amd.utils import git, knownhosts, log, sshkeys
 
 HAVE_KEYGEN = shutil.which("ssh-keygen") is not None
 
@@ -431,3 +433,66 @@ def test_no_keys_selected_when_declined(qa_home):
     qaengine.add_engine(eng)
     assert sshkeys.get_ssh_key("github.com") == ("", False)
     assert [t for t, _ in eng.asked] == ["Confirm"]
+
+
+def test_unreadable_known_hosts_is_a_warning(qa_home, capsys):
+    (qa_home / ".ssh" / "known_hosts").mkdir()            # a directory: the read fails
+    qaengine.add_engine(_Answers({"The CI/CD pipeline needs access": ["true"]}))
+    sshkeys.load_known_hosts_of_current_user()
+    assert logparse.logged_containing(capsys.readouterr().err, "Failed to get public keys from the known_hosts file "
+                                      "at path", "warning")
+
+
+@pytest.mark.parametrize("case", ["no-dir", "empty", "none-selected", "key-none"])
+def test_private_key_selection_edges(qa_home, capsys, case):
+    """sshkeys.go:105-160: no ~/.ssh (an error line), an empty one (a warning),
+    every key unselected (an info line), and NONE for the domain."""
+    import shutil as _sh
+    log.set_verbose(True)
+    answers = {"The CI/CD pipeline needs access": ["true"]}
+    if case == "no-dir":
+        _sh.rmtree(str(qa_home / ".ssh"))
+    elif case != "empty":
+        (qa_home / ".ssh" / "id_rsa").write_text("x")
+        answers["These are the files"] = [] if case == "none-selected" else ["id_rsa"]
+        answers["Select the key"] = ["NONE"]
+    qaengine.add_engine(_Answers(answers))
+    try:
+        assert sshkeys.get_ssh_key("git.corp.example") == ("", False)
+    finally:
+        log.set_verbose(False)
+    err = capsys.readouterr().err
+    want = {"no-dir": ("error", "Failed to read the ssh directory at path"),
+            "empty": ("warning", "No key files where found in"),
+            "none-selected": ("info", "All key files ignored."),
+            "key-none": ("debug", "No key selected for domain git.corp.example")}[case]
+    assert logparse.logged_containing(err, want[1], want[0])
+
+
+@pytest.mark.skipif(not HAVE_KEYGEN, reason="ssh-keygen not installed")
+def test_keygen_fallback_names_the_go_key_type(qa_home, capsys, keygen_fallback):
+    """Without the extension, an Ed25519 key fails as ``ParseRawPrivateKey``'s
+    type does in the reference's error text."""
+    _keygen(qa_home / ".ssh" / "id_ed25519", "ed25519")
+    qaengine.add_engine(_Answers({"The CI/CD pipeline needs access": ["true"], "These are the files": ["id_ed25519"],
+                                  "Select the key": ["id_ed25519"]}))
+    assert sshkeys.get_ssh_key("git.corp.example") == ("", False)
+    assert 'Unknown key type [*ed25519.PrivateKey]' in capsys.readouterr().err
+
+
+def test_native_converter_switches(monkeypatch):
+    monkeypatch.setenv("M2K_DISABLE_NATIVE", "1")
+    assert sshkeys._native() is None
+    monkeypatch.delenv("M2K_DISABLE_NATIVE")
+    import builtins
+    real = builtins.__import__
+
+    def no_ext(name, *a, **k):
+        if a and a[2] and "_m2k_sshkey" in a[2]:
+            raise ImportError("not built")
+        return real(name, *a, **k)
+    monkeypatch.setattr(builtins, "__import__", no_ext)
+    assert sshkeys._native() is None
+    monkeypatch.setenv("M2K_REQUIRE_NATIVE", "1")
+    with pytest.raises(ImportError):
+        sshkeys._native()

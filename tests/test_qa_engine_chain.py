@@ -151,3 +151,15 @@ def test_engine_base_prints_like_go():
     e.start_engine()
     with pytest.raises(NotImplementedError):
         e.fetch_answer(None)
+
+
+def test_cache_miss_error_prints_the_problem_like_go(tmp_path):
+    """``GetSolution`` (types/qaengine/cache.go:125) reports a miss with
+    ``%+v`` of the Problem struct: field names, nil slices as ``[]``."""
+    c = qa.Cache(str(tmp_path / "c.yaml"))
+    prob = qa.new_select_problem("Pick one:", ["ctx a", "ctx b"], "b", ["a", "b"])
+    with pytest.raises(qa.ProblemError) as ei:
+        c.get_solution(prob)
+    assert str(ei.value) == ("The problem {ID:%d Desc:Pick one: Context:[ctx a ctx b] Solution:{Type:Select "
+                             "Default:[b] Options:[a b] Answer:[]} Resolved:false} was not found in the cache"
+                             % prob.id)
