@@ -18,15 +18,56 @@ def _docker_config_dir():
     return os.environ.get("DOCKER_CONFIG") or os.path.join(os.path.expanduser("~"), ".docker")
 
 
+def _decode_auth(auth):
+    """docker/cli ``decodeAuth``: base64 of ``user:password``; ValueError when
+    it is not (the whole config file then fails to load)."""
+    import base64
+    import binascii
+    if not auth:
+        return
+    try:
+        decoded = base64.b64decode(auth.replace("\r", "").replace("\n", ""), validate=True)
+    except (binascii.Error, ValueError):
+        raise ValueError("illegal base64 data")
+    if b":" not in decoded:
+        raise ValueError("Invalid auth configuration file")
+
+
 def load_docker_auths():
-    """{registry: auth} from the docker CLI config (``config.json``)."""
+    """{registry: auth} as ``dockercliconfig.Load`` leaves the docker CLI
+    config (``config.json``; registrycustomizer.go:70-92).  Its
+    ``LoadFromReader`` decodes every ``auth`` into username and password and
+    then clears ``Auth``, so in the reference every value is empty: the
+    registries are listed, but no docker-config login is ever offered and the
+    default registry stays docker.io.  An auth that does not decode fails the
+    whole load (nothing listed).  ``M2K_COMPAT=fixed`` keeps the auths, so the
+    "Docker login from config" answer works."""
     path = os.path.join(_docker_config_dir(), "config.json")
     try:
         with open(path) as f:
             cfg = fastjson.load(f)
     except (OSError, ValueError):
         return {}
-    return {k: (v or {}).get("auth", "") for k, v in (cfg.get("auths") or {}).items()}
+    auths = {}
+    for k, v in ((cfg.get("auths") if isinstance(cfg, dict) else None) or {}).items():
+        auth = (v or {}).get("auth", "") if isinstance(v, dict) else ""
+        try:
+            _decode_auth(auth)
+        except ValueError:
+            return {}
+        auths[k] = auth if settings.fixed else ""
+    return auths
+
+
+def _url_host(regurl):
+    """``url.Parse(regurl).Host`` (userinfo dropped, port kept); None on a
+    parse error."""
+    import urllib.parse
+    try:
+        netloc = urllib.parse.urlparse(regurl).netloc
+    except ValueError:
+        return None
+    return netloc.rpartition("@")[2]
 
 
 class RegistryCustomizer:
@@ -48,15 +89,12 @@ class RegistryCustomizer:
         auths = {}
         defreg = ""
         if not settings.ignore_environment:
-            for regurl in sorted(load_docker_auths()):
-                auth = load_docker_auths()[regurl]
-                try:
-                    import urllib.parse
-                    u = urllib.parse.urlparse(regurl)
-                    if u.netloc:
-                        regurl = u.netloc
-                except ValueError:
-                    pass
+            config_auths = load_docker_auths()
+            for regurl in sorted(config_auths):   # a Go map: any order (DEVIATIONS 1)
+                auth = config_auths[regurl]
+                host = _url_host(regurl)
+                if host:
+                    regurl = host
                 if regurl == "":
                     continue
                 if not common.is_string_present(reg_list, regurl):

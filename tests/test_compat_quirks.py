@@ -326,3 +326,47 @@ def test_q2_write_containers_manual_image(tmp_path, mode, caplog):
     else:
         assert "legacy:latest" in open(readme).read()
         assert "legacy:latest" not in push
+
+
+def _registry_questions(tmp_path, monkeypatch, auths):
+    """The registry questions of a qaskip translate of a new nodejs image
+    with ``auths`` in the docker CLI config, as recorded in m2kqacache.yaml."""
+    import json
+    from move2kube_amd.utils import yamlio
+    cfg = tmp_path / "dockercfg"
+    cfg.mkdir()
+    (cfg / "config.json").write_text(json.dumps({"auths": auths}))
+    monkeypatch.setenv("DOCKER_CONFIG", str(cfg))
+    monkeypatch.setenv("HOME", str(tmp_path))
+    _translate(tmp_path, monkeypatch, {"nodejs": None}, ignore_env=False)
+    cache = yamlio.load(open(os.path.join(str(tmp_path / "out"), "q", "m2kqacache.yaml")).read())
+    return {s["description"]: s["solution"] for s in cache["spec"]["solutions"]}
+
+
+def test_docker_config_auths_are_cleared_by_the_loader(tmp_path, mode, monkeypatch):
+    """dockercliconfig.Load decodes each auth and clears it (LoadFromReader),
+    so the reference lists the config's registries but never offers the
+    docker-config login and keeps docker.io as the default registry; "fixed"
+    keeps the auth: the login is offered and its registry is the default."""
+    import base64
+    good = base64.b64encode(b"user:pw").decode()
+    qs = _registry_questions(tmp_path, monkeypatch, {"https://user@quay.io/v1/": {"auth": good},
+                                                     "registry.example.com": {}})
+    reg = qs["Select the registry where your images are hosted:"]
+    assert reg["options"] == ["Other", "quay.io", "registry.example.com", "docker.io"]
+    if mode == "reference":
+        assert reg["default"] == ["docker.io"] and reg["answer"] == ["docker.io"]
+        login = qs["[docker.io] What type of container registry login do you want to use?"]
+        assert "Docker login from config" not in login["options"]
+    else:
+        assert reg["default"] == ["quay.io"] and reg["answer"] == ["quay.io"]
+        login = qs["[quay.io] What type of container registry login do you want to use?"]
+        assert login["options"][-1] == "Docker login from config"
+
+
+def test_an_undecodable_docker_config_auth_drops_the_whole_config(tmp_path, monkeypatch):
+    """decodeAuth fails (not base64, or no ':'): Load returns the error and the
+    reference uses nothing of the file."""
+    qs = _registry_questions(tmp_path, monkeypatch, {"quay.io": {"auth": "bm9jb2xvbg=="},   # "nocolon"
+                                                     "other.io": {}})
+    assert qs["Select the registry where your images are hosted:"]["options"] == ["Other", "docker.io"]

@@ -8,7 +8,7 @@ import shutil
 from move2kube_amd import api
 from move2kube_amd.utils import fsindex
 
-from conftest import ref_path
+SAMPLES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "samples")  # the reference's corpus, byte for byte
 
 
 def test_handoff_allowed():
@@ -56,7 +56,7 @@ def _walks(monkeypatch):
 
 def test_same_output_with_and_without_handoff(tmp_path, monkeypatch):
     src = tmp_path / "samples"
-    shutil.copytree(ref_path("samples"), str(src), symlinks=True)
+    shutil.copytree(SAMPLES, str(src), symlinks=True)
     walks = _walks(monkeypatch)
     with api.Session(qaskip=True) as s:
         a = s.translate(str(src), str(tmp_path / "o1"))
@@ -72,7 +72,7 @@ def test_same_output_with_and_without_handoff(tmp_path, monkeypatch):
 
 def test_output_inside_source_walks_again(tmp_path, monkeypatch):
     src = tmp_path / "app"
-    shutil.copytree(ref_path("samples", "nodejs"), str(src))
+    shutil.copytree(os.path.join(SAMPLES, "nodejs"), str(src))
     walks = _walks(monkeypatch)
     with api.Session(qaskip=True) as s:
         s.translate(str(src), str(src))
@@ -84,7 +84,7 @@ def test_compose_files_parsed_once_per_command(tmp_path, monkeypatch):
     file's parse (``source/compose/utils.py:command_memo``)."""
     from move2kube_amd.source.compose import v3
     src = tmp_path / "dc"
-    shutil.copytree(ref_path("samples", "docker-compose"), str(src))
+    shutil.copytree(os.path.join(SAMPLES, "docker-compose"), str(src))
     calls = []
     real = v3.parse_v3.__wrapped__
 

@@ -11,7 +11,7 @@ import pytest
 from move2kube_amd import api
 from move2kube_amd.utils import common
 
-from conftest import ref_path
+SAMPLES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "samples")  # the reference's corpus, byte for byte
 
 
 def _bounded(fn, seconds=20):
@@ -42,8 +42,8 @@ def test_read_bytes_rejects_a_fifo_without_blocking(tmp_path):
 
 def _tree(tmp_path, name):
     src = tmp_path / name
-    shutil.copytree(ref_path("samples", "nodejs"), str(src / "app"))
-    shutil.copytree(ref_path("samples", "docker-compose"), str(src / "dc"))
+    shutil.copytree(os.path.join(SAMPLES, "nodejs"), str(src / "app"))
+    shutil.copytree(os.path.join(SAMPLES, "docker-compose"), str(src / "dc"))
     (src / "app" / "requirements.txt").write_text("flask\n")  # the python detectors then read *.py files
     return src
 

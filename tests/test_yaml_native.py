@@ -19,7 +19,7 @@ from move2kube_amd.ops import native
 from move2kube_amd.utils import yamlio
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-REFERENCE = "/root/reference"
+from conftest import REFERENCE  # noqa: E402
 SENTINEL = object()
 MODES = (yamlio._TYPED, yamlio._V2, yamlio._RAW)
 
