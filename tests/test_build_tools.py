@@ -121,3 +121,18 @@ def test_build_report(fake_toolchain, tmp_path, monkeypatch):
 def test_openssl_probe_without_a_compiler(monkeypatch):
     monkeypatch.setenv("CXX", "/nonexistent/c++")
     assert build.have_openssl_headers() is False
+
+
+def test_graft_build_report_tolerates_a_skipped_target(monkeypatch, capsys):
+    """``__graft_entry__.build()`` (the driver's build check) prints its JSON
+    report when ``_m2k_sshkey`` was skipped for missing OpenSSL headers."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as g
+    monkeypatch.setattr(build, "build_report", lambda force=True: [
+        {"target": "_m2k_native", "compiled": True},
+        {"target": "_m2k_sshkey", "skipped": "OpenSSL headers not found (libssl-dev)"}])
+    g.build()
+    d = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert d["build_mode"] == "full" and d["build_exercised"] == ["_m2k_native"]
