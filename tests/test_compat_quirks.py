@@ -10,6 +10,8 @@ import os
 
 import pytest
 
+import logparse
+
 from move2kube_amd.apiresourceset import KnativeAPIResourceSet
 from move2kube_amd.collector import images
 from move2kube_amd.containerizer.base import ContainerizerError, Containerizers
@@ -370,3 +372,48 @@ def test_an_undecodable_docker_config_auth_drops_the_whole_config(tmp_path, monk
     qs = _registry_questions(tmp_path, monkeypatch, {"quay.io": {"auth": "bm9jb2xvbg=="},   # "nocolon"
                                                      "other.io": {}})
     assert qs["Select the registry where your images are hosted:"]["options"] == ["Other", "docker.io"]
+
+
+def test_q1_fixed_mode_translates_a_knative_service(tmp_path, monkeypatch):
+    """With the type check fixed, a Knative service goes through
+    ``KnativeAPIResourceSet.Translate``: its revision template's pod spec
+    (container concurrency and timeout dropped) becomes the service's."""
+    monkeypatch.setattr(settings, "compat", "fixed")
+    ksvc = KSVC.replace("    spec:\n", "    spec:\n      containerConcurrency: 4\n      timeoutSeconds: 30\n")
+    objs = _translate(tmp_path, monkeypatch, {"ksvc.yaml": ksvc}, name="k")
+    dep = objs["hello-deployment.yaml"]
+    spec = dep["spec"]["template"]["spec"]
+    assert spec["containers"][0]["image"] == "gcr.io/knative-samples/helloworld-go"
+    assert "containerConcurrency" not in spec and "timeoutSeconds" not in spec
+
+
+def test_q1_knative_translate_skips_what_it_cannot_use(tmp_path, capsys):
+    """KnativeAPIResourceSet.Translate: a service without a file, an
+    unreadable file, one that no longer decodes, and another kind, each with
+    the reference's log line; the rest are translated."""
+    from move2kube_amd.utils import log
+    log.set_verbose(False)
+    good = tmp_path / "good.yaml"
+    good.write_text(KSVC)
+    bad = tmp_path / "bad.yaml"
+    bad.write_text("kind: [\n")
+    cfg = tmp_path / "cfg.yaml"
+    cfg.write_text("apiVersion: serving.knative.dev/v1\nkind: Configuration\nmetadata:\n  name: c\n")
+    p = plantypes.new_plan()
+    p.root_dir = str(tmp_path)
+    svcs = []
+    for name, path in (("nofile", None), ("gone", tmp_path / "gone.yaml"), ("bad", bad), ("cfg", cfg),
+                       ("hello", good)):
+        s = plantypes.Service(name)
+        if path is not None:
+            s.source_artifacts[plantypes.KNATIVE_FILE_ARTIFACT] = [str(path)]
+        svcs.append(s)
+    ir = KnativeAPIResourceSet().translate(svcs, p)
+    assert list(ir.services) == ["hello"]
+    err = capsys.readouterr().err
+    assert logparse.logged(err, "No knative artifacts found in service nofile", "warning")
+    assert logparse.logged_containing(err, 'Unable to read the knative file at path "%s"' % (tmp_path / "gone.yaml"),
+                                      "error")
+    assert logparse.logged_containing(err, 'Failed to decode the knative file at path "%s"' % bad, "error")
+    assert logparse.logged(err, 'The knative file at path "%s" does not contain the required type. Expected: '
+                                '*v1.Service Actual: *v1.Configuration' % cfg, "error")
