@@ -179,6 +179,21 @@ def get_transformer(ir):
     return K8sTransformer()
 
 
+def _parse_group_version(gv):
+    """``schema.ParseGroupVersion(gv).String()``: "" and "/" are the empty
+    version, no slash is a core version, one slash splits group and version;
+    more is an error (None)."""
+    if gv in ("", "/"):
+        return ""
+    n = gv.count("/")
+    if n == 0:
+        return gv
+    if n == 1:
+        group, ver = gv.split("/")
+        return group + "/" + ver if group else ver
+    return None
+
+
 class K8sTransformer(Transformer):
     def __init__(self):
         self.root_dir = ""
@@ -213,6 +228,14 @@ class K8sTransformer(Transformer):
         log.debug("Total transformed objects : %d", len(self.transformed_objects))
 
     def convert_objects(self):
+        """``convertToClusterSupportedKinds`` (k8stransformer.go:106-143): each
+        object to the first version the cluster lists for its kind.  For a
+        kind the cluster does not list, the reference keeps
+        ``GroupVersionKind().String()`` (``apps/v1, Kind=Deployment``) as
+        the version; ``ParseGroupVersion`` reads ``v1, Kind=Deployment`` as
+        the version, so the conversion fails with "no kind ... is registered"
+        and the object is written as it was.  A version with two slashes
+        (malformed cluster metadata) drops the object."""
         objs = []
         for obj in self.transformed_objects:
             kind = obj.get("kind", "")
@@ -220,14 +243,23 @@ class K8sTransformer(Transformer):
             version = obj.get("apiVersion", "")
             if versions is None:
                 if self.ignore_unsupported_kinds:
-                    log.error("Kind %s unsupported in target cluster. Will ignore object.", kind)
+                    log.error("Kind %s unsupported in target cluster. Will ignore object. %s", kind,
+                              "&TypeMeta{Kind:%s,APIVersion:%s,}" % (kind, version))   # %+v: TypeMeta's String()
                     continue
+                if not settings.fixed:
+                    group, _, ver = version.rpartition("/")
+                    version = "%s/%s, Kind=%s" % (group, ver, kind)
             elif kind == "Service":
                 for v in versions:
                     if not v.startswith(KNATIVE_GROUP):
                         version = v
             else:
                 version = versions[0]
+            gv = _parse_group_version(version)
+            if gv is None:
+                log.error("Unable to parse group version %s : unexpected GroupVersion string: %s", version, version)
+                continue
+            version = gv
             try:
                 obj = (convert.convert_fixed if settings.fixed else convert.convert_to_version)(obj, version)
             except convert.ConversionError as e:
