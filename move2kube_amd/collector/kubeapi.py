@@ -236,7 +236,9 @@ class KubeconfigClient(_HTTPClient):
 
     @staticmethod
     def _ssl_context(cluster, user):
-        ctx = ssl.create_default_context()
+        # client-go trusts only the cluster CA when one is given (tls.Config
+        # RootCAs), the system roots otherwise
+        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_CLIENT)
         if cluster.get("insecure-skip-tls-verify"):
             ctx.check_hostname = False
             ctx.verify_mode = ssl.CERT_NONE
@@ -244,6 +246,8 @@ class KubeconfigClient(_HTTPClient):
             ctx.load_verify_locations(cadata=base64.b64decode(cluster["certificate-authority-data"]).decode("utf-8", "replace"))
         elif cluster.get("certificate-authority"):
             ctx.load_verify_locations(cafile=cluster["certificate-authority"])
+        else:
+            ctx.load_default_certs()
         cert, key = user.get("client-certificate-data"), user.get("client-key-data")
         if cert and key:
             with tempfile.TemporaryDirectory(prefix="m2k-kc-") as d:
@@ -288,7 +292,8 @@ class ProxyClient(_HTTPClient):
         super().__init__("http", "127.0.0.1", port)
 
     def close(self):
-        super().close()
+        if hasattr(self, "_lock"):      # not yet set when the proxy failed to start
+            super().close()
         p = getattr(self, "proc", None)
         if p is not None and p.poll() is None:
             p.terminate()
