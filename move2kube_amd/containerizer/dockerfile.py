@@ -22,9 +22,20 @@ from .base import CONTAINERIZER_JSON_PORT, Containerizer, ContainerizerError
 DOCKERFILE_DETECT_SCRIPT = "m2kdfdetect.sh"
 
 
+_GO_JSON_KIND = {list: "array", str: "string", float: "number", bool: "bool"}
+
+
 def parse_detect_output(output):
-    """JSON object from a detect script; numbers decode as float64 like Go's encoding/json."""
-    return fastjson.loads(output, parse_int=float)
+    """The detect script's JSON as ``json.Unmarshal`` into a
+    ``map[string]interface{}`` leaves it: numbers are float64, ``null`` is the
+    nil (empty) map, any other non-object is Go's UnmarshalTypeError."""
+    v = fastjson.loads(output, parse_int=float)
+    if v is None:
+        return {}
+    if not isinstance(v, dict):
+        raise ValueError("json: cannot unmarshal %s into Go value of type map[string]interface {}"
+                         % _GO_JSON_KIND[type(v)])
+    return v
 
 
 def _port_from(m):
@@ -110,8 +121,10 @@ class DockerfileContainerizer(Containerizer):
         src_dir = srcs[0]
         r = run_detect(cdir, self.script, src_dir)
         if not r.ok:
-            log.error("Detect using Dockerfile containerizer at path %r on the source code at path %r failed.", cdir, src_dir)
-            raise ContainerizerError("detect failed with exit status %d" % r.code)
+            err = common.go_exit_status(r.code)
+            log.error("Detect using Dockerfile containerizer at path %r on the source code at path %r failed. "
+                      "Error: %r", cdir, src_dir, err)
+            raise ContainerizerError(err)
         contents = template
         if r.stdout != "":
             try:

@@ -19,9 +19,13 @@ class ReuseDockerfileContainerizer(Containerizer):
             raise ContainerizerError("Failed to reuse the Dockerfile. The service %s doesn't have any containerization "
                                      "target options" % service.service_name)
         df_path = service.target_options[0]
-        if not os.path.exists(df_path):
-            log.error("Unable to find the Dockerfile at path %r", df_path)
+        try:
+            os.stat(df_path)
+        except FileNotFoundError as e:      # os.IsNotExist: other stat errors pass silently
+            log.error("Unable to find the Dockerfile at path %r Error: %r", df_path, common.go_path_error(e, "stat"))
             log.error("Will assume the dockerfile will be copied and will proceed.")
+        except (OSError, ValueError):
+            pass
         df_dir = common.go_dir(df_path)
         script_path = common.go_join(df_dir, service.service_name + "-docker-build.sh")
         rel_ctx = "."

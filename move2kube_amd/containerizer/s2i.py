@@ -44,12 +44,13 @@ class S2IContainerizer(DockerfileContainerizer):
         if not r.ok:
             log.error("Detect using S2I containerizer at path %r on the source code at path %r failed. Error: %r",
                       cdir, src_dir, r.stdout)
-            raise ContainerizerError("detect failed with exit status %d" % r.code)
+            raise ContainerizerError(common.go_exit_status(r.code))
+        output = r.stdout.strip()
         try:
-            m = parse_detect_output(r.stdout.strip())
+            m = parse_detect_output(output)
         except ValueError as e:
             log.error("Unable to unmarshal the output of the detect script at path %r Output: %r Error: %r",
-                      cdir, r.stdout, str(e))
+                      cdir, output, str(e))
             raise ContainerizerError(str(e)) from e
         port = _port_from(m)
         if port is not None:

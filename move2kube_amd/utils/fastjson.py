@@ -67,7 +67,11 @@ def loads(s, parse_int=int):
             end += 1
         if end != n:
             raise ValueError("extra data")
-    except (StopIteration, ValueError, _GoRejects, RecursionError):
+    except (StopIteration, ValueError, _GoRejects, RecursionError, SystemError):
+        # SystemError: CPython 3.10's scanner reports an error inside an object
+        # or array through json.decoder.JSONDecodeError, looked up in
+        # sys.modules only; in a process that never imported json (a cold
+        # command) it returns NULL with no exception set
         raw = s if isinstance(s, (bytes, bytearray)) else s.encode("utf-8", "surrogatepass")
         raise ValueError(go_syntax_error(bytes(raw)) or "invalid JSON") from None
     if "\\u" in text or (text is s and not _valid_utf8(text)):

@@ -73,3 +73,28 @@ def test_loads_errors_are_go_texts(text, err):
 ])
 def test_lone_surrogates_decode_to_the_replacement_character(text, want):
     assert fastjson.loads(text) == want
+
+
+def test_errors_inside_containers_without_the_json_package():
+    """A cold command never imports ``json``; the C scanner's errors inside an
+    object or array then surface as SystemError and must still become Go's
+    text (truncated detector output, a half-written docker config)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    texts = ['{"port": 80', "[1 2]", '{"a": [1,]}', '{"a" 1}']
+    code = "\n".join([
+        "import sys",
+        "sys.path.insert(0, %r)" % root,
+        "from move2kube_amd.utils import fastjson",
+        "assert 'json.decoder' not in sys.modules",
+        "for t in %r:" % texts,
+        "    try:",
+        "        fastjson.loads(t, parse_int=float)",
+        "    except ValueError as e:",
+        "        print(e)"])
+    out = subprocess.run([sys.executable, "-S", "-c", code], capture_output=True, text=True, check=True).stdout
+    assert out.splitlines() == ["unexpected end of JSON input", "invalid character '2' after array element",
+                                "invalid character ']' looking for beginning of value",
+                                "invalid character '1' after object key"]

@@ -91,7 +91,7 @@ def test_s2i_renders_every_detector_file(s2i_case, capsys):
 
 
 @pytest.mark.parametrize("body,msg", [
-    ("exit 3\n", "detect failed with exit status 3"),
+    ("exit 3\n", "exit status 3"),
     ("echo 'not json'\n", None),
     ("echo '{\"port\": 80}'\n", "has no builder"),
 ])
