@@ -18,18 +18,117 @@ from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
 from . import Collector, concurrently, run
 
 
-def _cf_apps():
-    out = run(["cf", "curl", "/v2/apps"])
+class _Number(str):
+    """A JSON number kept as its literal text (Go reports ``number 1.5``)."""
+
+
+# sourcetypes.CfInstanceApps and the types under it (internal/collector/sourcetypes)
+_CF_TYPES = {
+    "CfInstanceApps": (("resources", "[]sourcetypes.CfResource"),),
+    "CfResource": (("entity", "sourcetypes.CfSourceApplication"),),
+    "CfSourceApplication": (("name", "string"), ("buildpack", "string"), ("detected_buildpack", "string"),
+                            ("memory", "int64"), ("instances", "int"), ("dockerimage", "string"),
+                            ("ports", "[]int32"), ("environment_json", "map[string]string")),
+}
+_INT_BITS = {"int": 64, "int64": 64, "int32": 32}
+
+
+def _json_kind(v):
+    if isinstance(v, _Number):
+        return "number"
+    if isinstance(v, bool):
+        return "bool"
+    return {str: "string", list: "array", dict: "object"}[type(v)]
+
+
+class _Unmarshal:
+    """``json.Unmarshal(output, &sourcetypes.CfInstanceApps{})`` (Go 1.15
+    encoding/json): keys match the field names exactly or case-insensitively,
+    unknown keys are ignored, ``null`` leaves a value as it is, and a type
+    mismatch is an ``UnmarshalTypeError`` naming the innermost struct and the
+    field path; the first one is returned once the whole document has been
+    decoded.  The decoded value is plain dicts/lists/str/int."""
+
+    def __init__(self):
+        self.err = None
+
+    def mismatch(self, value, typ, ctx):
+        if self.err is None:
+            if ctx[0]:
+                self.err = "json: cannot unmarshal %s into Go struct field %s.%s of type %s" % (
+                    value, ctx[0], ".".join(ctx[1]), typ)
+            else:
+                self.err = "json: cannot unmarshal %s into Go value of type %s" % (value, typ)
+
+    def value(self, v, typ, ctx):
+        if v is None:
+            return None
+        if typ.startswith("[]"):
+            if not isinstance(v, list):
+                return self.mismatch(_json_kind(v), typ, ctx)
+            return [self.value(x, typ[2:], ctx) for x in v]
+        if typ == "map[string]string":
+            if not isinstance(v, dict):
+                return self.mismatch(_json_kind(v), typ, ctx)
+            return {k: "" if x is None else self.value(x, "string", ctx) for k, x in v.items()}
+        if typ.startswith("sourcetypes."):
+            return self.struct(v, typ, ctx)
+        if typ == "string":
+            if isinstance(v, str) and not isinstance(v, _Number):
+                return v
+            return self.mismatch(_json_kind(v), typ, ctx)
+        bits = _INT_BITS[typ]
+        if isinstance(v, _Number):
+            digits = v[1:] if v[:1] == "-" else v
+            if digits.isdigit() and digits.isascii() and -(1 << (bits - 1)) <= int(v) < (1 << (bits - 1)):
+                return int(v)
+            return self.mismatch("number " + v, typ, ctx)
+        return self.mismatch(_json_kind(v), typ, ctx)
+
+    def struct(self, v, typ, ctx):
+        if not isinstance(v, dict):
+            return self.mismatch(_json_kind(v), typ, ctx)
+        name = typ.split(".", 1)[1]
+        fields = _CF_TYPES[name]
+        out = {}
+        for key, x in v.items():
+            f = next((f for f in fields if f[0] == key), None) or \
+                next((f for f in fields if f[0] == key.casefold()), None)
+            if f is None:
+                continue
+            got = self.value(x, f[1], (name, ctx[1] + [f[0]]))
+            if x is not None:
+                out[f[0]] = got
+        return out
+
+
+def decode_cf_apps(output):
+    """The entity of every resource of ``cf curl /v2/apps`` output; ValueError
+    with encoding/json's text when Go would fail the Unmarshal."""
+    doc = fastjson.loads(output, parse_int=_Number, parse_float=_Number)
+    u = _Unmarshal()
+    res = u.value(doc, "sourcetypes.CfInstanceApps", ("", []))
+    if u.err is not None:
+        raise ValueError(u.err)
+    return [(r or {}).get("entity") or {} for r in (res or {}).get("resources") or []]
+
+
+def _cf_apps(skipping):
+    """``cf curl /v2/apps`` decoded; the command's and the decode's errors are
+    logged as the reference's two callers log them."""
+    try:
+        out = run(["cf", "curl", "/v2/apps"])
+    except Exception as e:  # noqa: BLE001
+        log.error("%s", e)
+        raise
     log.debug("Cf Curl output %s", out)
     try:
-        data = fastjson.loads(out)
+        apps = decode_cf_apps(out)
     except ValueError as e:
-        log.error("Error in unmarshalling yaml: %s. Skipping.", e)
+        log.error("Error in unmarshalling yaml: %s. " + skipping, e)
         raise
-    res = []
-    for r in (data or {}).get("resources") or []:
-        res.append((r or {}).get("entity") or {})
-    return res
+    log.debug("Detected %d apps", len(apps))
+    return apps
 
 
 def _s(v):
@@ -40,11 +139,7 @@ class CfAppsCollector(Collector):
     annotations = ("cf", "cloudfoundry")
 
     def collect(self, input_path, output_path):
-        try:
-            apps = _cf_apps()
-        except Exception as e:  # noqa: BLE001
-            log.error("%s", e)
-            raise
+        apps = _cf_apps("Skipping.")
         output_path = os.path.join(output_path, "cf")
         try:
             os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
@@ -52,28 +147,36 @@ class CfAppsCollector(Collector):
             log.error("Unable to create outputPath %s : %s", output_path, common.go_path_error(e, "mkdir"))
         inst = collection.CfInstanceApps()
         file_name = "instanceapps_"
-        log.debug("Detected %d apps", len(apps))
         for ent in apps:
-            app = collection.CfApplication(_s(ent.get("name")))
+            app = collection.CfApplication(ent.get("name", ""))
             log.debug("Reading info about %s", app.name)
-            if _s(ent.get("buildpack")) != "null":
-                app.buildpack = _s(ent.get("buildpack"))
-            if _s(ent.get("detected_buildpack")) != "null":
-                app.detected_buildpack = _s(ent.get("detected_buildpack"))
-            if _s(ent.get("dockerimage")) != "null":
-                app.docker_image = _s(ent.get("dockerimage"))
-            app.instances = int(ent.get("instances") or 0)
-            app.memory = int(ent.get("memory") or 0)
-            app.env = {k: _s(v) for k, v in (ent.get("environment_json") or {}).items()}
-            app.ports = [int(p) for p in ent.get("ports") or []]
+            if ent.get("buildpack", "") != "null":
+                app.buildpack = ent.get("buildpack", "")
+            if ent.get("detected_buildpack", "") != "null":
+                app.detected_buildpack = ent.get("detected_buildpack", "")
+            if ent.get("dockerimage", "") != "null":
+                app.docker_image = ent.get("dockerimage", "")
+            app.instances = ent.get("instances", 0)
+            app.memory = ent.get("memory", 0)
+            app.env = ent.get("environment_json") or {}
+            app.ports = ent.get("ports") or []
             inst.applications.append(app)
             file_name += app.name
         path = os.path.join(output_path, common.normalize_for_filename(file_name) + ".yaml")
-        common.write_yaml(path, inst)
+        try:
+            common.write_yaml(path, inst)
+        except OSError as e:
+            err = common.go_path_error(e, "open")
+            log.error("Unable to write collect output : %s", err)
+            raise RuntimeError(err) from e
 
 
 def get_all_cf_instance_buildpacks():
-    out = run(["cf", "buildpacks"]).decode("utf-8", "replace")
+    try:
+        out = run(["cf", "buildpacks"]).decode("utf-8", "replace")
+    except Exception as e:  # noqa: BLE001
+        log.warning("Error while getting buildpacks : %s", e)
+        raise
     bps = []
     for line in out.split("\n"):
         if line == "Getting buildpacks...":
@@ -87,18 +190,23 @@ def get_all_cf_instance_buildpacks():
 
 def get_all_cf_app_buildpacks():
     bps = []
-    for ent in _cf_apps():
-        if _s(ent.get("buildpack")):
-            bps.append(_s(ent.get("buildpack")))
-        if _s(ent.get("detected_buildpack")):
-            bps.append(_s(ent.get("detected_buildpack")))
+    for ent in _cf_apps("Skipping"):
+        if ent.get("buildpack"):
+            bps.append(ent["buildpack"])
+        if ent.get("detected_buildpack"):
+            bps.append(ent["detected_buildpack"])
     return bps
 
 
 def get_all_used_buildpacks(directory):
     from ..source.cfmanifest import read_application_manifest
     bps = []
-    for path in common.get_files_by_ext(directory, [".yml", ".yaml"]):
+    try:
+        files = common.get_files_by_ext(directory, [".yml", ".yaml"])
+    except (OSError, ValueError) as e:
+        log.warning("Unable to fetch yaml files and recognize application manifest yamls : %s", e)
+        files = []
+    for path in files:
         try:
             apps, _ = read_application_manifest(path, "", plantypes.YAMLS)
         except Exception as e:  # noqa: BLE001
@@ -171,7 +279,12 @@ class CFContainerTypesCollector(Collector):
     def collect(self, input_path, output_path):
         from ..containerizer.cnb import CNBContainerizer
         output_path = os.path.join(output_path, "cf")
-        os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+        try:
+            os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+        except OSError as e:
+            err = common.go_path_error(e, "mkdir")
+            log.error("Unable to create output path %s : %s", output_path, err)
+            raise RuntimeError(err) from e
         cz = collection.CfContainerizers()
         cnb = CNBContainerizer()
         cnb.init("")
@@ -186,6 +299,11 @@ class CFContainerTypesCollector(Collector):
         cz.buildpack_containerizers = get_buildpack_containerizers(names, buildpacks)
         file_name = "cfcontainertypes_" + "".join(names)
         path = os.path.join(output_path, common.normalize_for_filename(file_name) + ".yaml")
-        common.write_yaml(path, cz)
+        try:
+            common.write_yaml(path, cz)
+        except OSError as e:
+            err = common.go_path_error(e, "open")
+            log.error("Unable to write cf container type output %s : %s", file_name, err)
+            raise RuntimeError(err) from e
         if settings.fixed and not names:
             raise RuntimeError("No buildpacks found")

@@ -27,11 +27,11 @@ def _reject_constant(name):
 class _Context:
     """The attributes ``_json.make_scanner`` reads from a ``JSONDecoder``."""
 
-    def __init__(self, parse_int=int):
+    def __init__(self, parse_int=int, parse_float=float):
         self.strict = True
         self.object_hook = None
         self.object_pairs_hook = None
-        self.parse_float = float
+        self.parse_float = parse_float
         self.parse_int = parse_int
         self.parse_constant = _reject_constant
         self.memo = {}
@@ -53,11 +53,11 @@ def _text(s):
         return "".join("\ufffd" if "\udc80" <= c <= "\udcff" else c for c in t)
 
 
-def loads(s, parse_int=int):
+def loads(s, parse_int=int, parse_float=float):
     text = _text(s)
-    scan = _scanners.get(parse_int)
+    scan = _scanners.get((parse_int, parse_float))
     if scan is None:
-        scan = _scanners[parse_int] = _json.make_scanner(_Context(parse_int))
+        scan = _scanners[parse_int, parse_float] = _json.make_scanner(_Context(parse_int, parse_float))
     i, n = 0, len(text)
     while i < n and text[i] in _WS:
         i += 1
