@@ -320,3 +320,97 @@ def test_paginate_like_survey():
     assert survey.paginate(7, ch, 5) == ([2, 3, 4, 5, 6, 7, 8], 3)
     assert survey.paginate(7, ch, 9) == ([3, 4, 5, 6, 7, 8, 9], 6)
     assert survey.paginate(7, [1, 2], 1) == ([1, 2], 1)
+
+
+def test_cli_engine_every_tty_prompt_type(term, monkeypatch, capsys):
+    """cliengine.go:38-197: each problem type through its survey prompt; a
+    confirm default that strconv.ParseBool refuses is warned about and read
+    as false."""
+    monkeypatch.delenv("M2K_QA_PLAIN", raising=False)
+    eng = CliEngine(stdin=term.fin, stdout=term.fout)
+    prob = qa.new_multiselect_problem("Pick services:", ["hint"], ["a"], ["a", "b", "c"])
+    term.keys(DOWN, " ", "\r")
+    assert eng.fetch_answer(prob).answer == ["a", "b"]
+    prob = qa.new_input_problem("Name:", ["hint"], "dflt")
+    term.keys("\r")
+    assert eng.fetch_answer(prob).answer == ["dflt"]
+    prob = qa.new_multiline_input_problem("Text:", ["hint"], "")
+    term.keys("x\r", "\r", "\r")
+    assert eng.fetch_answer(prob).answer == ["x"]
+    prob = qa.new_password_problem("Password:", ["hint"])
+    term.keys("pw\r")
+    assert eng.fetch_answer(prob).answer == ["pw"]
+    prob = qa.new_confirm_problem("Sure?", ["hint"], False)
+    prob.default = ["maybe"]
+    term.keys("\r")
+    assert eng.fetch_answer(prob).answer == ["false"]
+    import logparse
+    assert logparse.logged(capsys.readouterr().err, 'Unable to parse default value : strconv.ParseBool: parsing '
+                           '"maybe": invalid syntax', "warning")
+    prob = qa.new_input_problem("Odd:", [], "")
+    prob.type = "Unknown"
+    with pytest.raises(log.FatalError):
+        eng.fetch_answer(prob)
+
+
+def _plain(monkeypatch, text):
+    import io
+    monkeypatch.delenv("M2K_QA_PLAIN", raising=False)
+    out = io.StringIO()
+    return CliEngine(stdin=io.StringIO(text), stdout=out), out
+
+
+def test_plain_select_retries_an_unknown_answer(monkeypatch):
+    eng, out = _plain(monkeypatch, "nope\n\n")
+    prob = qa.new_select_problem("Choose:", ["ctx"], "b", ["a", "b"])
+    assert eng.fetch_answer(prob).answer == ["b"]
+    text = out.getvalue()
+    assert text.startswith("? %d. Choose: \nHints: \n [ctx]\n   1) a\n  >2) b\n" % prob.id)
+    assert "  invalid answer: Unknown options selected\n" in text
+
+
+@pytest.mark.parametrize("typed,want", [
+    ("\n", ["a"]), ("-\n", []), ("2, c\n", ["b", "c"]), ("1,,3\n", ["a", "c"]),
+    ("9\nb\n", ["b"]),                      # out of range is a name, and no option has it: asked again
+])
+def test_plain_multiselect(monkeypatch, typed, want):
+    eng, out = _plain(monkeypatch, typed)
+    prob = qa.new_multiselect_problem("Pick:", [], ["a"], ["a", "b", "c"])
+    assert eng.fetch_answer(prob).answer == want
+    assert "  [✓] 1) a\n  [ ] 2) b\n" in out.getvalue()
+
+
+def test_plain_confirm_input_multiline_password(monkeypatch, capsys):
+    eng, out = _plain(monkeypatch, "yes\n\nfirst\nsecond\n\nsecret\n")
+    c = qa.new_confirm_problem("Sure?", [], False)
+    assert eng.fetch_answer(c).answer == ["true"] and "(y/N) > " in out.getvalue()
+    i = qa.new_input_problem("Name:", [], "dflt")
+    assert eng.fetch_answer(i).answer == ["dflt"] and "(dflt) > " in out.getvalue()
+    m = qa.new_multiline_input_problem("Text:", [], "keep")
+    assert eng.fetch_answer(m).answer == ["first\nsecond"]
+    p = qa.new_password_problem("Password:", [])
+    assert eng.fetch_answer(p).answer == ["secret"]
+    eng, out = _plain(monkeypatch, "\n\n")
+    m = qa.new_multiline_input_problem("Text:", [], "keep")
+    assert eng.fetch_answer(m).answer == ["keep"]
+    c = qa.new_confirm_problem("Sure?", [], True)
+    c.default = ["sometimes"]
+    assert eng.fetch_answer(c).answer == ["false"] and "(y/N) > " in out.getvalue()
+    assert "Unable to parse default value : " in capsys.readouterr().err
+
+
+def test_plain_end_of_input_and_unknown_type_are_fatal(monkeypatch):
+    eng, _ = _plain(monkeypatch, "")
+    with pytest.raises(log.FatalError):
+        eng.fetch_answer(qa.new_input_problem("Name:", [], "d"))
+    eng, _ = _plain(monkeypatch, "x\n")
+    prob = qa.new_input_problem("Odd:", [], "")
+    prob.type = "Unknown"
+    with pytest.raises(log.FatalError):
+        eng.fetch_answer(prob)
+
+
+def test_plain_mode_forced_on_a_tty(term, monkeypatch):
+    monkeypatch.setenv("M2K_QA_PLAIN", "1")
+    eng = CliEngine(stdin=term.fin, stdout=term.fout)
+    assert eng._terminal() is None
