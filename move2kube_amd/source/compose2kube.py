@@ -70,7 +70,8 @@ class ComposeTranslator(Translator):
             try:
                 proj = parse_v2(path)
             except ComposeError as e2:
-                log.debug("Failed to parse file at path %s as a docker compose file. Error V3: %s Error V1V2: %s", path, e3, e2)
+                log.debug("Failed to parse file at path %s as a docker compose file. Error V3: %r Error V1V2: %r",
+                          path, str(e3), str(e2))
                 return []
             log.debug("Found a docker compose file at path %s", path)
             out = []
@@ -84,7 +85,11 @@ class ComposeTranslator(Translator):
         return out
 
     def get_service_options(self, input_path, plan):
-        yamls = common.get_files_by_ext(input_path, [".yaml", ".yml"])
+        try:
+            yamls = common.get_files_by_ext(input_path, [".yaml", ".yml"])
+        except (OSError, ValueError) as e:
+            log.error("Unable to fetch yaml files at path %s Error: %r", input_path, common.go_error_text(e))
+            raise
         image_meta = {}
         for p in yamls:
             try:
