@@ -55,6 +55,152 @@ def substitute(s, mapping, warn_missing=False):
     return _PATTERN.sub(repl, s)
 
 
+# -- v3: docker/cli compose/template + compose/interpolation ------------------
+
+_V3_PATTERN = _lazy_re(r"\$(?i:(?P<escaped>\$)|(?P<named>[_a-z][_a-z0-9]*)|"
+                       r"\{(?P<braced>[_a-z][_a-z0-9]*(?::?[-?][^}]*)?)\}|(?P<invalid>))")
+
+
+class InvalidTemplateError(InterpolationError):
+    """docker/cli ``template.InvalidTemplateError``; ``template`` is what
+    ``newPathError`` quotes."""
+
+    def __init__(self, template):
+        super().__init__("Invalid template: " + log.go_quote(template))
+        self.template = template
+
+
+def _v3_funcs(sub, mapping):
+    """``DefaultSubstituteFuncs`` in order - softDefault ``:-``, hardDefault
+    ``-``, requiredNonEmpty ``:?``, required ``?`` - each applied when its
+    separator occurs anywhere in the substitution (``strings.Contains``) and
+    splitting at the first occurrence, so ``${A:?no-value}`` is a hard
+    default ``value`` for the variable ``A:?no``.  Returns (value, applied);
+    raises InvalidTemplateError for a required variable."""
+    for sep, empty_too, required in ((":-", True, False), ("-", False, False), (":?", True, True),
+                                     ("?", False, True)):
+        if sep not in sub:
+            continue
+        name, arg = sub.split(sep, 1)
+        value = mapping(name)
+        missing = value is None or (empty_too and value == "")
+        if required:
+            if missing:
+                raise InvalidTemplateError("required variable %s is missing a value: %s" % (name, arg))
+            return value
+        return arg if missing else value
+    value = mapping(sub)
+    return "" if value is None else value
+
+
+def substitute_v3(template, mapping):
+    """``template.Substitute``: (result, error or None).  As in docker/cli the
+    error is a variable that every later substitution overwrites - with
+    nothing when it succeeds - so a malformed ``$`` or a missing required
+    variable only fails the value when no substitution follows it; its own
+    place becomes ""."""
+    err = [None]
+
+    def repl(m):
+        if m.group("escaped") is not None:
+            return "$"
+        sub = m.group("named") or m.group("braced")
+        if not sub:
+            err[0] = InvalidTemplateError(template)
+            return ""
+        try:
+            value = _v3_funcs(sub, mapping)
+        except InvalidTemplateError as e:
+            err[0] = e
+            return ""
+        err[0] = None
+        return value
+    if "$" not in template:
+        return template, None
+    return _V3_PATTERN.sub(repl, template), err[0]
+
+
+def _to_int(v):
+    t = v[1:] if v[:1] in "+-" else v
+    if not t or not t.isascii() or not t.isdigit():
+        raise ValueError("strconv.Atoi: parsing %s: invalid syntax" % log.go_quote(v))
+    n = -int(t) if v[:1] == "-" else int(t)
+    if not -(1 << 63) <= n < (1 << 63):
+        raise ValueError("strconv.Atoi: parsing %s: value out of range" % log.go_quote(v))
+    return n
+
+
+def _to_float(v):
+    from ...utils.common import go_parse_float
+    return go_parse_float(v)
+
+
+def _to_bool(v):
+    low = v.lower()
+    if low in ("y", "yes", "true", "on"):
+        return True
+    if low in ("n", "no", "false", "off"):
+        return False
+    raise ValueError("invalid boolean: %s" % v)
+
+
+# loader/interpolate.go interpolateTypeCastMapping: an interpolated string at
+# one of these paths becomes the type the schema expects ("*" any key, "[]" a
+# list element)
+_V3_CASTS = tuple((tuple(pattern.split(".")), cast) for pattern, cast in (
+    ("services.*.configs.[].mode", _to_int), ("services.*.secrets.[].mode", _to_int),
+    ("services.*.healthcheck.retries", _to_int), ("services.*.healthcheck.disable", _to_bool),
+    ("services.*.deploy.replicas", _to_int), ("services.*.deploy.update_config.parallelism", _to_int),
+    ("services.*.deploy.update_config.max_failure_ratio", _to_float),
+    ("services.*.deploy.rollback_config.parallelism", _to_int),
+    ("services.*.deploy.rollback_config.max_failure_ratio", _to_float),
+    ("services.*.deploy.restart_policy.max_attempts", _to_int),
+    ("services.*.deploy.placement.max_replicas_per_node", _to_int),
+    ("services.*.ports.[].target", _to_int), ("services.*.ports.[].published", _to_int),
+    ("services.*.ulimits.*", _to_int), ("services.*.ulimits.*.hard", _to_int), ("services.*.ulimits.*.soft", _to_int),
+    ("services.*.privileged", _to_bool), ("services.*.read_only", _to_bool), ("services.*.stdin_open", _to_bool),
+    ("services.*.tty", _to_bool), ("volumes.*.external", _to_bool), ("networks.*.external", _to_bool),
+    ("networks.*.internal", _to_bool), ("networks.*.attachable", _to_bool)))
+
+
+def _caster(path):
+    parts = path.split(".")
+    for pattern, cast in _V3_CASTS:
+        if len(pattern) == len(parts) and all(p in ("*", x) for p, x in zip(pattern, parts)):
+            return cast
+    return None
+
+
+def _interpolate_v3(value, path, mapping):
+    if isinstance(value, str):
+        new, err = substitute_v3(value, mapping)
+        if err is not None:
+            raise InterpolationError("invalid interpolation format for %s: %s. You may need to escape any $ with "
+                                     "another $." % (path, log.go_quote(err.template)))
+        if new == value:
+            return value
+        cast = _caster(path)
+        if cast is None:
+            return new
+        try:
+            return cast(new)
+        except ValueError as e:
+            raise InterpolationError("error while interpolating %s: failed to cast to expected type: %s"
+                                     % (path, e)) from None
+    if isinstance(value, dict):
+        return {k: _interpolate_v3(v, path + "." + str(k), mapping) for k, v in value.items()}
+    if isinstance(value, list):
+        return [_interpolate_v3(v, path + ".[]", mapping) for v in value]
+    return value
+
+
+def interpolate_v3(config, mapping):
+    """``interpolation.Interpolate`` with the loader's type casts over a v3
+    config dict; the first error in document order (Go walks its maps in
+    random order) as InterpolationError with docker/cli's text."""
+    return {k: _interpolate_v3(v, str(k), mapping) for k, v in config.items()}
+
+
 def interpolate(obj, mapping, warn_missing=False):
     if isinstance(obj, str):
         return substitute(obj, mapping, warn_missing)

@@ -17,7 +17,7 @@ from ...utils import common, log, yamlio
 from ...utils.constants import VOLUME_PREFIX
 from . import schema as cschema
 from . import utils as cu
-from .interpolate import EnvFileError, InterpolationError, interpolate, parse_env_file
+from .interpolate import EnvFileError, InterpolationError, interpolate_v3, parse_env_file
 
 SUPPORTED_V3 = {"3", "3.0", "3.1", "3.2", "3.3", "3.4", "3.5", "3.6", "3.7", "3.8", "3.9"}
 
@@ -229,7 +229,7 @@ def parse_v3(path):
         raise ComposeError("unsupported Compose file version: %s" % version)
     env = cu.get_environment_variables()
     try:
-        parsed = interpolate(parsed, env.get)
+        parsed = interpolate_v3(parsed, env.get)
     except InterpolationError as e:
         raise ComposeError(str(e))
     services = _validate(parsed)
