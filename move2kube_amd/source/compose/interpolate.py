@@ -201,6 +201,124 @@ def interpolate_v3(config, mapping):
     return {k: _interpolate_v3(v, str(k), mapping) for k, v in config.items()}
 
 
+# -- v1/v2: libcompose config/interpolation.go (57bd716502dc) -----------------
+
+def _lc_name_char(c):
+    return c == "_" or "A" <= c <= "Z" or "a" <= c <= "z" or "0" <= c <= "9"
+
+
+class _LcFailed(Exception):
+    """parseLine's ``success == false`` - or an input on which libcompose
+    indexes past the end of the line (a trailing ``$`` or ``${NAME:``: a
+    panic) or rescans forever (a default without its ``}`` that a later
+    ``}`` appears to close)."""
+
+
+def _lc_default(line, pos):
+    """parseDefaultValue: every leading ``:`` and ``-`` is skipped, the rest up
+    to ``}`` is the default; (default, index before the ``}``)."""
+    n = len(line)
+    while pos < n and line[pos] in ":-":
+        pos += 1
+    start = pos
+    while pos < n:
+        if line[pos] == "}":
+            return line[start:pos], pos - 1
+        pos += 1
+    raise _LcFailed()
+
+
+def _lc_braces(line, pos, mapping, defaults):
+    """parseVariableWithBraces: a default (``:-`` or ``-``) is recorded in the
+    package-level ``defaultValues`` under the name read so far, then the
+    closing ``}`` returns the mapping of the name."""
+    n = len(line)
+    name = []
+    while pos < n:
+        c = line[pos]
+        if c == "}":
+            if not name:
+                raise _LcFailed()
+            return mapping("".join(name)), pos
+        if _lc_name_char(c):
+            name.append(c)
+        elif c == "-" or c == ":":
+            if c == ":" and (pos + 1 >= n or line[pos + 1] != "-"):
+                raise _LcFailed()
+            defaults["".join(name)], pos = _lc_default(line, pos)
+        else:
+            raise _LcFailed()
+        pos += 1
+    raise _LcFailed()
+
+
+def _lc_parse_line(line, mapping, defaults):
+    out = []
+    pos, n = 0, len(line)
+    while pos < n:
+        c = line[pos]
+        if c != "$":
+            out.append(c)
+            pos += 1
+            continue
+        pos += 1
+        if pos >= n:
+            raise _LcFailed()
+        c = line[pos]
+        if c == "$":
+            out.append("$")
+        elif c == "{":
+            val, pos = _lc_braces(line, pos + 1, mapping, defaults)
+            out.append(val)
+        elif _lc_name_char(c) and not ("0" <= c <= "9"):
+            start = pos
+            while pos < n and _lc_name_char(line[pos]):
+                pos += 1
+            out.append(mapping(line[start:pos]))
+            pos -= 1
+        else:
+            raise _LcFailed()
+        pos += 1
+    return "".join(out)
+
+
+def _lc_value(key, value, mapping, defaults):
+    if isinstance(value, str):
+        try:
+            return _lc_parse_line(value, mapping, defaults)
+        except _LcFailed:
+            raise InterpolationError('Invalid interpolation format for key "%s": "%s"' % (key, value)) from None
+    if isinstance(value, list):
+        return [_lc_value(key, v, mapping, defaults) for v in value]
+    if isinstance(value, dict):
+        return {k: _lc_value(key, v, mapping, defaults) for k, v in value.items()}
+    return value
+
+
+def interpolate_v1v2(raw_services, lookup, defaults):
+    """``InterpolateRawServiceMap``: every field of every service, the error
+    naming the field's key.  ``lookup(name)`` is libcompose's environment
+    lookup (None when it finds nothing; the OS lookup finds nothing for an
+    empty variable).  An unset variable takes a default recorded by any
+    ``${NAME:-x}`` or ``${NAME-x}`` read before it in this command (libcompose
+    keeps them in a package-level map, so they outlive the value and the file
+    that set them); so does a variable set to "" - both forms mean "unset or
+    empty" here.  Otherwise unset is "" with a warning, which the reference
+    never shows: it parses at logrus FatalLevel (v1v2.go:118-121)."""
+    def mapping(name):
+        value = lookup(name)
+        if value is None:
+            if name in defaults:
+                return defaults[name]
+            log.warning("The %s variable is not set. Substituting a blank string.", name)
+            return ""
+        if value == "" and name in defaults:
+            return defaults[name]
+        return value
+    return {name: ({k: _lc_value(k, v, mapping, defaults) for k, v in svc.items()} if isinstance(svc, dict) else svc)
+            for name, svc in raw_services.items()}
+
+
 def interpolate(obj, mapping, warn_missing=False):
     if isinstance(obj, str):
         return substitute(obj, mapping, warn_missing)

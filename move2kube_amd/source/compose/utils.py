@@ -270,7 +270,7 @@ def resolve_bind_source(src, working_dir):
     return src
 
 
-def command_memo(name, error_type, wrap):
+def command_memo(name, error_type, wrap, state=None):
     """Memoise a compose-file parser for the enclosing ``fsindex.scope()``
     (one command): the planner tries every YAML file as compose and the
     translator parses the same files again for each of their services.  The
@@ -278,7 +278,8 @@ def command_memo(name, error_type, wrap):
     ``--ignoreenv``, none of which change within a command.  A parse error
     (``error_type``) is worded with ``wrap % (path, %q of the cause)``,
     remembered, and logged at debug level on every call as the reference's
-    parser does."""
+    parser does.  ``state`` (snapshot/restore) is command-wide state the
+    parse reads and writes: the memo keys on it and replays its effect."""
     from ...utils.log import go_quote
 
     def deco(fn):
@@ -299,14 +300,17 @@ def command_memo(name, error_type, wrap):
                 except error_type as e:
                     log.debug(str(e))
                     raise
-            key = (path, settings.ignore_environment)
+            key = (path, settings.ignore_environment, state.snapshot() if state is not None else None)
             hit = cache.get(key)
             if hit is None:
                 try:
                     hit = (True, checked(path))
                 except error_type as e:
                     hit = (False, e)
+                hit += (state.snapshot() if state is not None else None,)
                 cache[key] = hit
+            elif state is not None:
+                state.restore(hit[2])
             if hit[0]:
                 return hit[1]
             log.debug(str(hit[1]))

@@ -20,7 +20,7 @@ from ...utils import common, log, yamlio
 from ...utils.constants import VOLUME_PREFIX, settings
 from . import schema as cschema
 from . import utils as cu
-from .interpolate import EnvFileError, InterpolationError, interpolate, parse_env_file
+from .interpolate import EnvFileError, InterpolationError, interpolate_v1v2, parse_env_file
 from .v3 import ComposeError, _as_list_of_str, _labels, _scalar_str
 
 V1_SERVICE_KEYS = {
@@ -92,8 +92,32 @@ def _env_lookup():
     def lookup(k):
         if k in dotenv:
             return dotenv[k]
-        return os.environ.get(k)
+        return os.environ.get(k) or None    # OsEnvLookup: an empty variable is not found
     return lookup
+
+
+def _lc_defaults():
+    """libcompose's package-level ``defaultValues``: one map for the whole
+    command (the reference's process), shared by every file it parses."""
+    from ...utils import fsindex
+    d = fsindex.scoped_cache("libcompose-defaults")
+    return d if d is not None else {}
+
+
+class _DefaultsState:
+    """What the compose-file memo keys on and replays: a file parsed again
+    with other defaults in force parses differently, and its parse records
+    its own defaults."""
+
+    @staticmethod
+    def snapshot():
+        return tuple(sorted(_lc_defaults().items()))
+
+    @staticmethod
+    def restore(snap):
+        d = _lc_defaults()
+        d.clear()
+        d.update(snap)
 
 
 def _prune_env_files(raw_services, compose_path):
@@ -152,7 +176,7 @@ def _load_file(path, lookup, compose_path):
     ``parseV2`` does for the main file and for every ``extends: {file: ...}``."""
     version, raw_services, parsed = _read_raw(path)
     try:
-        raw_services = interpolate(raw_services, lookup, warn_missing=True)
+        raw_services = interpolate_v1v2(raw_services, lookup, _lc_defaults())
     except InterpolationError as e:
         raise ComposeError(str(e))
     _prune_env_files(raw_services, compose_path)
@@ -268,13 +292,22 @@ def _parse_service(svc, in_file, datas, lookup, compose_path, depth=0):
     return merged
 
 
-@cu.command_memo("compose-v1v2", ComposeError, "Failed to load docker compose file at path %s Error: %s")
+@cu.command_memo("compose-v1v2", ComposeError, "Failed to load docker compose file at path %s Error: %s",
+                  state=_DefaultsState)
 def parse_v2(path):
     """Parse a v1/v2 compose file the way the reference's libcompose
     ``project.Parse()`` does (``v1v2.go:93-129``): interpolation (``.env`` then
     OS env), env-file pruning, validation, then per service ``env_file``
     folding and ``extends`` resolution (same file or ``file:``, chained).
+    The reference sets logrus to FatalLevel around ``Parse`` (v1v2.go:118-121),
+    so nothing logged in here - libcompose's warnings, the env-file pruning's
+    own - is shown.
     Returns {"version", "project", "services": [...], "networks": {...}}."""
+    with log.hold():        # dropped: FatalLevel
+        return _parse_v2(path)
+
+
+def _parse_v2(path):
     lookup = _env_lookup()
     version, raw_services, parsed = _load_file(path, lookup, path)
     base = os.path.dirname(os.path.abspath(path))
