@@ -338,14 +338,16 @@ class EnvFileError(ValueError):
     """A line docker/cli's ``opts.ParseEnvFile`` refuses."""
 
 
-def parse_env_file(path):
+def parse_env_file(path, first_wins=False):
     """docker/cli ``opts.ParseEnvFile`` (``parseKeyValueFile``): lines as
     ``bufio.Scanner`` splits them, a UTF-8 BOM dropped from the first,
     leading white space trimmed, ``#`` comments; ``KEY=VAL`` keeps the value
     as written (trailing blanks too), a bare ``KEY`` takes the OS
     environment's value when there is one.  A key with blanks, an empty key,
     bytes that are not UTF-8 or a 64 KiB line raise :class:`EnvFileError`
-    with docker/cli's text; an unreadable file raises OSError."""
+    with docker/cli's text; an unreadable file raises OSError.  A key given
+    twice keeps its last value, or its first with ``first_wins`` (libcompose's
+    ``EnvfileLookup`` returns the first line that names the key)."""
     from ...utils import common
     data = common.read_bytes(path)
     lines, too_long = common.go_scan_lines(data)
@@ -368,10 +370,11 @@ def parse_env_file(path):
         if not variable:
             raise EnvFileError("poorly formatted environment: no variable name on line '%s'" % line)
         if eq:
-            out[variable] = value
+            if not (first_wins and variable in out):
+                out[variable] = value
         else:
             v = os.environ.get(line)
-            if v is not None:
+            if v is not None and not (first_wins and common.go_trim_space(line) in out):
                 out[common.go_trim_space(line)] = v
     if too_long:
         raise EnvFileError("bufio.Scanner: token too long")

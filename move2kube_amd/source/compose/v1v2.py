@@ -85,7 +85,7 @@ def _env_lookup():
     dotenv = {}
     if os.path.isfile(env_path):
         try:
-            dotenv = parse_env_file(env_path)
+            dotenv = parse_env_file(env_path, first_wins=True)
         except (OSError, EnvFileError):   # libcompose EnvfileLookup: an unparsable .env is empty
             dotenv = {}
 

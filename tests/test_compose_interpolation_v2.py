@@ -109,3 +109,11 @@ def test_invalid_interpolation_fails_the_load(tmp_path, monkeypatch):
         v1v2.parse_v2(str(p))
     assert str(ei.value) == ('Failed to load docker compose file at path %s Error: "Invalid interpolation format for '
                              'key \\"command\\": \\"echo ${A?required}\\""' % p)
+
+
+def test_dotenv_lookup_takes_the_first_line_naming_the_key(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    (tmp_path / ".env").write_text("TAG=one\nTAG=two\n")
+    p = tmp_path / "docker-compose.yml"
+    p.write_text('version: "2"\nservices:\n  web:\n    image: "nginx:${TAG}"\n')
+    assert v1v2.parse_v2(str(p))["services"][0]["image"] == "nginx:one"
