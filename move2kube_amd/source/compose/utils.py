@@ -270,6 +270,13 @@ def resolve_bind_source(src, working_dir):
     return src
 
 
+def duration_seconds(d):
+    """``int64(time.Duration(d).Seconds())``: whole seconds, truncated toward
+    zero (a negative "-1.5s" is -1)."""
+    q = abs(d) // 10 ** 9
+    return -q if d < 0 else q
+
+
 def command_memo(name, error_type, wrap, state=None):
     """Memoise a compose-file parser for the enclosing ``fsindex.scope()``
     (one command): the planner tries every YAML file as compose and the

@@ -505,13 +505,14 @@ class V1V2Loader:
             if secctx:
                 cont["securityContext"] = secctx
             # group_add goes to a pod security context the reference never attaches (kept for parity)
-            try:
-                [int(g) for g in cs["group_add"]]
+            try:    # getGroupAdd (v1v2.go:448-459)
+                for g in cs["group_add"]:
+                    common.cast_to_int(g)
             except ValueError as e:
-                log.warning("GroupAdd should be in gid format, not as group name : %s", e)
+                log.warning("GroupAdd should be in gid format, not as group name : unable to get group_add: %s", e)
             if cs["stop_grace_period"]:
                 try:
-                    sc.pod_spec["terminationGracePeriodSeconds"] = int(cu.parse_duration(cs["stop_grace_period"]) // 10 ** 9)
+                    sc.pod_spec["terminationGracePeriodSeconds"] = cu.duration_seconds(cu.parse_duration(cs["stop_grace_period"]))
                 except ValueError:
                     log.warning("Failed to parse duration %s for service %s", cs["stop_grace_period"], name)
             if cs["mem_limit"]:

@@ -666,13 +666,13 @@ class V3Loader:
         else:
             log.warning("Could not find command to execute in probe : %s", hc["test"])
         if hc["timeout"] is not None:
-            probe["timeoutSeconds"] = int(cu.parse_duration(hc["timeout"]) // 10 ** 9)
+            probe["timeoutSeconds"] = cu.duration_seconds(cu.parse_duration(hc["timeout"]))
         if hc["interval"] is not None:
-            probe["periodSeconds"] = int(cu.parse_duration(hc["interval"]) // 10 ** 9)
+            probe["periodSeconds"] = cu.duration_seconds(cu.parse_duration(hc["interval"]))
         if hc["retries"] is not None:
             probe["failureThreshold"] = int(hc["retries"])
         if hc["start_period"] is not None:
-            probe["initialDelaySeconds"] = int(cu.parse_duration(hc["start_period"]) // 10 ** 9)
+            probe["initialDelaySeconds"] = cu.duration_seconds(cu.parse_duration(hc["start_period"]))
         return probe
 
     @staticmethod

@@ -242,3 +242,24 @@ def test_v2_named_volume_names(tmp_path, monkeypatch):
     assert srcs == ["myapp_a", "real-b", "c", "d", "e", os.path.join(root, "f")]
     monkeypatch.setenv("COMPOSE_PROJECT_NAME", "Other_Name")
     assert _v2_services(root)["s"]["volumes"][0]["source"] == "othername_a"
+
+
+def test_v2_group_names_and_negative_grace_period(tmp_path, monkeypatch, capsys):
+    """getGroupAdd's cast error, wrapped (v1v2.go:448-459), is the warning
+    text; durationInSeconds truncates toward zero as int64(d.Seconds()) does."""
+    import logparse
+    from move2kube_amd.models import plan as plantypes
+    from move2kube_amd.source.compose.v1v2 import V1V2Loader
+    from move2kube_amd.utils import log
+    monkeypatch.chdir(tmp_path)
+    p = tmp_path / "docker-compose.yml"
+    p.write_text('version: "2"\nservices:\n  web:\n    image: nginx\n    group_add: ["100", "wheel"]\n'
+                 '    stop_grace_period: -1500ms\n')
+    plan = plantypes.new_plan()
+    plan.root_dir = str(tmp_path)
+    svc = plantypes.Service.new("web", plantypes.COMPOSE2KUBE)
+    log.set_verbose(False)
+    ir = V1V2Loader().convert_to_ir(str(p), plan, svc)
+    assert ir.services["web"].pod_spec["terminationGracePeriodSeconds"] == -1
+    assert logparse.logged(capsys.readouterr().err, 'GroupAdd should be in gid format, not as group name : unable to '
+                           'get group_add: unable to cast "wheel" of type string to int', "warning")
