@@ -1,58 +1,23 @@
-"""Compose variable interpolation.
+"""Compose variable interpolation, each version as its reference library does it.
 
-* v3 follows docker/cli ``template.Substitute``: ``$$`` escapes, ``$VAR``,
-  ``${VAR}``, ``${VAR:-default}``, ``${VAR-default}``, ``${VAR:?err}``,
-  ``${VAR?err}``; an unset variable becomes the empty string; a malformed
-  ``$`` is an error.
-* v1/v2 follows libcompose: the same substitution syntax, unset variables are
-  replaced by "" with a warning.
+* v3: docker/cli ``compose/template.Substitute`` (``$$``, ``$VAR``,
+  ``${VAR}``, ``${VAR:-d}``, ``${VAR-d}``, ``${VAR:?e}``, ``${VAR?e}``) and
+  ``compose/interpolation.Interpolate`` with the loader's type casts.
+* v1/v2: libcompose's hand-written scanner (``$$``, ``$VAR``, ``${VAR}``,
+  ``${VAR:-d}``/``${VAR-d}``, no ``?`` forms) with its package-level
+  defaults.
 Only values are interpolated (not keys), recursively through maps and lists.
+Also ``parse_env_file``: docker/cli's ``opts.ParseEnvFile``.
 """
 
 import os
-import re
 
 from ...utils import log
 from ...utils.lazyre import lazy as _lazy_re
 
-_PATTERN = _lazy_re(
-    r"\$(?:(?P<escaped>\$)|(?P<named>[_a-zA-Z][_a-zA-Z0-9]*)|\{(?P<braced>[_a-zA-Z][_a-zA-Z0-9]*(?::?[-?][^}]*)?)\}|(?P<invalid>))")
-_BRACED_RE = _lazy_re(r"^([_a-zA-Z][_a-zA-Z0-9]*)(?:(:?)([-?])(.*))?$", re.S)
-
 
 class InterpolationError(ValueError):
     pass
-
-
-def substitute(s, mapping, warn_missing=False):
-    def repl(m):
-        if m.group("escaped") is not None:
-            return "$"
-        name = m.group("named") or m.group("braced")
-        if name is None:
-            raise InterpolationError("Invalid template: %r" % s)
-        if m.group("braced") is not None:
-            mm = _BRACED_RE.match(name)
-            var, colon, op, arg = mm.group(1), mm.group(2), mm.group(3), mm.group(4)
-            val = mapping(var)
-            if op == "-":
-                if val is None or (colon and val == ""):
-                    return arg
-                return val
-            if op == "?":
-                if val is None or (colon and val == ""):
-                    raise InterpolationError("required variable %s is missing a value: %s" % (var, arg))
-                return val
-            name = var
-        val = mapping(name)
-        if val is None:
-            if warn_missing:
-                log.warning("The %s variable is not set. Substituting a blank string.", name)
-            return ""
-        return val
-    if "$" not in s:
-        return s
-    return _PATTERN.sub(repl, s)
 
 
 # -- v3: docker/cli compose/template + compose/interpolation ------------------
@@ -317,21 +282,6 @@ def interpolate_v1v2(raw_services, lookup, defaults):
         return value
     return {name: ({k: _lc_value(k, v, mapping, defaults) for k, v in svc.items()} if isinstance(svc, dict) else svc)
             for name, svc in raw_services.items()}
-
-
-def interpolate(obj, mapping, warn_missing=False):
-    if isinstance(obj, str):
-        return substitute(obj, mapping, warn_missing)
-    if isinstance(obj, dict):
-        return {k: interpolate(v, mapping, warn_missing) for k, v in obj.items()}
-    if isinstance(obj, list):
-        return [interpolate(v, mapping, warn_missing) for v in obj]
-    return obj
-
-
-def os_env_mapping(env=None):
-    env = dict(os.environ) if env is None else env
-    return env.get
 
 
 class EnvFileError(ValueError):

@@ -1,0 +1,54 @@
+"""Small off-path branches: the translator registry when a translator fails
+(reference ``internal/source/translator.go:48-66``: the counts are logged
+before the error is checked, then "[%T] Failed : %s"), the abstract
+translator, and the lazy regular expressions / modules."""
+
+import pytest
+
+import logparse
+from move2kube_amd.models import plan as plantypes
+from move2kube_amd.source import translator
+from move2kube_amd.utils import lazyre, log
+
+
+def test_a_failing_translator_is_warned_about_and_skipped(monkeypatch, capsys):
+    from move2kube_amd.source.compose2kube import ComposeTranslator
+
+    def boom(self, services, plan):
+        raise RuntimeError("compose exploded")
+    monkeypatch.setattr(ComposeTranslator, "translate", boom)
+    plan = plantypes.new_plan()
+    log.set_verbose(True)
+    try:
+        ir = translator.translate(plan)
+    finally:
+        log.set_verbose(False)
+    assert ir.services == {}
+    err = capsys.readouterr().err
+    assert logparse.logged(err, "[*source.ComposeTranslator] Failed : compose exploded", "warning")
+    msgs = [m for _lv, m in logparse.messages(err)]
+    i = msgs.index("[*source.ComposeTranslator] Failed : compose exploded")
+    assert msgs[i - 2:i] == ["Services translated : 0", "Containers translated : 0"]
+    assert "[*source.CfManifestTranslator] Done" in msgs[i:]
+
+
+def test_abstract_translator():
+    t = translator.Translator()
+    assert repr(t) == "*source.Translator" and t.get_translator_type() == ""
+    with pytest.raises(NotImplementedError):
+        t.get_service_options("", None)
+    with pytest.raises(NotImplementedError):
+        t.translate([], None)
+
+
+def test_lazy_pattern_and_module():
+    p = lazyre.lazy(r"a(b)")
+    assert repr(p) == "LazyPattern('a(b)')"
+    assert p.compiled().pattern == "a(b)"
+    with pytest.raises(AttributeError):
+        p.__wrapped__
+    assert p.match("ab").group(1) == "b" and p.groups == 1
+    m = lazyre.LazyModule("colorsys")
+    with pytest.raises(AttributeError):
+        m.__wrapped__
+    assert m.rgb_to_hsv(0, 0, 0) == (0.0, 0.0, 0.0)
