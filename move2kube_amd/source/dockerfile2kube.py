@@ -44,7 +44,12 @@ class DockerfileTranslator(Translator):
 
     def get_service_options(self, input_path, plan):
         services = []
-        sdfs = get_dockerfile_services(input_path, plan.name)
+        try:
+            sdfs = get_dockerfile_services(input_path, plan.name)
+        except OSError as e:
+            err = common.go_path_error(e, "stat")
+            log.error("Unable to get Dockerfiles : %s", err)
+            raise RuntimeError(err) from e
         for sn in sorted(sdfs):
             dfs = sdfs[sn]
             ns = self.new_service(sn)
@@ -63,10 +68,13 @@ class DockerfileTranslator(Translator):
         ir = irtypes.new_ir(plan)
         for service in services:
             if service.translation_type != self.translation_type:
+                log.debug("The service %s has translation type %s . Expected %s . Skipping.", service.service_name,
+                          service.translation_type, self.translation_type)
                 continue
             if not service.target_options:
                 log.debug("The service %s has no containerization target options. Skipping.", service.service_name)
                 continue
+            log.debug("Translating %s", service.service_name)
             try:
                 c = ReuseDockerfileContainerizer().get_container(plan, service)
             except Exception as e:  # noqa: BLE001
@@ -100,9 +108,15 @@ def find_dockerfiles(input_path):
 
 
 def get_dockerfile_services(input_path, proj_name):
-    if not os.path.exists(input_path):
-        log.warning("Error in walking through files due to : %s does not exist", input_path)
-        return {}
+    """``getDockerfileServices`` (dockerfile2kube.go:147-199): a missing input
+    path is warned about (unquoted, unlike ``GetFilesByExt``) and raised as
+    OSError; a file is walked as itself, with the walk's "is not a directory"
+    warning."""
+    try:
+        os.stat(input_path)
+    except FileNotFoundError as e:
+        log.warning("Error in walking through files due to : %s", common.go_path_error(e, "stat"))
+        raise
     files = find_dockerfiles(input_path)
     log.debug("No of dockerfiles identified : %d", len(files))
     repo_dfs = {}

@@ -52,3 +52,36 @@ def test_lazy_pattern_and_module():
     with pytest.raises(AttributeError):
         m.__wrapped__
     assert m.rgb_to_hsv(0, 0, 0) == (0.0, 0.0, 0.0)
+
+
+def test_dockerfile_planner_on_a_missing_input_path(tmp_path, capsys):
+    """dockerfile2kube.go:44-50,147-152: the walk warning (unquoted), the
+    planner's error, then the registry's "[%T] Failed"."""
+    from move2kube_amd.source.dockerfile2kube import DockerfileTranslator
+    gone = tmp_path / "gone"
+    plan = plantypes.new_plan()
+    with pytest.raises(RuntimeError, match="^stat %s: no such file or directory$" % gone):
+        DockerfileTranslator().get_service_options(str(gone), plan)
+    err = capsys.readouterr().err
+    assert logparse.logged(err, "Error in walking through files due to : stat %s: no such file or directory" % gone,
+                           "warning")
+    assert logparse.logged(err, "Unable to get Dockerfiles : stat %s: no such file or directory" % gone, "error")
+
+
+def test_dockerfile_translate_debug_lines(tmp_path, capsys):
+    from move2kube_amd.source.dockerfile2kube import DockerfileTranslator
+    (tmp_path / "Dockerfile").write_text("FROM alpine\nEXPOSE 8080\n")
+    plan = plantypes.new_plan()
+    plan.root_dir = str(tmp_path)
+    (svc,) = DockerfileTranslator().get_service_options(str(tmp_path), plan)
+    other = plantypes.Service.new("x", plantypes.ANY2KUBE)
+    log.set_verbose(True)
+    try:
+        ir = DockerfileTranslator().translate([other, svc], plan)
+    finally:
+        log.set_verbose(False)
+    assert list(ir.services) == [svc.service_name]
+    err = capsys.readouterr().err
+    assert logparse.logged(err, "The service x has translation type %s . Expected %s . Skipping."
+                           % (plantypes.ANY2KUBE, plantypes.DOCKERFILE2KUBE), "debug")
+    assert logparse.logged(err, "Translating %s" % svc.service_name, "debug")
