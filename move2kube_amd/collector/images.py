@@ -60,8 +60,12 @@ def get_docker_inspect_result(image):
 def get_all_image_names():
     try:
         out = run(["docker", "image", "list", "--format", "{{.Repository}}:{{.Tag}}"])
-    except (OSError, CommandError) as e:
+    except CommandError as e:
         log.warning("Error while running docker image list : %s", e)
+        raise
+    except OSError:
+        # the reference runs it through `bash -c`: a missing docker is bash's 127
+        log.warning("Error while running docker image list : %s", common.go_exit_status(127))
         raise
     images = []
     for image in out.decode("utf-8", "replace").split("\n"):
@@ -75,20 +79,37 @@ def get_all_image_names():
 
 
 def get_dc_image_names(directory):
+    """``getDCImageNames`` (imagescollector.go:156-170): every YAML file read
+    with ``common.ReadYaml`` into ``sourcetypes.DockerCompose`` - a file whose
+    ``services`` is not a mapping of mappings (null services and fields
+    allowed) fails that typed decode and is skipped; a listing error is a
+    warning and no file is read."""
     names = []
-    for path in common.get_files_by_ext(directory, [".yml", ".yaml"]):
+    try:
+        files = common.get_files_by_ext(directory, [".yml", ".yaml"])
+    except (OSError, ValueError) as e:
+        log.warning("Unable to fetch yaml files and recognize Docker image yamls : %s", common.go_error_text(e, "lstat"))
+        files = []
+    for path in files:
         try:
             doc = common.read_yaml(path)
         except Exception:  # noqa: BLE001
             continue
+        if doc is None:
+            continue
         if not isinstance(doc, dict):
             continue
         services = doc.get("services")
-        if not isinstance(services, dict):
+        if services is None:
+            continue
+        if not isinstance(services, dict) or not all(
+                v is None or (isinstance(v, dict) and not isinstance(v.get("image"), (dict, list)))
+                for v in services.values()):
             continue
         for name in sorted(services):
-            svc = services[name]
-            names.append(str(svc.get("image", "")) if isinstance(svc, dict) else "")
+            svc = services[name] or {}
+            image = svc.get("image")
+            names.append("" if image is None else common.go_bool_str(image) if isinstance(image, bool) else str(image))
     return names
 
 
@@ -97,7 +118,12 @@ class ImagesCollector(Collector):
 
     def collect(self, input_path, output_path):
         output_path = os.path.join(output_path, "images")
-        os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+        try:
+            os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+        except OSError as e:
+            err = common.go_path_error(e, "mkdir")
+            log.error("Unable to create output directory %s : %s", output_path, err)
+            raise RuntimeError(err) from e
         names = get_all_image_names() if input_path == "" else get_dc_image_names(input_path)
         log.debug("Images : %s", names)
         # one `docker inspect` per image, up to 8 at a time (the reference runs
@@ -120,3 +146,7 @@ class ImagesCollector(Collector):
                 common.write_yaml(path, info)
             except OSError as e:
                 log.error("Unable to write file %s : %s", path, common.go_path_error(e, "open"))
+            else:
+                if not settings.fixed:
+                    # imagescollector.go:75-76 logs the write's error unconditionally: %s of a nil error
+                    log.error("Unable to write file %s : %s", path, "%!s(<nil>)")

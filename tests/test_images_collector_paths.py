@@ -95,7 +95,8 @@ def test_compose_image_names_skip_non_compose_yaml(tmp_path):
     (tmp_path / "b.yaml").write_text("- just a list\n")
     (tmp_path / "c.yaml").write_text("services: [x]\n")
     (tmp_path / "d.yml").write_text("key: [unclosed\n")
-    assert images.get_dc_image_names(str(tmp_path)) == ["", "nginx"]
+    # a scalar service fails yaml.v3's decode into sourcetypes.DCService: the whole file is skipped
+    assert images.get_dc_image_names(str(tmp_path)) == []
 
 
 def test_collect_skips_failures_and_reports_unwritable_output(tmp_path, monkeypatch, capsys):
@@ -132,3 +133,57 @@ def test_collect_re_raises_what_is_not_a_command_failure(tmp_path, monkeypatch):
     monkeypatch.setattr(images, "get_docker_inspect_result", boom)
     with pytest.raises(KeyError):
         images.ImagesCollector().collect(str(src), str(tmp_path / "out"))
+
+
+@pytest.mark.parametrize("mode", ["reference", "fixed"])
+def test_every_written_image_file_logs_the_nil_write_error_in_reference_mode(tmp_path, monkeypatch, capsys, mode):
+    from move2kube_amd.utils import common
+    from move2kube_amd.utils.constants import settings
+    monkeypatch.setattr(settings, "compat", mode)
+    src = tmp_path / "src"
+    src.mkdir()
+    (src / "docker-compose.yaml").write_text("services:\n  a: {image: ok:1}\n")
+    _docker(tmp_path, monkeypatch, "printf '[{\"RepoTags\":[\"ok:1\"],\"ContainerConfig\":{}}]'\n")
+    log.set_verbose(False)
+    images.ImagesCollector().collect(str(src), str(tmp_path / "out"))
+    path = tmp_path / "out" / "images" / (common.normalize_for_filename("ok:1") + ".yaml")
+    assert path.is_file()
+    logged = logparse.logged(capsys.readouterr().err, "Unable to write file %s : %%!s(<nil>)" % path, "error")
+    assert logged == (mode == "reference")
+
+
+def test_compose_files_the_typed_decode_refuses_are_skipped(tmp_path):
+    """sourcetypes.DockerCompose: services must map to mappings (or null)."""
+    (tmp_path / "a.yaml").write_text("services:\n  x: {image: one:1}\n  y:\n  z: {image: 3}\n")
+    (tmp_path / "b.yaml").write_text("services:\n  x: {image: two:1}\n  y: [not, a, service]\n")
+    (tmp_path / "c.yaml").write_text("services:\n  x: {image: {nested: 1}}\n")
+    (tmp_path / "d.yaml").write_text("services: [x]\n")
+    (tmp_path / "e.yaml").write_text("just: a file\n")
+    assert images.get_dc_image_names(str(tmp_path)) == ["one:1", "", "3"]
+
+
+def test_listing_failure_is_a_warning(tmp_path, monkeypatch, capsys):
+    from move2kube_amd.utils import common
+
+    def boom(*a):
+        raise OSError(13, "Permission denied", str(tmp_path))
+    monkeypatch.setattr(common, "get_files_by_ext", boom)
+    assert images.get_dc_image_names(str(tmp_path)) == []
+    assert logparse.logged_containing(capsys.readouterr().err, "Unable to fetch yaml files and recognize Docker image "
+                                      "yamls : ", "warning")
+
+
+def test_output_directory_that_cannot_be_made(tmp_path, capsys):
+    (tmp_path / "out").mkdir()
+    (tmp_path / "out" / "images").write_text("a file")
+    with pytest.raises(RuntimeError, match="^mkdir %s: not a directory$" % (tmp_path / "out" / "images")):
+        images.ImagesCollector().collect(str(tmp_path / "src"), str(tmp_path / "out"))
+    assert logparse.logged(capsys.readouterr().err, "Unable to create output directory %s : mkdir %s: not a directory"
+                           % (tmp_path / "out" / "images", tmp_path / "out" / "images"), "error")
+
+
+def test_docker_missing_for_the_image_list_is_bash_127(tmp_path, monkeypatch, capsys):
+    monkeypatch.setenv("PATH", str(tmp_path))
+    with pytest.raises(OSError):
+        images.get_all_image_names()
+    assert logparse.logged(capsys.readouterr().err, "Error while running docker image list : exit status 127", "warning")
