@@ -209,15 +209,33 @@ class ClusterCollector(Collector):
 
     def collect_using_api(self):
         from . import kubeapi  # http.client/ssl: only when the k8s collector runs
-        client = kubeapi.open_client(self.get_cluster_command())
         try:
-            groups = self.get_server_groups(client)
+            client = kubeapi.open_client(self.get_cluster_command())
+        except kubeapi.ClientConfigError as e:      # getAPI (clustercollector.go:179-186, 301-306)
+            log.warning("Failed to get the default config for the cluster API client. Error: %r", str(e))
+            log.warning("Failed to api handle for cluster")
+            raise
+        try:
+            err = "Failed to retrieve preferred group information from cluster"
+            try:
+                groups = self.get_server_groups(client)
+            except kubeapi.DiscoveryError:
+                log.error("API request for server-group list failed")
+                log.warning(err)
+                raise
             gv_list = self.get_preferred_resources_using_api(groups)
             if not gv_list:
-                raise RuntimeError("Failed to retrieve preferred group information from cluster")
-            kinds = self.get_kinds_for_groups(client, groups)
+                log.warning(err)
+                raise RuntimeError(err)
+            err = "Failed to retrieve <kind, group-version> information from cluster"
+            try:
+                kinds = self.get_kinds_for_groups(client, groups)
+            except (kubeapi.DiscoveryError, RuntimeError):
+                log.warning(err)
+                raise
             if not kinds:
-                raise RuntimeError("Failed to retrieve <kind, group-version> information from cluster")
+                log.warning(err)
+                raise RuntimeError(err)
         finally:
             client.close()
         self.sort_gv_by_preference(gv_list, kinds)

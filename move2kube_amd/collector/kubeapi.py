@@ -50,6 +50,26 @@ class UnsupportedConfig(DiscoveryError):
     """The kubeconfig needs something only the cluster CLI can do."""
 
 
+class NoKubeconfig(UnsupportedConfig):
+    """No kubeconfig file exists."""
+
+
+class ClientConfigError(DiscoveryError):
+    """client-go's ``ClientConfig()`` error: no configuration at all."""
+
+
+# clientcmd ErrEmptyConfig inside errConfigurationInvalid (client-go v0.19)
+EMPTY_CONFIG = ("invalid configuration: no configuration has been provided, try setting KUBERNETES_MASTER "
+                "environment variable")
+IN_CLUSTER_TOKEN = "/var/run/secrets/kubernetes.io/serviceaccount/token"
+
+
+def in_cluster_possible():
+    """``inClusterClientConfig.Possible``: the service env vars and a token file."""
+    return (os.environ.get("KUBERNETES_SERVICE_HOST", "") != "" and os.environ.get("KUBERNETES_SERVICE_PORT", "") != ""
+            and os.path.isfile(IN_CLUSTER_TOKEN))
+
+
 # ---------------------------------------------------------------------------
 # kubeconfig loading (client-go NewDefaultClientConfigLoadingRules)
 # ---------------------------------------------------------------------------
@@ -97,7 +117,7 @@ def load_kubeconfig(paths=None):
                         val[fk] = os.path.join(base, val[fk])
                 merged[section][name] = val
     if not found:
-        raise UnsupportedConfig("no kubeconfig file found (%s)" % os.pathsep.join(paths or kubeconfig_paths()))
+        raise NoKubeconfig("no kubeconfig file found (%s)" % os.pathsep.join(paths or kubeconfig_paths()))
     return merged
 
 
@@ -307,9 +327,15 @@ class ProxyClient(_HTTPClient):
 
 
 def open_client(cluster_cmd):
-    """Direct kubeconfig client, else a proxy through the cluster CLI."""
+    """Direct kubeconfig client, else a proxy through the cluster CLI.  With
+    no kubeconfig at all and no in-cluster service account, client-go's
+    ``ClientConfig()`` fails and so does this (ClientConfigError)."""
     try:
         return KubeconfigClient()
+    except NoKubeconfig as e:
+        if not in_cluster_possible():
+            raise ClientConfigError(EMPTY_CONFIG) from None
+        log.debug("Direct discovery not possible (%s); using %s proxy", e, cluster_cmd)
     except (UnsupportedConfig, ssl.SSLError, OSError, ValueError) as e:
         log.debug("Direct discovery not possible (%s); using %s proxy", e, cluster_cmd)
     return ProxyClient(cluster_cmd)

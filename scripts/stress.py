@@ -217,7 +217,14 @@ def _collect_k8s(work, env, launcher):
     full = dict(os.environ)
     full.update(env)
     full["PATH"] = os.pathsep.join([bindir, STUBBIN, "/usr/bin", "/bin"])
-    full["KUBECONFIG"] = os.path.join(work, "no-kubeconfig")
+    # exec credentials: discovery goes through the stand-in `kubectl proxy`
+    kc = os.path.join(work, "kubeconfig")
+    with open(kc, "w") as f:
+        f.write('{"current-context": "c", "contexts": [{"name": "c", "context": {"cluster": "k", "user": "u"}}], '
+                '"clusters": [{"name": "k", "cluster": {"server": "https://stub.invalid"}}], '
+                '"users": [{"name": "u", "user": {"exec": {"command": "stub-token", "apiVersion": "x"}}}]}')
+    full["KUBECONFIG"] = kc
+    full.pop("KUBERNETES_SERVICE_HOST", None)
     full["HOME"] = os.path.join(work, "home")
     full["PYTHONPATH"] = ROOT + os.pathsep + full.get("PYTHONPATH", "")
     out = os.path.join(work, "collect")

@@ -19,8 +19,14 @@ STUBS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "st
 @pytest.fixture
 def stub_path(monkeypatch, tmp_path):
     monkeypatch.setenv("PATH", STUBS + os.pathsep + "/usr/bin:/bin")
-    # never a real cluster: no kubeconfig unless a test writes one
-    monkeypatch.setenv("KUBECONFIG", str(tmp_path / "no-kubeconfig"))
+    # never a real cluster: a kubeconfig whose exec credentials send discovery
+    # through the stub `kubectl proxy`, unless a test writes another one
+    kc = tmp_path / "stub-kubeconfig"
+    kc.write_text('{"current-context": "c", "contexts": [{"name": "c", "context": {"cluster": "k", "user": "u"}}], '
+                  '"clusters": [{"name": "k", "cluster": {"server": "https://stub.invalid"}}], '
+                  '"users": [{"name": "u", "user": {"exec": {"command": "stub-token", "apiVersion": "x"}}}]}')
+    monkeypatch.setenv("KUBECONFIG", str(kc))
+    monkeypatch.delenv("KUBERNETES_SERVICE_HOST", raising=False)
     monkeypatch.setenv("M2K_STUB_LOG", str(tmp_path / "stub.log"))
     return tmp_path
 
@@ -396,3 +402,46 @@ def test_collector_registry_matches_the_classes():
     for c, (_, _, ann) in zip(got, collector.REGISTRY):
         assert tuple(c.get_annotations()) == ann
     assert [type(c).__name__ for c in collector.get_collectors(["cf"])] == ["CFContainerTypesCollector", "CfAppsCollector"]
+
+
+def test_no_kubeconfig_fails_the_api_path_as_client_go_does(stub_path, monkeypatch, capsys):
+    """clustercollector.go:179-186,301-306 and collect: with no kubeconfig and
+    no in-cluster service account, client-go's ClientConfig() fails with
+    ErrEmptyConfig; the CLI fallback collects instead, and no proxy starts."""
+    monkeypatch.setenv("KUBECONFIG", str(stub_path / "none"))
+    m = _collect_map(stub_path)["spec"]["apiKindVersionMap"]
+    assert m["Deployment"] == ["apps/v1"]
+    calls = _stub_calls(stub_path)
+    assert not any(c.startswith("kubectl proxy") for c in calls)
+    assert any(c.startswith("kubectl api-resources") for c in calls)
+    err = capsys.readouterr().err
+    empty = ("invalid configuration: no configuration has been provided, try setting KUBERNETES_MASTER "
+             "environment variable")
+    assert logparse.logged(err, 'Failed to get the default config for the cluster API client. Error: "%s"' % empty,
+                           "warning")
+    assert logparse.logged(err, "Failed to api handle for cluster", "warning")
+    assert logparse.logged(err, 'Failed to collect using the API. Error: "%s" . Falling back to using the CLI.'
+                           % empty, "warning")
+
+
+def test_server_groups_failure_lines(stub_path, monkeypatch, capsys):
+    api = _FakeAPI(stub_path, "--fail", "/apis")
+    try:
+        monkeypatch.setenv("KUBECONFIG", _kubeconfig(stub_path / "kc", {"server": "http://127.0.0.1:%d" % api.port}, {}))
+        _collect_map(stub_path)
+    finally:
+        api.stop()
+    err = capsys.readouterr().err
+    assert logparse.logged(err, "API request for server-group list failed", "error")
+    assert logparse.logged(err, "Failed to retrieve preferred group information from cluster", "warning")
+
+
+def test_kinds_failure_lines(stub_path, monkeypatch, capsys):
+    api = _FakeAPI(stub_path, "--fail", "/apis/apps/v1")
+    try:
+        monkeypatch.setenv("KUBECONFIG", _kubeconfig(stub_path / "kc", {"server": "http://127.0.0.1:%d" % api.port}, {}))
+        _collect_map(stub_path)
+    finally:
+        api.stop()
+    assert logparse.logged(capsys.readouterr().err, "Failed to retrieve <kind, group-version> information from cluster",
+                           "warning")
