@@ -248,7 +248,12 @@ class ClusterCollector(Collector):
         if len(lines) < 2:
             raise ValueError("Description incomplete")
         if "KIND" not in lines[0]:
-            raise ValueError("no KIND")
+            # clustercollector.go:622 returns the command's nil error here: an
+            # explain that starts with another line (newer kubectl prints GROUP
+            # first) gives kind "" and version "" without an error
+            if settings.fixed:
+                raise ValueError("no KIND")
+            return "", ""
         kind = lines[0].split(":")[1].strip()
         group, version = "", ""
         if "VERSION" in lines[1]:
@@ -260,12 +265,18 @@ class ClusterCollector(Collector):
         return kind, _gv_string(group, version)
 
     def is_supported_gv(self, kind, gv):
+        """``isSupportedGV``: (supported, error text)."""
         try:
             out = self._run("explain", kind, "--api-version=" + gv, "--recursive").decode("utf-8", "replace")
-        except (CommandError, OSError):
-            return False
+        except (CommandError, OSError) as e:
+            log.debug("Error while running %s for verifying [%s]\n", self.get_cluster_command(), gv)
+            return False, str(e) if isinstance(e, CommandError) else common.go_exit_status(127)
         lines = out.split("\n")
-        return len(lines) >= 2 and "VERSION" in lines[1]
+        if len(lines) < 2:
+            return False, "Description incomplete"
+        if "VERSION" in lines[1]:
+            return True, None
+        return False, "GV [%s] not found" % gv
 
     def get_preferred_gv_using_cli(self, kind, groups):
         out = []
@@ -273,10 +284,11 @@ class ClusterCollector(Collector):
             prio = scheme.prioritized_versions_for_group(group)
             if prio:
                 for gv in prio:
-                    if self.is_supported_gv(kind, gv):
+                    ok, err = self.is_supported_gv(kind, gv)
+                    if ok:
                         out.append(gv)
                     else:
-                        log.debug("Group version not found by CLI for kind [%s]", kind)
+                        log.debug("Group version not found by CLI for kind [%s] : %s", kind, err)
             else:
                 try:
                     out.append(self.get_gvk_using_name_cli(kind)[1])

@@ -445,3 +445,54 @@ def test_kinds_failure_lines(stub_path, monkeypatch, capsys):
         api.stop()
     assert logparse.logged(capsys.readouterr().err, "Failed to retrieve <kind, group-version> information from cluster",
                            "warning")
+
+
+def _explain_cc(monkeypatch, outputs):
+    """A ClusterCollector whose CLI answers from ``outputs`` (argv tuple ->
+    bytes, or an Exception to raise)."""
+    from move2kube_amd.collector import CommandError
+    cc = ClusterCollector()
+    monkeypatch.setattr(cc, "get_cluster_command", lambda: "kubectl")
+
+    def run(*args, combined=False):
+        out = outputs.get(args, CommandError(["kubectl"] + list(args), 1))
+        if isinstance(out, Exception):
+            raise out
+        return out
+    monkeypatch.setattr(cc, "_run", run)
+    return cc
+
+
+def test_cli_explain_without_a_kind_line_is_kind_empty_in_reference_mode(monkeypatch):
+    """clustercollector.go:616-623: an explain whose first line is not KIND
+    (newer kubectl prints GROUP first) returns the command's nil error, so
+    the kind and version are "" and the map gets an entry for kind ""."""
+    outputs = {("api-resources", "-o", "name"): b"deployments.apps\npods\n",
+               ("explain", "deployments"): b"GROUP:      apps\nKIND:       Deployment\nVERSION:    v1\n",
+               ("explain", "pods"): b"KIND:     Pod\nVERSION:  v1\n"}
+    for gv in ("apps/v1", "apps/v1beta2", "apps/v1beta1"):
+        outputs[("explain", "", "--api-version=" + gv, "--recursive")] = b"KIND: x\n"
+    cc = _explain_cc(monkeypatch, outputs)
+    assert cc.collect_using_cli() == {"": [], "Pod": ["v1"]}
+    settings.compat = "fixed"
+    assert cc.collect_using_cli() == {"Pod": ["v1"]}
+
+
+def test_cli_unsupported_versions_are_debug_lines_with_the_reason(monkeypatch, capsys):
+    from move2kube_amd.utils import log
+    outputs = {("api-resources", "-o", "name"): b"deployments.apps\n",
+               ("explain", "deployments"): b"KIND: Deployment\nVERSION: apps/v1\n",
+               ("explain", "Deployment", "--api-version=apps/v1", "--recursive"): b"KIND: Deployment\nVERSION: v1\n",
+               ("explain", "Deployment", "--api-version=apps/v1beta2", "--recursive"): b"short",
+               ("explain", "Deployment", "--api-version=apps/v1beta1", "--recursive"): b"KIND: x\nFIELDS:\n"}
+    cc = _explain_cc(monkeypatch, outputs)
+    log.set_verbose(True)
+    try:
+        assert cc.collect_using_cli() == {"Deployment": ["apps/v1"]}
+    finally:
+        log.set_verbose(False)
+    err = capsys.readouterr().err
+    assert logparse.logged(err, "Group version not found by CLI for kind [Deployment] : Description incomplete",
+                           "debug")
+    assert logparse.logged(err, "Group version not found by CLI for kind [Deployment] : GV [apps/v1beta1] not found",
+                           "debug")
