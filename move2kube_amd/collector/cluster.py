@@ -137,13 +137,18 @@ class ClusterCollector(Collector):
                 log.warning("Error while fetching storage classes using command [%s get sc -o yaml]",
                             shutil.which(self.get_cluster_command()) or self.get_cluster_command())
             raise
-        doc = yamlio.load(out.decode("utf-8", "replace")) or {}
+        try:
+            doc = yamlio.load(out.decode("utf-8", "replace")) or {}
+        except yamlio.YAMLError as e:
+            log.error("Error in unmarshalling yaml: %s. Skipping.", e)
+            raise
         names = []
-        for sc in doc.get("items") or []:
+        for sc in (doc.get("items") if isinstance(doc, dict) else None) or []:
             if isinstance(sc, dict):
                 names.append(str((sc.get("metadata") or {}).get("name", "")))
             else:
-                log.warning("Unknown type detected in cluster metadata [%s]", type(sc).__name__)
+                # %T of the failed assertion's zero value (clustercollector.go:150-156)
+                log.warning("Unknown type detected in cluster metadata [%s]", "map[string]interface {}")
         return names
 
     # -- discovery API -----------------------------------------------------
@@ -399,7 +404,12 @@ class ClusterCollector(Collector):
     # -- entry point -------------------------------------------------------
     def collect(self, input_path, output_path):
         output_path = os.path.join(output_path, "clusters")
-        os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+        try:
+            os.makedirs(output_path, mode=DEFAULT_DIRECTORY_PERMISSION, exist_ok=True)
+        except OSError as e:
+            err = common.go_path_error(e, "mkdir")
+            log.error("Unable to create output directory at path %r Error: %r", output_path, err)
+            raise RuntimeError(err) from e
         if self.get_cluster_command() == "":
             msg = "No kubectl or oc in path. Add kubectl to path and rerun to collect data about the cluster in context."
             log.warning(msg)

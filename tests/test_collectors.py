@@ -496,3 +496,27 @@ def test_cli_unsupported_versions_are_debug_lines_with_the_reason(monkeypatch, c
                            "debug")
     assert logparse.logged(err, "Group version not found by CLI for kind [Deployment] : GV [apps/v1beta1] not found",
                            "debug")
+
+
+def test_storage_class_output_the_decode_refuses_or_items_of_another_type(monkeypatch, capsys):
+    """clustercollector.go:137-160: a yaml.v3 error is logged and no class is
+    kept; an item that is not a mapping is warned about with %T of the failed
+    assertion's zero value."""
+    cc = _explain_cc(monkeypatch, {("get", "sc", "-o", "yaml"): b"items: [unclosed\n"})
+    import pytest as _pytest
+    with _pytest.raises(Exception):
+        cc.get_storage_classes()
+    assert logparse.logged_containing(capsys.readouterr().err, "Error in unmarshalling yaml: yaml: ", "error")
+    cc = _explain_cc(monkeypatch, {("get", "sc", "-o", "yaml"):
+                                   b"items:\n- metadata: {name: gold}\n- just-a-string\n"})
+    assert cc.get_storage_classes() == ["gold"]
+    assert logparse.logged(capsys.readouterr().err, "Unknown type detected in cluster metadata "
+                           "[map[string]interface {}]", "warning")
+
+
+def test_cluster_output_directory_that_cannot_be_made(tmp_path, capsys):
+    (tmp_path / "clusters").write_text("a file")
+    with pytest.raises(RuntimeError):
+        ClusterCollector().collect("", str(tmp_path))
+    assert logparse.logged(capsys.readouterr().err, 'Unable to create output directory at path "%s" Error: "mkdir %s: '
+                           'not a directory"' % (tmp_path / "clusters", tmp_path / "clusters"), "error")
