@@ -313,7 +313,10 @@ def _match_string(s1, s2):
     rx = m[2]
     if rx is _NOT_COMPILED:
         try:
-            rx = re.compile(_go_regex(s1))
+            import warnings
+            with warnings.catch_warnings():     # "[--" etc.: Python's FutureWarning; RE2 is silent
+                warnings.simplefilter("ignore", FutureWarning)
+                rx = re.compile(_go_regex(s1))
         except re.error as e:
             log.debug("Unable to compile string %s : %s", s1, e)
             rx = None
