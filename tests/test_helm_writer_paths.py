@@ -128,3 +128,26 @@ def test_unsupported_kinds_ignored_and_bad_versions_dropped(capsys):
                                 "&TypeMeta{Kind:Deployment,APIVersion:apps/v1,}", "error")
     assert logparse.logged(err, "Unable to parse group version a/b/c : unexpected GroupVersion string: a/b/c",
                            "error")
+
+
+def test_container_files_that_cannot_be_written(tmp_path, capsys):
+    """transformer.go:60-99: a directory that cannot be made skips its file
+    with an error line; a file that cannot be written is a warning; the
+    scripts are still written."""
+    from move2kube_amd.models import ir as irtypes
+    c = irtypes.new_container("NewDockerfile", "web:1", True)
+    c.add_file("blocked/Dockerfile", "FROM x\n")
+    c.add_file("web/web-docker-build.sh", "docker build .\n")
+    c.add_file("web/taken", "x")
+    out = tmp_path / "out"
+    (out / "containers" / "web" / "taken").mkdir(parents=True)      # the file's path is a directory
+    (out / "containers" / "blocked").write_text("a file where a directory goes")
+    log.set_verbose(False)
+    assert transformer.write_containers([c], str(out), str(tmp_path), "quay.io", "ns") is True
+    err = capsys.readouterr().err
+    assert logparse.logged_containing(err, "Unable to create directory %s : mkdir %s: " % (
+        out / "containers" / "blocked", out / "containers" / "blocked"), "error")
+    assert logparse.logged(err, "Error writing file at %s : open %s: is a directory" % (
+        out / "containers" / "web" / "taken", out / "containers" / "web" / "taken"), "warning")
+    assert (out / "containers" / "web" / "web-docker-build.sh").read_text() == "docker build .\n"
+    assert (out / "buildimages.sh").exists() and (out / "pushimages.sh").exists() and (out / "copysources.sh").exists()
