@@ -30,10 +30,9 @@ SERVICE_KEYS = {
     "read_only", "restart", "secrets", "security_opt", "shm_size", "stdin_open", "stop_grace_period",
     "stop_signal", "sysctls", "tmpfs", "tty", "ulimits", "user", "userns_mode", "volumes", "working_dir",
 }
-FORBIDDEN = {"volume_driver": "use the driver key on a named volume", "volumes_from": "use named volumes",
-             "cpu_quota": "use deploy.resources", "cpu_shares": "use deploy.resources",
-             "cpuset": "use deploy.resources", "mem_limit": "use deploy.resources",
-             "memswap_limit": "use deploy.resources", "extends": "not supported in v3"}
+# docker/cli types.ForbiddenProperties
+FORBIDDEN = ("extends", "volume_driver", "volumes_from", "cpu_quota", "cpu_shares", "cpuset", "mem_limit",
+             "memswap_limit")
 
 
 class ComposeError(ValueError):
@@ -170,8 +169,6 @@ def _validate(d):
         if not isinstance(svc, dict):
             raise ComposeError("services.%s must be a mapping" % sname)
         for k in svc:
-            if k in FORBIDDEN:
-                raise ComposeError("Compose file contains unsupported option: '%s'. %s" % (k, FORBIDDEN[k]))
             if k not in SERVICE_KEYS and not str(k).startswith("x-"):
                 raise ComposeError("services.%s Additional property %s is not allowed" % (sname, k))
     for key in ("networks", "volumes", "secrets", "configs"):
@@ -179,6 +176,15 @@ def _validate(d):
         if v is not None and not isinstance(v, dict):
             raise ComposeError("%s must be a mapping" % key)
     return services
+
+
+def _check_forbidden(d):
+    """docker/cli ``validateForbidden``, before interpolation: a service using
+    one of ``types.ForbiddenProperties`` fails the load."""
+    services = d.get("services")
+    if isinstance(services, dict) and any(isinstance(svc, dict) and any(k in FORBIDDEN for k in svc)
+                                          for svc in services.values()):
+        raise ComposeError("Configuration contains forbidden properties")
 
 
 def _go_repr(k):
@@ -224,14 +230,15 @@ def parse_v3(path):
         raise ComposeError("Top-level object must be a mapping")
     _check_string_keys(parsed, "")
     parsed = remove_non_existent_env_files(path, parsed)
-    version = _version(parsed)
-    if version not in SUPPORTED_V3:
-        raise ComposeError("unsupported Compose file version: %s" % version)
+    version = _version(parsed)      # schema.Version: read before interpolation
+    _check_forbidden(parsed)
     env = cu.get_environment_variables()
     try:
         parsed = interpolate_v3(parsed, env.get)
     except InterpolationError as e:
         raise ComposeError(str(e))
+    if version not in SUPPORTED_V3:   # schema.Validate: no schema for the version
+        raise ComposeError("unsupported Compose file version: %s" % version)
     services = _validate(parsed)
     try:
         cschema.validate_v3(parsed)

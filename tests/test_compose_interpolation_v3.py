@@ -105,3 +105,26 @@ def test_interpolated_numbers_load(tmp_path, monkeypatch):
     q.write_text('version: "3.7"\nservices:\n  web:\n    image: nginx\n    deploy:\n      replicas: "2"\n')
     with pytest.raises(v3.ComposeError, match="replicas must be a integer"):
         v3.parse_v3(str(q))
+
+
+def test_forbidden_properties_fail_before_interpolation(tmp_path):
+    """loader.Load runs validateForbidden before interpolating: its error wins
+    over a malformed ${...} in the same file."""
+    p = tmp_path / "docker-compose.yaml"
+    p.write_text('version: "3"\nservices:\n  web:\n    image: "$"\n    mem_limit: 1g\n')
+    with pytest.raises(v3.ComposeError) as ei:
+        v3.parse_v3(str(p))
+    assert str(ei.value) == ('Unable to load Compose file at path %s Error: "Configuration contains forbidden '
+                             'properties"' % p)
+
+
+def test_version_is_read_before_interpolation_and_checked_after(tmp_path, monkeypatch):
+    monkeypatch.setenv("V", "3.7")
+    p = tmp_path / "docker-compose.yaml"
+    p.write_text('version: "${V}"\nservices:\n  web:\n    image: "$"\n')
+    with pytest.raises(v3.ComposeError) as ei:
+        v3.parse_v3(str(p))
+    assert "invalid interpolation format for services.web.image" in str(ei.value)
+    p.write_text('version: "${V}"\nservices:\n  web:\n    image: nginx\n')
+    with pytest.raises(v3.ComposeError, match=r"unsupported Compose file version: \$\{V\}"):
+        v3.parse_v3(str(p))
