@@ -373,7 +373,11 @@ class K8sTransformer(Transformer):
         opath = os.path.join(basepath, project + "-operator")
         if os.path.exists(opath):
             shutil.rmtree(opath, ignore_errors=True)
-        _mkdir(opath)
+        try:
+            _mkdir(opath)
+        except OSError as e:
+            log.error("Unable to create Operator directory %s : %s", opath, common.go_path_error(e, "mkdir"))
+            return None
         chart = os.path.abspath(os.path.join(basepath, project))
         span = trace.span("operator-sdk init (external tool)", "external")
         span.__enter__()
@@ -385,7 +389,9 @@ class K8sTransformer(Transformer):
         except OSError as e:
             out.close()
             span.__exit__(None, None, None)
-            log.warning("Error during operator creation : %s", e)
+            # cmd.Output() that cannot start: "<err>, <no output>" (k8stransformer.go:243-246)
+            err = "fork/exec %s: %s" % (sdk, common.go_errno_text(e.errno)) if e.errno else str(e)
+            log.warning("Error during operator creation : %s, %s", err, "")
             return None
         return child, out, span
 

@@ -90,7 +90,17 @@ def test_operator_sdk_that_cannot_start(tmp_path, monkeypatch, capsys):
     _sdk(tmp_path, monkeypatch, "")
     (tmp_path / "bin" / "operator-sdk").write_bytes(b"\x7fELF not really")   # exec format error
     assert transformer.K8sTransformer.create_operator("proj", str(tmp_path)) is False
-    assert logparse.logged_containing(capsys.readouterr().err, "Error during operator creation : ", "warning")
+    assert logparse.logged(capsys.readouterr().err, "Error during operator creation : fork/exec %s: exec format "
+                           "error, " % (tmp_path / "bin" / "operator-sdk"), "warning")
+
+
+def test_operator_directory_that_cannot_be_made(tmp_path, monkeypatch, capsys):
+    _sdk(tmp_path, monkeypatch, "exit 0\n")
+    (tmp_path / "proj-operator").mkdir()
+    monkeypatch.setattr(transformer, "_mkdir", lambda p: (_ for _ in ()).throw(PermissionError(13, "x", p)))
+    assert transformer.K8sTransformer.create_operator("proj", str(tmp_path)) is False
+    assert logparse.logged(capsys.readouterr().err, "Unable to create Operator directory %s : mkdir %s: permission "
+                           "denied" % (tmp_path / "proj-operator", tmp_path / "proj-operator"), "error")
 
 
 def _convert(objs, kinds, ignore=False):
