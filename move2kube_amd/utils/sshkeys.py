@@ -45,7 +45,10 @@ def load_known_hosts_of_current_user():
     if _state["known_hosts_loaded"]:
         return
     _state["known_hosts_loaded"] = True
-    path = os.path.join(_home(), ".ssh", "known_hosts")
+    home = _home()
+    log.debug("Home directory: %r", home)
+    path = os.path.join(home, ".ssh", "known_hosts")
+    log.debug("Looking in the known_hosts at path %r for public keys.", path)
     msg = ("The CI/CD pipeline needs access to the git repos in order to clone, build and push.\n"
            "Move2Kube has public keys for github.com, gitlab.com, and bitbucket.org by default.\n"
            "If any of the repos use ssh authentication we will need public keys in order to verify.\n"
@@ -62,6 +65,9 @@ def load_known_hosts_of_current_user():
         return
     for domain, lines in keys.items():
         DOMAIN_TO_PUBLIC_KEYS.setdefault(domain, lines)
+    if log.debug_enabled():   # log.Debug("DomainToPublicKeys:", m): fmt.Sprint, no space after a string
+        from .gotemplate import go_sprint
+        log.debug("%s", "DomainToPublicKeys:" + go_sprint(DOMAIN_TO_PUBLIC_KEYS))
 
 
 def _load_ssh_keys_of_current_user():
@@ -70,8 +76,11 @@ def _load_ssh_keys_of_current_user():
     if _state["keys_loaded"]:
         return
     _state["keys_loaded"] = True
-    d = os.path.join(_home(), ".ssh")
+    home = _home()
+    log.debug("Home directory: %r", home)
+    d = os.path.join(home, ".ssh")
     _state["key_dir"] = d
+    log.debug("Looking in ssh directory at path %r for keys.", d)
     msg = ("The CI/CD pipeline needs access to the git repos in order to clone, build and push.\n"
            "If any of the repos require ssh keys you will need to provide them.\n"
            "Do you want to load the private ssh keys from [%s]?:" % d)

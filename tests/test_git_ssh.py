@@ -496,3 +496,22 @@ def test_native_converter_switches(monkeypatch):
     monkeypatch.setenv("M2K_REQUIRE_NATIVE", "1")
     with pytest.raises(ImportError):
         sshkeys._native()
+
+
+def test_user_key_loading_debug_lines(qa_home, capsys):
+    """sshkeys.go:60-63,97,111-113: the home and the paths looked in, and the
+    merged host keys as log.Debug's fmt.Sprint prints a Go map."""
+    (qa_home / ".ssh" / "known_hosts").write_text("git.corp.example ssh-rsa %s\n" % _keys()["ssh-rsa"])
+    qaengine.add_engine(_Answers({"The CI/CD pipeline needs access": ["true"]}))
+    log.set_verbose(True)
+    try:
+        sshkeys.load_known_hosts_of_current_user()
+        sshkeys._load_ssh_keys_of_current_user()
+    finally:
+        log.set_verbose(False)
+    msgs = [m for lv, m in logparse.messages(capsys.readouterr().err) if lv == "debug"]
+    assert msgs.count('Home directory: "%s"' % qa_home) == 2
+    assert 'Looking in the known_hosts at path "%s" for public keys.' % (qa_home / ".ssh" / "known_hosts") in msgs
+    assert 'Looking in ssh directory at path "%s" for keys.' % (qa_home / ".ssh") in msgs
+    (dump,) = [m for m in msgs if m.startswith("DomainToPublicKeys:")]
+    assert dump.startswith("DomainToPublicKeys:map[") and "git.corp.example:[git.corp.example ssh-rsa " in dump
