@@ -13,103 +13,26 @@ import os
 
 from ..models import collection
 from ..models import plan as plantypes
-from ..utils import common, fastjson, log
+from ..utils import common, gojson, log
 from ..utils.constants import DEFAULT_DIRECTORY_PERMISSION, settings
 from . import Collector, concurrently, run
 
 
-class _Number(str):
-    """A JSON number kept as its literal text (Go reports ``number 1.5``)."""
-
-
 # sourcetypes.CfInstanceApps and the types under it (internal/collector/sourcetypes)
-_CF_TYPES = {
-    "CfInstanceApps": (("resources", "[]sourcetypes.CfResource"),),
-    "CfResource": (("entity", "sourcetypes.CfSourceApplication"),),
-    "CfSourceApplication": (("name", "string"), ("buildpack", "string"), ("detected_buildpack", "string"),
-                            ("memory", "int64"), ("instances", "int"), ("dockerimage", "string"),
-                            ("ports", "[]int32"), ("environment_json", "map[string]string")),
-}
-_INT_BITS = {"int": 64, "int64": 64, "int32": 32}
-
-
-def _json_kind(v):
-    if isinstance(v, _Number):
-        return "number"
-    if isinstance(v, bool):
-        return "bool"
-    return {str: "string", list: "array", dict: "object"}[type(v)]
-
-
-class _Unmarshal:
-    """``json.Unmarshal(output, &sourcetypes.CfInstanceApps{})`` (Go 1.15
-    encoding/json): keys match the field names exactly or case-insensitively,
-    unknown keys are ignored, ``null`` leaves a value as it is, and a type
-    mismatch is an ``UnmarshalTypeError`` naming the innermost struct and the
-    field path; the first one is returned once the whole document has been
-    decoded.  The decoded value is plain dicts/lists/str/int."""
-
-    def __init__(self):
-        self.err = None
-
-    def mismatch(self, value, typ, ctx):
-        if self.err is None:
-            if ctx[0]:
-                self.err = "json: cannot unmarshal %s into Go struct field %s.%s of type %s" % (
-                    value, ctx[0], ".".join(ctx[1]), typ)
-            else:
-                self.err = "json: cannot unmarshal %s into Go value of type %s" % (value, typ)
-
-    def value(self, v, typ, ctx):
-        if v is None:
-            return None
-        if typ.startswith("[]"):
-            if not isinstance(v, list):
-                return self.mismatch(_json_kind(v), typ, ctx)
-            return [self.value(x, typ[2:], ctx) for x in v]
-        if typ == "map[string]string":
-            if not isinstance(v, dict):
-                return self.mismatch(_json_kind(v), typ, ctx)
-            return {k: "" if x is None else self.value(x, "string", ctx) for k, x in v.items()}
-        if typ.startswith("sourcetypes."):
-            return self.struct(v, typ, ctx)
-        if typ == "string":
-            if isinstance(v, str) and not isinstance(v, _Number):
-                return v
-            return self.mismatch(_json_kind(v), typ, ctx)
-        bits = _INT_BITS[typ]
-        if isinstance(v, _Number):
-            digits = v[1:] if v[:1] == "-" else v
-            if digits.isdigit() and digits.isascii() and -(1 << (bits - 1)) <= int(v) < (1 << (bits - 1)):
-                return int(v)
-            return self.mismatch("number " + v, typ, ctx)
-        return self.mismatch(_json_kind(v), typ, ctx)
-
-    def struct(self, v, typ, ctx):
-        if not isinstance(v, dict):
-            return self.mismatch(_json_kind(v), typ, ctx)
-        name = typ.split(".", 1)[1]
-        fields = _CF_TYPES[name]
-        out = {}
-        for key, x in v.items():
-            f = next((f for f in fields if f[0] == key), None) or \
-                next((f for f in fields if f[0] == key.casefold()), None)
-            if f is None:
-                continue
-            got = self.value(x, f[1], (name, ctx[1] + [f[0]]))
-            if x is not None:
-                out[f[0]] = got
-        return out
+_CF_APP = ("struct", "sourcetypes.CfSourceApplication", (
+    ("name", gojson.STRING), ("buildpack", gojson.STRING), ("detected_buildpack", gojson.STRING),
+    ("memory", ("int", "int64", 64)), ("instances", ("int", "int", 64)), ("dockerimage", gojson.STRING),
+    ("ports", ("slice", "[]int32", ("int", "int32", 32))),
+    ("environment_json", ("map", "map[string]string", gojson.STRING))))
+_CF_APPS = ("struct", "sourcetypes.CfInstanceApps", (
+    ("resources", ("slice", "[]sourcetypes.CfResource",
+                   ("struct", "sourcetypes.CfResource", (("entity", _CF_APP),)))),))
 
 
 def decode_cf_apps(output):
     """The entity of every resource of ``cf curl /v2/apps`` output; ValueError
     with encoding/json's text when Go would fail the Unmarshal."""
-    doc = fastjson.loads(output, parse_int=_Number, parse_float=_Number)
-    u = _Unmarshal()
-    res = u.value(doc, "sourcetypes.CfInstanceApps", ("", []))
-    if u.err is not None:
-        raise ValueError(u.err)
+    res = gojson.unmarshal(output, _CF_APPS)
     return [(r or {}).get("entity") or {} for r in (res or {}).get("resources") or []]
 
 

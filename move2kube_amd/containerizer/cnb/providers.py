@@ -16,7 +16,7 @@ import shutil
 import sys
 import threading
 
-from ...utils import common, fastjson, log, proc
+from ...utils import common, fastjson, gojson, log, proc
 from ...utils.constants import settings
 from ...utils.lazyre import LazyModule
 from ...utils.lazyre import lazy as _lazy_re
@@ -36,16 +36,26 @@ CONTAINER_PARALLEL = int(os.environ.get("M2K_CNB_PARALLEL", "4") or 4)
 _lock = threading.Lock()
 
 
+# cnb.order (provider.go:33-48): buildpackRef embeds buildpackInfo
+_ORDER = ("slice", "cnb.order", ("struct", "cnb.orderEntry", (
+    ("group", ("slice", "[]cnb.buildpackRef", ("struct", "cnb.buildpackRef", (
+        ("id", gojson.STRING), ("version", gojson.STRING), ("homepage", gojson.STRING),
+        ("optional", gojson.BOOL))))),)))
+
+
 def get_builders_from_label(label):
+    """``getBuildersFromLabel``: the buildpack ids of the builder's order
+    label, decoded into ``cnb.order`` as json.Unmarshal does."""
     try:
-        order = fastjson.loads(label)
-    except (ValueError, TypeError) as e:
+        order = gojson.unmarshal(label, _ORDER)
+    except ValueError as e:
         log.warning("Unable to read order : %s", e)
         return []
+    log.debug("Builder data :%s", label)
     out = []
     for og in order or []:
         for bp in (og or {}).get("group") or []:
-            out.append(bp.get("id", ""))
+            out.append((bp or {}).get("id", ""))
     return out
 
 
@@ -577,7 +587,14 @@ class ContainerRuntimeProvider:
 
 class PackProvider:
     def is_available(self):
-        return shutil.which("pack") is not None and os.path.exists(DOCKER_SOCK)
+        if shutil.which("pack") is None:
+            log.debug("Unable to find pack : %s", 'exec: "pack": executable file not found in $PATH')
+            return False
+        if not os.path.exists(DOCKER_SOCK):
+            log.debug("Unable to find pack docker socket, ignoring CNB based containerization approach : %s",
+                      "stat %s: no such file or directory" % DOCKER_SOCK)
+            return False
+        return True
 
     def is_builder_supported(self, path, builder):
         if not self.is_available():
@@ -586,11 +603,16 @@ class PackProvider:
                                 stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL)
         try:
             for raw in child.stdout:
-                t = raw.decode("utf-8", "replace")
+                t = raw.decode("utf-8", "replace").rstrip("\r\n")
+                if t.strip() == "":
+                    continue
+                log.debug("%s", t)
                 if "===> ANALYZING" in t:
+                    log.debug("Found compatible cnb for %s", path)
                     child.kill()
                     return True
                 if "No buildpack groups passed detection." in t:
+                    log.debug("No compatible cnb for %s", path)
                     child.kill()
                     return False
         finally:
