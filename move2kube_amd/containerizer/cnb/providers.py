@@ -107,7 +107,9 @@ class DockerAPIProvider:
 
     def _request(self, method, path, body=None, headers=None, timeout=600, raw=False):
         if not self.sock_path or not os.path.exists(self.sock_path):
-            raise ProviderError("docker socket not available")
+            # docker/client's errConnectionFailed
+            raise ProviderError("Cannot connect to the Docker daemon at unix://%s. Is the docker daemon running?"
+                                % (self.sock_path or DOCKER_SOCK))
         conn = _UnixHTTPConnection(self.sock_path, timeout=timeout)
         try:
             hdrs = dict(headers or {})
@@ -160,26 +162,58 @@ class DockerAPIProvider:
         host = {}
         if volsrc and voldest:
             host["Mounts"] = [{"Type": "bind", "Source": volsrc, "Target": voldest, "ReadOnly": True}]
+        # the debug lines of runContainer (dockerapiprovider.go:152-225)
         try:
             resp = self._request("POST", "/containers/create", body=dict(cfg, HostConfig=host))
-        except ProviderError:
-            resp = self._request("POST", "/containers/create", body=cfg)
+        except ProviderError as e:
+            log.debug("Error during container creation : %s", e)
+            try:
+                resp = self._request("POST", "/containers/create", body=cfg)
+            except ProviderError:
+                log.debug("Container creation failed with image %s with no volumes", image)
+                raise
+            log.debug("Container %s created with image %s with no volumes", resp["Id"], image)
             if volsrc and voldest:
-                self._copy_dir(resp["Id"], volsrc, voldest)
+                try:
+                    self._copy_dir(resp["Id"], volsrc, voldest)
+                except ProviderError as e:
+                    log.debug("Container data copy failed for image %s with volume %s:%s : %s", image, volsrc,
+                              voldest, e)
+                    self._remove(resp["Id"])
+                    raise
+                log.debug("Data copied from %s to %s in container %s with image %s", volsrc, voldest, resp["Id"],
+                          image)
         cid = resp["Id"]
+        log.debug("Container %s created with image %s", cid, image)
         try:
-            self._request("POST", "/containers/%s/start" % cid, raw=True)
-            st = self._request("POST", "/containers/%s/wait?condition=not-running" % cid)
-            logs = self._request("GET", "/containers/%s/logs?stdout=1" % cid, raw=True).decode("utf-8", "replace")
+            try:
+                self._request("POST", "/containers/%s/start" % cid, raw=True)
+            except ProviderError as e:
+                log.debug("Error during container startup of container %s : %s", cid, e)
+                raise
+            try:
+                st = self._request("POST", "/containers/%s/wait?condition=not-running" % cid)
+            except ProviderError as e:
+                log.debug("Error during waiting for container : %s", e)
+                raise
             code = (st or {}).get("StatusCode", 0)
+            log.debug("Container exited with status code: %d", code)
+            try:
+                logs = self._request("GET", "/containers/%s/logs?stdout=1" % cid, raw=True).decode("utf-8", "replace")
+            except ProviderError as e:
+                log.debug("Error while getting container logs : %s", e)
+                raise
             if code != 0:
                 raise ProviderError("Container execution terminated with error code : %d" % code)
             return logs
         finally:
-            try:
-                self._request("DELETE", "/containers/%s?force=1" % cid, raw=True)
-            except ProviderError:
-                pass
+            self._remove(cid)
+
+    def _remove(self, cid):
+        try:
+            self._request("DELETE", "/containers/%s?force=1" % cid, raw=True)
+        except ProviderError:
+            pass
 
     def is_sock_accessible(self):
         if self.sock_state is None:

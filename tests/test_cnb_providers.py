@@ -497,3 +497,35 @@ def test_error_tuples_tolerate_a_partly_imported_subprocess(monkeypatch):
     monkeypatch.setitem(sys.modules, "subprocess", types.ModuleType("subprocess"))
     assert providers._chain_errors() == (providers.ProviderError, OSError, ValueError, KeyError)
     assert providers._start_errors() == (OSError,)
+
+
+def test_docker_api_run_container_debug_lines(nobind_dockerd, tmp_path, capsys):
+    """dockerapiprovider.go:152-225: the bind-mounted create fails, the plain
+    one succeeds and the source is copied in, then the container's id, exit
+    status and removal."""
+    import logparse
+    from move2kube_amd.utils import log
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "package.json").write_text("{}")
+    p = providers.DockerAPIProvider()
+    log.set_verbose(True)
+    try:
+        assert p.is_builder_supported(str(app), "gcr.io/buildpacks/builder") is True
+    finally:
+        log.set_verbose(False)
+    msgs = [m for lv, m in logparse.messages(capsys.readouterr().err) if lv == "debug"]
+    assert any(m.startswith("Error during container creation : docker API POST /containers/create") for m in msgs)
+    (created,) = [m for m in msgs if m.endswith("with image gcr.io/buildpacks/builder with no volumes")]
+    cid = created.split()[1]
+    assert "Data copied from %s to /workspace in container %s with image gcr.io/buildpacks/builder" % (app, cid) in msgs
+    assert "Container %s created with image gcr.io/buildpacks/builder" % cid in msgs
+    assert "Container exited with status code: 0" in msgs
+
+
+def test_docker_api_without_a_daemon(monkeypatch, tmp_path):
+    monkeypatch.setenv("DOCKER_HOST", "unix://" + str(tmp_path / "none.sock"))
+    p = providers.DockerAPIProvider()
+    with pytest.raises(providers.ProviderError, match=r"^Cannot connect to the Docker daemon at unix://.*none\.sock\. "
+                                                      r"Is the docker daemon running\?$"):
+        p.run_container("hello-world")
