@@ -679,6 +679,16 @@ class PackProvider:
 # runc + skopeo + umoci
 # ---------------------------------------------------------------------------
 
+# skopeo's inspect.Output (Created is a *time.Time, decoded by its own
+# UnmarshalJSON: not checked here)
+_SKOPEO_INSPECT = ("struct", "inspect.Output", (
+    ("Name", gojson.STRING), ("Tag", gojson.STRING), ("Digest", gojson.STRING),
+    ("RepoTags", ("slice", "[]string", gojson.STRING)), ("DockerVersion", gojson.STRING),
+    ("Labels", ("map", "map[string]string", gojson.STRING)), ("Architecture", gojson.STRING),
+    ("Os", gojson.STRING), ("Layers", ("slice", "[]string", gojson.STRING)),
+    ("Env", ("slice", "[]string", gojson.STRING))))
+
+
 class RuncProvider:
     @staticmethod
     def _paths():
@@ -689,7 +699,12 @@ class RuncProvider:
         return os.path.join(base, "images"), os.path.join(base, "bundles")
 
     def is_available(self):
-        return all(shutil.which(t) for t in ("runc", "skopeo", "umoci"))
+        for tool in ("runc", "skopeo", "umoci"):
+            if shutil.which(tool) is None:
+                log.debug("Unable to find %s, ignoring runc based cnb check : %s", tool,
+                          'exec: "%s": executable file not found in $PATH' % tool)
+                return False
+        return True
 
     def _init(self, builders):
         images, bundles = self._paths()
@@ -716,6 +731,8 @@ class RuncProvider:
         image, _ = common.get_image_name_and_tag(builder)
         cfg_path = os.path.join(bundles, image, "config.json")
         if not os.path.exists(os.path.dirname(cfg_path)):
+            log.debug("Unable to find pack builder oci bundle, ignoring builder : %s",
+                      "stat %s: no such file or directory" % os.path.dirname(cfg_path))
             raise ProviderError("Runc Builder image not available : %s" % builder)
         spec = common.read_json(cfg_path)
         mount = {"destination": "/workspace", "type": "bind", "source": os.path.abspath(path), "options": ["rbind", "ro"]}
@@ -741,16 +758,23 @@ class RuncProvider:
         if not self.is_available():
             raise ProviderError("Runc not supported in this instance")
         out = {}
+        log.debug("Getting data of all builders %s", "[" + " ".join(builders) + "]")
         for b in builders:
-            p = _run(["skopeo", "inspect", "docker://" + b])
+            p = _run(["skopeo", "inspect", "docker://" + b])     # CombinedOutput
+            log.debug("Builder %s data :%s", b, p.stdout.decode("utf-8", "replace"))
             if p.returncode != 0:
+                log.warning("Error while getting supported buildpacks for builder %s : %s", b,
+                            common.go_exit_status(p.returncode))
                 continue
             try:
-                labels = fastjson.loads(p.stdout).get("Labels") or {}
-            except ValueError:
+                labels = (gojson.unmarshal(p.stdout, _SKOPEO_INSPECT) or {}).get("Labels") or {}
+            except ValueError as e:
+                log.warning("Unable to seriablize inspect output for builder %s : %s", b, e)
                 continue
-            if ORDER_LABEL in labels:
-                out[b] = get_builders_from_label(labels[ORDER_LABEL])
+            if ORDER_LABEL not in labels:
+                log.warning("%s missing in builder %s : %s", ORDER_LABEL, b, "%!s(<nil>)")
+                continue
+            out[b] = get_builders_from_label(labels[ORDER_LABEL])
         return out
 
 

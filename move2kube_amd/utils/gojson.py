@@ -1,6 +1,7 @@
 """``json.Unmarshal`` into a typed Go value (Go 1.15 ``encoding/json``), for
 the places the reference decodes a tool's JSON output into its own structs:
-``cf curl /v2/apps`` (``sourcetypes.CfInstanceApps``) and a CNB builder's
+``cf curl /v2/apps`` (``sourcetypes.CfInstanceApps``), ``skopeo inspect``
+(``inspect.Output``) and a CNB builder's
 ``io.buildpacks.builder.metadata`` order label (``cnb.order``).
 
 The syntax check and the scanning are :mod:`fastjson`'s; this module walks
@@ -92,8 +93,10 @@ class _Decoder:
             return self.mismatch(_kind(v), gotype, ctx)
         out = {}
         for key, x in v.items():
-            f = next((f for f in fields if f[0] == key), None) or \
-                next((f for f in fields if f[0] == key.casefold()), None)
+            f = next((f for f in fields if f[0] == key), None)
+            if f is None:
+                folded = key.casefold()
+                f = next((f for f in fields if f[0].casefold() == folded), None)
             if f is None:
                 continue
             got = self.value(x, f[1], (_short(gotype), ctx[1] + [f[0]]))

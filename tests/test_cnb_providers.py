@@ -529,3 +529,33 @@ def test_docker_api_without_a_daemon(monkeypatch, tmp_path):
     with pytest.raises(providers.ProviderError, match=r"^Cannot connect to the Docker daemon at unix://.*none\.sock\. "
                                                       r"Is the docker daemon running\?$"):
         p.run_container("hello-world")
+
+
+def test_runc_provider_log_lines(runc_env, monkeypatch, tmp_path, capsys):
+    """runcprovider.go:45-99: the builders' data, a failed inspect, a missing
+    order label (logged with the nil error), and the tools looked for."""
+    import logparse
+    from move2kube_amd.utils import log
+    p = providers.RuncProvider()
+    log.set_verbose(True)
+    try:
+        p.get_all_buildpacks(["b:latest", "missing/image:1"])
+        monkeypatch.setattr(providers, "_run", lambda cmd, timeout=600: __import__("subprocess").CompletedProcess(
+            cmd, 0, b'{"Name": "x", "Labels": {"other": "y"}}'))
+        assert p.get_all_buildpacks(["nolabel:1"]) == {}
+        monkeypatch.setattr(providers, "_run", lambda cmd, timeout=600: __import__("subprocess").CompletedProcess(
+            cmd, 0, b'{"Labels": {"a": 1}}'))
+        assert p.get_all_buildpacks(["badlabels:1"]) == {}
+        monkeypatch.setenv("PATH", str(tmp_path))
+        assert not p.is_available()
+    finally:
+        log.set_verbose(False)
+    err = capsys.readouterr().err
+    assert logparse.logged(err, "Getting data of all builders [b:latest missing/image:1]", "debug")
+    assert logparse.logged(err, "Error while getting supported buildpacks for builder missing/image:1 : exit status 1",
+                           "warning")
+    assert logparse.logged(err, "%s missing in builder nolabel:1 : %%!s(<nil>)" % providers.ORDER_LABEL, "warning")
+    assert logparse.logged(err, "Unable to seriablize inspect output for builder badlabels:1 : json: cannot unmarshal "
+                                "number into Go struct field Output.Labels of type string", "warning")
+    assert logparse.logged(err, 'Unable to find runc, ignoring runc based cnb check : exec: "runc": executable file '
+                                'not found in $PATH', "debug")
