@@ -230,10 +230,17 @@ def yaml_attr_present(path, attr):
 
 
 def write_yaml(output_path, data, sort_maps=False):
-    """Write ``data`` (a plain structure or an object with ``to_yaml()``) like go-yaml v3."""
+    """Write ``data`` (a plain structure or an object with ``to_yaml()``) like
+    go-yaml v3; a write error is logged as ``common.WriteYaml`` logs it
+    (utils.go:159-176) and raised for the caller's own line."""
     if hasattr(data, "to_yaml"):
         data = data.to_yaml()
-    write_text(output_path, yamlio.dump(data, sort_maps=sort_maps))
+    text = yamlio.dump(data, sort_maps=sort_maps)
+    try:
+        write_text(output_path, text)
+    except OSError as e:
+        log.error("Error writing yaml to file. error: %s,  outputPath %s", go_path_error(e, "open"), output_path)
+        raise
 
 
 def read_yaml(path):

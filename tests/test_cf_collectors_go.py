@@ -158,3 +158,17 @@ def test_container_types_output_directory_failure(tmp_path, monkeypatch, capsys)
         cfc.CFContainerTypesCollector().collect(str(tmp_path / "src"), str(tmp_path / "out"))
     assert logparse.logged(capsys.readouterr().err, "Unable to create output path %s : mkdir %s: not a directory"
                            % (tmp_path / "out" / "cf", tmp_path / "out" / "cf"), "error")
+
+
+def test_write_failures_are_logged_by_write_yaml_too(cf_stub, tmp_path, capsys):
+    """common.WriteYaml logs its own error line before the caller's."""
+    cf_stub.setenv("CF_CURL", '{"resources": [{"entity": {"name": "a"}}]}')
+    from move2kube_amd.utils import common
+    target = tmp_path / "out" / "cf" / (common.normalize_for_filename("instanceapps_a") + ".yaml")
+    target.mkdir(parents=True)
+    with pytest.raises(RuntimeError):
+        cfc.CfAppsCollector().collect("", str(tmp_path / "out"))
+    msgs = logparse.messages(capsys.readouterr().err)
+    assert msgs == [("error", "Error writing yaml to file. error: open %s: is a directory,  outputPath %s"
+                     % (target, target)),
+                    ("error", "Unable to write collect output : open %s: is a directory" % target)]
