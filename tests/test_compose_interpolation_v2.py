@@ -117,3 +117,20 @@ def test_dotenv_lookup_takes_the_first_line_naming_the_key(tmp_path, monkeypatch
     p = tmp_path / "docker-compose.yml"
     p.write_text('version: "2"\nservices:\n  web:\n    image: "nginx:${TAG}"\n')
     assert v1v2.parse_v2(str(p))["services"][0]["image"] == "nginx:one"
+
+
+def test_scanner_never_crashes_or_hangs():
+    """Any value: a string or an InterpolationError, never another exception
+    or a loop (libcompose itself panics or rescans on some of these)."""
+    from hypothesis import given, settings as hsettings, strategies as st
+    alphabet = st.sampled_from(list("$${}:-?AB_1 x"))
+
+    @hsettings(max_examples=400, deadline=None)
+    @given(st.lists(alphabet, max_size=14).map("".join))
+    def check(value):
+        try:
+            out = _run(value, env={"A": "a", "B": ""})
+        except InterpolationError:
+            return
+        assert isinstance(out, str)
+    check()

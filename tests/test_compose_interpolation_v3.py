@@ -128,3 +128,15 @@ def test_version_is_read_before_interpolation_and_checked_after(tmp_path, monkey
     p.write_text('version: "${V}"\nservices:\n  web:\n    image: nginx\n')
     with pytest.raises(v3.ComposeError, match=r"unsupported Compose file version: \$\{V\}"):
         v3.parse_v3(str(p))
+
+
+def test_substitute_never_crashes():
+    from hypothesis import given, settings as hsettings, strategies as st
+    alphabet = st.sampled_from(list("$${}:-?AB_1 x"))
+
+    @hsettings(max_examples=400, deadline=None)
+    @given(st.lists(alphabet, max_size=14).map("".join))
+    def check(value):
+        out, err = substitute_v3(value, ENV.get)
+        assert isinstance(out, str) and (err is None or isinstance(err.template, str))
+    check()
