@@ -80,7 +80,8 @@ _FUZZ_INNER = ["target", "published", "source", "type", "mode", "resources", "li
                "replicas", "test", "interval", "disable", "external", "name", "driver", "file", "read_only",
                "size", "protocol", "x-a"]
 _FUZZ_SCALARS = [None, True, False, 0, 1, -5, 80, 1.5, "", "x", "80:80", "1g", "a=b", "/tmp:/x:ro",
-                 "8080-8081:80-81", "udp", "10s", "${X}", "$$", "CMD-SHELL", "127.0.0.1:5000:5000/udp"]
+                 "8080-8081:80-81", "udp", "10s", "${X}", "$$", "CMD-SHELL", "127.0.0.1:5000:5000/udp",
+                 "${N:-3}", "${B:-yes}", "${F:-0.5}", "$", "${X:?needed}", "${X-a}b", "$1"]
 
 
 def _fuzz_value(rng, depth=0):
@@ -103,7 +104,7 @@ def test_compose_loaders_never_crash(tmp_path):
     plan = plantypes.new_plan()
     plan.root_dir = str(tmp_path)
     loaded = 0
-    for _ in range(250):
+    for _ in range(400):
         svc = {rng.choice(_FUZZ_KEYS): _fuzz_value(rng) for _ in range(rng.randint(1, 6))}
         doc = {"version": rng.choice(["3", "3.7", "2", "2.1"]), "services": {"s": svc}}
         for key in ("volumes", "networks", "secrets"):
