@@ -174,12 +174,11 @@ class RegistryCustomizer:
                     # to; only now is it referenced from imagePullSecrets
                     secret_name = IMAGE_PULL_SECRET_PREFIX + common.make_file_name_compliant(registry)
                     pull_secrets[registry] = secret_name
-                    import json
-                    content = json.dumps({"auths": {registry: entry}}, indent="\t").encode()
+                    content = fastjson.go_marshal_indent({"auths": {registry: entry}}, "\t")
                 else:
                     secret_name = pull_secrets.get(registry, "")
-                    import json
-                    content = json.dumps({"auths": {ir.kubernetes.registry_url: entry}}, indent="\t").encode()
+                    # configfile.SaveToWriter: json.MarshalIndent(configFile, "", "\t")
+                    content = fastjson.go_marshal_indent({"auths": {ir.kubernetes.registry_url: entry}}, "\t")
                 ir.add_storage(irtypes.Storage(name=secret_name, storage_type=irtypes.PULL_SECRET_KIND,
                                                content={".dockerconfigjson": content}))
         ir.values.registry_namespace = ir.kubernetes.registry_namespace
@@ -314,6 +313,13 @@ class IngressCustomizer:
         return host, secret
 
 
+def _go_type(x):
+    """``%T`` of the reference's value: ``*customizer.<type>``, the Go type name being
+    the class name with its first letter lowered."""
+    n = type(x).__name__
+    return "*customizer." + n[:1].lower() + n[1:]
+
+
 def get_customizers():
     return [RegistryCustomizer(), StorageCustomizer(), IngressCustomizer()]
 
@@ -321,15 +327,15 @@ def get_customizers():
 def customize(ir):
     log.info("Begin Customization")
     for c in get_customizers():
-        log.debug("[%s] Begin Customization", type(c).__name__)
+        log.debug("[%s] Begin Customization", _go_type(c))
         try:
             with trace.span(type(c).__name__, "customizer"):
                 c.customize(ir)
         except Exception as e:  # noqa: BLE001
             if isinstance(e, log.FatalError):
                 raise
-            log.warning("[%s] Failed : %s", type(c).__name__, e)
+            log.warning("[%s] Failed : %s", _go_type(c), e)
         else:
-            log.debug("[%s] Done", type(c).__name__)
+            log.debug("[%s] Done", _go_type(c))
     log.info("Customization done")
     return ir

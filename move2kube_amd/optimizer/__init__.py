@@ -163,6 +163,13 @@ class PortMergeOptimizer:
         return out
 
 
+def _go_type(x):
+    """``%T`` of the reference's value: ``*optimize.<type>``, the Go type name being
+    the class name with its first letter lowered."""
+    n = type(x).__name__
+    return "*optimize." + n[:1].lower() + n[1:]
+
+
 def get_optimizers():
     return [NormalizeCharacterOptimizer(), IngressOptimizer(), ReplicaOptimizer(), ImagePullPolicyOptimizer(),
             PortMergeOptimizer()]
@@ -171,15 +178,15 @@ def get_optimizers():
 def optimize(ir):
     log.info("Begin Optimization")
     for o in get_optimizers():
-        log.debug("[%s] Begin Optimization", type(o).__name__)
+        log.debug("[%s] Begin Optimization", _go_type(o))
         try:
             with trace.span(type(o).__name__, "optimizer"):
                 ir = o.optimize(ir)
         except Exception as e:  # noqa: BLE001
             if isinstance(e, log.FatalError):
                 raise
-            log.warning("[%s] Failed : %s", type(o).__name__, e)
+            log.warning("[%s] Failed : %s", _go_type(o), e)
         else:
-            log.debug("[%s] Done", type(o).__name__)
+            log.debug("[%s] Done", _go_type(o))
     log.info("Optimization done")
     return ir

@@ -64,6 +64,13 @@ class IngressParameterizer:
         ir.target_cluster_spec.host = "{{ .Release.Name }}-{{ .Values.ingresshost }}"
 
 
+def _go_type(x):
+    """``%T`` of the reference's value: ``*parameterize.<type>``, the Go type name being
+    the class name with its first letter lowered."""
+    n = type(x).__name__
+    return "*parameterize." + n[:1].lower() + n[1:]
+
+
 def get_parameterizers():
     return [ImageNameParameterizer(), StorageClassParameterizer(), IngressParameterizer()]
 
@@ -71,13 +78,13 @@ def get_parameterizers():
 def parameterize(ir):
     log.info("Begin Parameterization")
     for p in get_parameterizers():
-        log.debug("[%s] Begin Parameterization", type(p).__name__)
+        log.debug("[%s] Begin Parameterization", _go_type(p))
         try:
             with trace.span(type(p).__name__, "parameterizer"):
                 p.parameterize(ir)
         except Exception as e:  # noqa: BLE001
-            log.warning("[%s] Failed : %s", type(p).__name__, e)
+            log.warning("[%s] Failed : %s", _go_type(p), e)
         else:
-            log.debug("[%s] Done", type(p).__name__)
+            log.debug("[%s] Done", _go_type(p))
     log.info("Parameterization done")
     return ir

@@ -28,6 +28,7 @@ class SchemaError(ValueError):
 #  ("list", item)                                   array of item
 #  ("map", value)                                   mapping with any keys
 #  ("obj", {key: spec})                             mapping, known keys typed
+#  ("format", "duration")                           a string time.ParseDuration takes
 
 STR, INT, NUM, BOOL, NULL = "string", "integer", "number", "boolean", "null"
 
@@ -53,19 +54,24 @@ STR_OR_LIST = _or(STR, LIST_OF_STR)
 LIST_OR_DICT = _or(_map(_or(STR, NUM, BOOL, NULL)), LIST_OF_STR)
 STR_OR_NUM = _or(STR, NUM)
 EXTERNAL = _or(BOOL, _obj(name=STR))
+# docker/cli schema.go registers a "duration" format checker (time.ParseDuration);
+# the 3.x schemas put it on every duration-typed string
+DURATION = ("format", "duration")
 
 _BUILD = _or(STR, _obj(context=STR, dockerfile=STR, args=LIST_OR_DICT, labels=LIST_OR_DICT,
                        cache_from=LIST_OF_STR, network=STR, target=STR, shm_size=STR_OR_NUM,
                        extra_hosts=LIST_OR_DICT, isolation=STR))
 _FILE_REF = _list(_or(STR, _obj(source=STR, target=STR, uid=STR, gid=STR, mode=NUM)))
 _RESOURCE = _obj(cpus=STR_OR_NUM, memory=STR_OR_NUM, generic_resources=_list(_map(_or(STR, NUM, _map(_or(STR, NUM))))))
-_UPDATE = _obj(parallelism=INT, delay=STR, failure_action=STR, monitor=STR, max_failure_ratio=NUM, order=STR)
+_UPDATE = _obj(parallelism=INT, delay=DURATION, failure_action=STR, monitor=DURATION, max_failure_ratio=NUM, order=STR)
 _DEPLOY = _obj(
     mode=STR, endpoint_mode=STR, replicas=INT, labels=LIST_OR_DICT, rollback_config=_UPDATE, update_config=_UPDATE,
     resources=_obj(limits=_RESOURCE, reservations=_RESOURCE),
-    restart_policy=_obj(condition=STR, delay=STR, max_attempts=INT, window=STR),
+    restart_policy=_obj(condition=STR, delay=DURATION, max_attempts=INT, window=DURATION),
     placement=_obj(constraints=LIST_OF_STR, preferences=_list(_obj(spread=STR)), max_replicas_per_node=INT))
 _HEALTHCHECK = _obj(disable=BOOL, interval=STR, retries=NUM, test=STR_OR_LIST, timeout=STR, start_period=STR)
+_V3_HEALTHCHECK = _obj(disable=BOOL, interval=DURATION, retries=NUM, test=STR_OR_LIST, timeout=DURATION,
+                       start_period=DURATION)
 _PORTS = _list(_or(NUM, STR, _obj(mode=STR, host_ip=STR, target=INT, published=_or(STR, INT), protocol=STR)))
 _VOLUMES = _list(_or(STR, _obj(type=STR, source=STR, target=STR, read_only=BOOL, consistency=STR,
                               bind=_obj(propagation=STR), volume=_obj(nocopy=BOOL),
@@ -87,8 +93,8 @@ _COMMON_SERVICE = dict(
 
 V3_SERVICE = _obj(**dict(
     _COMMON_SERVICE, configs=_FILE_REF, secrets=_FILE_REF, credential_spec=_obj(file=STR, registry=STR, config=STR),
-    depends_on=LIST_OF_STR, deploy=_DEPLOY, init=BOOL, isolation=STR, stop_grace_period=STR,
-    sysctls=LIST_OR_DICT, userns_mode=STR))
+    depends_on=LIST_OF_STR, deploy=_DEPLOY, init=BOOL, isolation=STR, stop_grace_period=DURATION,
+    sysctls=LIST_OR_DICT, userns_mode=STR, healthcheck=_V3_HEALTHCHECK))
 
 _TOP_VOLUME = _or(NULL, _obj(name=STR, driver=STR, driver_opts=_map(STR_OR_NUM), external=EXTERNAL,
                              labels=LIST_OR_DICT))
@@ -117,6 +123,8 @@ def _human(t):
 
 
 def _type_name(spec):
+    if spec == DURATION:
+        return STR
     if isinstance(spec, str):
         return spec
     if spec[0] == "or":
@@ -147,6 +155,8 @@ def _matches_scalar(v, t):
 
 def _shape_ok(v, spec):
     """Does ``v`` have the outer shape of ``spec`` (used to pick an alternative)."""
+    if spec == DURATION:
+        return isinstance(v, str)
     if isinstance(spec, str):
         return _matches_scalar(v, spec)
     kind = spec[0]
@@ -159,6 +169,15 @@ def _shape_ok(v, spec):
 
 def check(v, spec, path):
     """Raise SchemaError naming the first value whose type does not fit ``spec``."""
+    if spec == DURATION:
+        if not isinstance(v, str):
+            raise SchemaError("%s must be a string" % path)
+        from .utils import parse_duration
+        try:
+            parse_duration(v)
+        except ValueError:
+            raise SchemaError("%s Does not match format 'duration'" % path) from None
+        return
     if isinstance(spec, str):
         if not _matches_scalar(v, spec):
             raise SchemaError("%s must be a %s" % (path, _human(spec)))

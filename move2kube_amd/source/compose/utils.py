@@ -121,19 +121,24 @@ def parse_duration(s):
 
 
 _BRACKETED_HOST_RE = _lazy_re(r"^\[([^\]]+)\]:(.*)$")
-_RAM_RE = _lazy_re(r"^(\d+(?:\.\d+)*) ?([kKmMgGtTpP])?[iI]?[bB]?$")
+_RAM_RE = _lazy_re(r"^([0-9]+(?:\.[0-9]+)*) ?([kKmMgGtTpP])?[iI]?[bB]?\Z")
 _RAM_MULT = {"k": 1024, "m": 1024 ** 2, "g": 1024 ** 3, "t": 1024 ** 4, "p": 1024 ** 5}
 
 
 def ram_in_bytes(v):
-    """docker/go-units ``RAMInBytes`` (binary multipliers); ints pass through."""
+    """docker/go-units v0.4.0 ``RAMInBytes`` (binary multipliers; RE2's
+    ``\\d`` and ``$``: ASCII digits, end of text); ints pass through.  Errors
+    are ``invalid size: '<s>'`` and ParseFloat's for ``1.2.3``."""
     if isinstance(v, bool):
         raise ValueError("invalid size")
     if isinstance(v, (int, float)):
         return int(v)
-    m = _RAM_RE.match(str(v).strip())
+    v = str(v)
+    m = _RAM_RE.match(v)
     if not m:
-        raise ValueError("invalid size: %r" % v)
+        raise ValueError("invalid size: '%s'" % v)
+    if m.group(1).count(".") > 1:
+        raise ValueError('strconv.ParseFloat: parsing "%s": invalid syntax' % m.group(1))
     num = float(m.group(1))
     unit = (m.group(2) or "").lower()
     return int(num * _RAM_MULT.get(unit, 1))
@@ -183,91 +188,241 @@ def shell_split(s):
 
 
 # ---------------------------------------------------------------------------
-# port specs (docker/go-connections nat.ParsePortSpec)
+# port specs: docker/cli ``toServicePortConfigs`` over go-connections'
+# ``nat.ParsePortSpecs`` and ``opts.ConvertPortToPortConfig``
 # ---------------------------------------------------------------------------
 
-def _port_range(s):
-    if "-" in s:
-        a, b = s.split("-", 1)
-        a, b = int(a), int(b)
-        if b < a:
-            raise ValueError("invalid range")
-        return list(range(a, b + 1))
-    return [int(s)]
+def _parse_uint16(s):
+    """``strconv.ParseUint(s, 10, 16)``; None when it fails."""
+    if not s or not s.isascii() or not s.isdigit():
+        return None
+    v = int(s)
+    return v if v <= 0xFFFF else None
+
+
+def _parse_port_range(ports):
+    """``nat.ParsePortRange``: (start, end), or None on any error (the
+    callers replace the error with their own text)."""
+    if not ports:
+        return None
+    if "-" not in ports:
+        v = _parse_uint16(ports)
+        return None if v is None else (v, v)
+    parts = ports.split("-")
+    a, b = _parse_uint16(parts[0]), _parse_uint16(parts[1])
+    if a is None or b is None or b < a:
+        return None
+    return a, b
+
+
+def _split_host_port(hostport):
+    """``net.SplitHostPort`` (Go 1.15): (host, port), or raises ValueError
+    with the ``*net.AddrError`` text."""
+    def err(why):
+        return ValueError("address %s: %s" % (hostport, why) if hostport else why)
+    i = hostport.rfind(":")
+    if i < 0:
+        raise err("missing port in address")
+    j = k = 0
+    if hostport[:1] == "[":
+        end = hostport.find("]")
+        if end < 0:
+            raise err("missing ']' in address")
+        if end + 1 == len(hostport):
+            raise err("missing port in address")
+        if end + 1 != i:
+            raise err("too many colons in address" if hostport[end + 1] == ":" else "missing port in address")
+        host = hostport[1:end]
+        j, k = 1, end + 1
+    else:
+        host = hostport[:i]
+        if ":" in host:
+            raise err("too many colons in address")
+    if "[" in hostport[j:]:
+        raise err("unexpected '[' in address")
+    if "]" in hostport[k:]:
+        raise err("unexpected ']' in address")
+    return host, hostport[i + 1:]
+
+
+def _go_parse_ipv4(s):
+    for i in range(4):
+        if not s:
+            return False
+        if i:
+            if s[0] != ".":
+                return False
+            s = s[1:]
+        n = 0
+        c = 0
+        while c < len(s) and "0" <= s[c] <= "9":
+            n = min(n * 10 + ord(s[c]) - 48, 0xFFFFFF)
+            c += 1
+        if c == 0 or n > 0xFF:
+            return False
+        s = s[c:]
+    return not s
+
+
+def go_parse_ip_ok(s):
+    """Is ``net.ParseIP(s)`` (Go 1.15) non-nil: dotted IPv4 (leading zeros
+    allowed) or IPv6 without a zone."""
+    for ch in s:
+        if ch == ".":
+            return _go_parse_ipv4(s)
+        if ch == ":":
+            if "%" in s:
+                return False
+            import ipaddress
+            try:
+                ipaddress.IPv6Address(s)
+            except ValueError:
+                return False
+            return True
+    return False
 
 
 def parse_port_spec(raw):
-    """Returns [(host_ip, published, target, proto)]; published 0 when unset."""
-    spec = str(raw)
-    proto = "tcp"
-    if "/" in spec:
-        spec, proto = spec.rsplit("/", 1)
-        proto = proto.lower() or "tcp"
-    parts = spec.rsplit(":", 2) if spec.count(":") <= 2 else None
-    if parts is None:
-        # IPv6 host ip in brackets
-        m = _BRACKETED_HOST_RE.match(spec)
-        if not m:
-            raise ValueError("Invalid port spec %r" % raw)
-        rest = m.group(2).split(":")
-        parts = [m.group(1)] + rest
-    host_ip, host_port, cont = "", "", ""
-    if len(parts) == 1:
-        cont = parts[0]
-    elif len(parts) == 2:
-        host_port, cont = parts
+    """``nat.ParsePortSpec``: [(host_ip, host_port, container_port, proto)]
+    with the host port a string ("", a number, or a range when one container
+    port takes a host range); ValueError with go-connections' text."""
+    parts = raw.split(":")
+    n = len(parts)
+    if n == 1:
+        raw_ip, host_port, cport = "", "", parts[0]
+    elif n == 2:
+        raw_ip, host_port, cport = "", parts[0], parts[1]
+    elif n == 3:
+        raw_ip, host_port, cport = parts
     else:
-        host_ip, host_port, cont = parts
-    if not cont:
-        raise ValueError("No port specified: %r" % raw)
-    cports = _port_range(cont)
-    hports = _port_range(host_port) if host_port else []
+        raw_ip, host_port, cport = ":".join(parts[:n - 2]), parts[n - 2], parts[n - 1]
+    # SplitProtoPort
+    pp = cport.split("/")
+    if not cport or not pp[0]:
+        proto, cport = "", ""
+    elif len(pp) == 1:
+        proto = "tcp"
+    elif not pp[1]:
+        proto, cport = "tcp", pp[0]
+    else:
+        proto, cport = pp[1], pp[0]
+    try:
+        ip, _ = _split_host_port(raw_ip + ":")
+    except ValueError as e:
+        raise ValueError("Invalid ip address %s: %s" % (raw_ip, e))
+    if ip and not go_parse_ip_ok(ip):
+        raise ValueError("Invalid ip address: %s" % ip)
+    if cport == "":
+        raise ValueError("No port specified: %s<empty>" % raw)
+    cr = _parse_port_range(cport)
+    if cr is None:
+        raise ValueError("Invalid containerPort: %s" % cport)
+    start, end = cr
+    hstart = hend = 0
+    if host_port:
+        hr = _parse_port_range(host_port)
+        if hr is None:
+            raise ValueError("Invalid hostPort: %s" % host_port)
+        hstart, hend = hr
+    if host_port and end - start != hend - hstart and end != start:
+        raise ValueError("Invalid ranges specified for container and host Ports: %s and %s" % (cport, host_port))
+    if proto.lower() not in ("tcp", "udp", "sctp"):
+        raise ValueError("Invalid proto: %s" % proto)
     out = []
-    if hports and len(hports) != len(cports):
-        if len(hports) > 1:
-            raise ValueError("Invalid ranges specified for container and host Ports: %r" % raw)
-        # single host port range start for a container range -> docker picks a port
-        hports = hports * len(cports)
-    for i, c in enumerate(cports):
-        out.append((host_ip, hports[i] if hports else 0, c, proto))
+    for i in range(end - start + 1):
+        if host_port:
+            host_port = str(hstart + i)
+        if start == end and hstart != hend:
+            host_port = "%s-%d" % (host_port, hend)
+        out.append((ip, host_port, start + i, proto.lower()))
+    return out
+
+
+def to_service_port_configs(value):
+    """docker/cli ``toServicePortConfigs``: one short-syntax entry ->
+    [(target, published, protocol, mode)], its ports in the string order of
+    their ``nat.Port`` keys ("10/tcp" before "9/tcp"), a host port range
+    expanded into one config per host port, and the warning
+    ``ConvertPortToPortConfig`` logs for a host IP other than 0.0.0.0."""
+    bindings = {}
+    for ip, host_port, cport, proto in parse_port_spec(value):
+        bindings.setdefault("%d/%s" % (cport, proto), []).append((ip, host_port))
+    out = []
+    for key in sorted(bindings):
+        cport, proto = key.split("/")
+        for ip, host_port in bindings[key]:
+            if ip and ip != "0.0.0.0":
+                log.warning("ignoring IP-address (%s:%s:%s) service will listen on '0.0.0.0'", ip, host_port, key)
+            r = _parse_port_range(host_port) or (0, 0)
+            for published in range(r[0], r[1] + 1):
+                out.append((int(cport), published, proto, "ingress"))
     return out
 
 
 # ---------------------------------------------------------------------------
-# volume specs
+# volume specs: docker/cli ``loader.ParseVolume`` (cli/compose/loader/volume.go)
 # ---------------------------------------------------------------------------
 
-def parse_volume_v3(spec):
-    """docker/cli ``loader.ParseVolume`` for Linux hosts.
+def _is_windows_drive(buf, ch):
+    return ch == ":" and len(buf) == 1 and buf[0].isalpha()
 
-    Returns dict(type, source, target, read_only)."""
+
+def _is_file_path(source):
+    if source[0] in "./~" or source.startswith("\\\\"):
+        return True
+    return len(source) > 1 and _is_windows_drive(source[0], source[1])
+
+
+def parse_volume_v3(spec):
+    """Short volume syntax -> dict(type, source, target, read_only); ValueError
+    with docker/cli's text.  A one-letter first section followed by ``:`` is
+    a Windows drive (``c:/data:/data``), so ``v:/data`` is an anonymous
+    volume whose target is ``v:/data``; a section after ``source:target`` is
+    the options (``ro``/``rw``; others ignored) and one more is too many."""
     spec = str(spec)
-    parts = spec.split(":")
     vol = {"type": "volume", "source": "", "target": "", "read_only": False}
-    if len(parts) == 1:
-        vol["target"] = parts[0]
-    else:
-        vol["source"] = parts[0]
-        vol["target"] = parts[1]
-        if len(parts) >= 3:
-            for opt in parts[2].split(","):
-                if opt == "ro":
-                    vol["read_only"] = True
-                elif opt == "rw":
-                    vol["read_only"] = False
+    if not spec:
+        raise ValueError("invalid empty volume spec")
+    if len(spec) <= 2:
+        vol["target"] = spec
+        return vol
+    buf = ""
+    for ch in spec + "\0":
+        if _is_windows_drive(buf, ch):
+            buf += ch
+        elif ch in (":", "\0"):
+            err = None
+            if not buf:
+                err = "empty section between colons"
+            elif vol["source"] == "" and ch == "\0":
+                vol["target"] = buf
+            elif vol["source"] == "":
+                vol["source"] = buf
+            elif vol["target"] == "":
+                vol["target"] = buf
+            elif ch == ":":
+                err = "too many colons"
+            else:
+                for opt in buf.split(","):
+                    if opt == "ro":
+                        vol["read_only"] = True
+                    elif opt == "rw":
+                        vol["read_only"] = False
+            if err:
+                raise ValueError("invalid spec: %s: %s" % (spec, err))
+            buf = ""
+        else:
+            buf += ch
     src = vol["source"]
-    if src and (src[0] in "./~"):
-        vol["type"] = "bind"
+    vol["type"] = "bind" if src and _is_file_path(src) else "volume"
     return vol
 
 
-def resolve_bind_source(src, working_dir):
-    if src.startswith("~"):
-        home = os.path.expanduser("~")
-        src = home + src[1:]
-    if not os.path.isabs(src):
-        src = os.path.normpath(os.path.join(working_dir, src))
-    return src
+def go_abs_path(working_dir, p):
+    """docker/cli loader ``absPath``: ``filepath.Join`` unless already absolute."""
+    if os.path.isabs(p):
+        return p
+    return os.path.normpath(os.path.join(working_dir, p)) if (working_dir or p) else ""
 
 
 def duration_seconds(d):
@@ -285,39 +440,39 @@ def command_memo(name, error_type, wrap, state=None):
     ``--ignoreenv``, none of which change within a command.  A parse error
     (``error_type``) is worded with ``wrap % (path, %q of the cause)``,
     remembered, and logged at debug level on every call as the reference's
-    parser does.  ``state`` (snapshot/restore) is command-wide state the
-    parse reads and writes: the memo keys on it and replays its effect."""
+    parser does; so are the lines the parse itself logs.  ``state``
+    (snapshot/restore) is command-wide state the parse reads and writes: the
+    memo keys on it and replays its effect."""
     from ...utils.log import go_quote
 
     def deco(fn):
         def checked(path):
-            try:
-                return fn(path)
-            except RecursionError:  # nested too deeply for the recursive walks: this file only
-                raise error_type(wrap % (path, go_quote("document nested too deeply"))) from None
-            except error_type as e:
-                raise error_type(wrap % (path, go_quote(str(e)))) from None
+            """(ok, result or error, log lines the parse wrote)."""
+            with log.hold() as held:
+                try:
+                    return True, fn(path), held.lines
+                except RecursionError:  # nested too deeply for the recursive walks: this file only
+                    err = error_type(wrap % (path, go_quote("document nested too deeply")))
+                except error_type as e:
+                    err = error_type(wrap % (path, go_quote(str(e))))
+            return False, err, held.lines
 
         @functools.wraps(fn)
         def parse(path):
             cache = fsindex.scoped_cache(name)
             if cache is None:
-                try:
-                    return checked(path)
-                except error_type as e:
-                    log.debug(str(e))
-                    raise
-            key = (path, settings.ignore_environment, state.snapshot() if state is not None else None)
-            hit = cache.get(key)
-            if hit is None:
-                try:
-                    hit = (True, checked(path))
-                except error_type as e:
-                    hit = (False, e)
-                hit += (state.snapshot() if state is not None else None,)
-                cache[key] = hit
-            elif state is not None:
-                state.restore(hit[2])
+                hit = checked(path)
+            else:
+                key = (path, settings.ignore_environment, state.snapshot() if state is not None else None)
+                hit = cache.get(key)
+                if hit is None:
+                    hit = checked(path) + (state.snapshot() if state is not None else None,)
+                    cache[key] = hit
+                elif state is not None:
+                    state.restore(hit[3])
+            # the parse's own log lines (a loader warning) come again with every call
+            if hit[2]:
+                log.emit(hit[2])
             if hit[0]:
                 return hit[1]
             log.debug(str(hit[1]))

@@ -316,8 +316,8 @@ def _parse_v2(path):
         merged = _parse_service(svc, os.path.abspath(path), raw_services, lookup, path)
         try:
             services.append(_load_service(name, merged, base, version))
-        except (ValueError, TypeError) as e:  # bad port spec, memory size, ...
-            raise ComposeError("Failed to load service %s in %s: %s" % (name, path, e))
+        except (ValueError, TypeError) as e:  # utils.Convert's yaml decode: MemStringorInt's RAMInBytes
+            raise ComposeError(str(e)) from None
     services.sort(key=lambda s: s["name"])
     networks = {}
     project = _project_name(base)
@@ -422,7 +422,8 @@ def _load_service(name, d, base, version):
     s["group_add"] = _as_list_of_str(d.get("group_add"))
     s["stop_grace_period"] = _scalar_str(d.get("stop_grace_period") or "")
     mem = d.get("mem_limit")
-    s["mem_limit"] = cu.ram_in_bytes(mem) if mem not in (None, "") else 0
+    # MemStringorInt: an int, else the scalar's text through RAMInBytes ("" fails)
+    s["mem_limit"] = cu.ram_in_bytes(mem) if mem is not None else 0
     s["restart"] = _scalar_str(d.get("restart") or "")
     s["labels"] = _labels(d.get("labels"))
     s["hostname"] = _scalar_str(d.get("hostname") or "")

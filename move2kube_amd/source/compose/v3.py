@@ -15,6 +15,7 @@ from ...containerizer.reusedockerfile import ReuseDockerfileContainerizer
 from ...models import ir as irtypes
 from ...utils import common, log, yamlio
 from ...utils.constants import VOLUME_PREFIX
+from ...utils.log import go_quote
 from . import schema as cschema
 from . import utils as cu
 from .interpolate import EnvFileError, InterpolationError, interpolate_v3, parse_env_file
@@ -213,6 +214,48 @@ def _check_string_keys(v, prefix):
             _check_string_keys(x, "%s[%d]" % (prefix, i))
 
 
+def _external(spec):
+    ext = spec.get("external")
+    return isinstance(ext, dict) or bool(ext)
+
+
+def _version_ge(v, other):
+    """docker ``versions.GreaterThanOrEqualTo``: dotted fields compared as
+    integers (a non-number is 0)."""
+    def ints(x):
+        out = []
+        for f in x.split("."):
+            f = f.strip()
+            out.append(int(f) if f.isascii() and f.isdigit() else 0)
+        return out
+    a, b = ints(v), ints(other)
+    n = max(len(a), len(b))
+    return a + [0] * (n - len(a)) >= b + [0] * (n - len(b))
+
+
+def _external_name(kind, name, spec, version, deprecated_from):
+    """The ``external.name`` rules of ``LoadNetworks`` / ``LoadVolumes`` /
+    ``loadFileObjectConfig``: it conflicts with ``name``, is deprecated (a
+    warning) from ``deprecated_from`` on, and becomes the name; an external
+    object without either is named after its key."""
+    external = _external(spec)
+    out = {"name": _scalar_str(spec.get("name") or ""), "external": external}
+    if not external:
+        return out
+    ext = spec.get("external")
+    ext_name = _scalar_str(ext.get("name") or "") if isinstance(ext, dict) else ""
+    if ext_name:
+        if out["name"]:
+            raise ComposeError("%s %s: %s.external.name and %s.name conflict; only use %s.name"
+                               % (kind, name, kind, kind, kind))
+        if _version_ge(version, deprecated_from):
+            log.warning("%s %s: %s.external.name is deprecated in favor of %s.name", kind, name, kind, kind)
+        out["name"] = ext_name
+    elif not out["name"]:
+        out["name"] = name
+    return out
+
+
 @cu.command_memo("compose-v3", ComposeError, "Unable to load Compose file at path %s Error: %s")
 def parse_v3(path):
     """Parse and load a v3 compose file -> normalized config dict (``ParseV3``,
@@ -247,37 +290,124 @@ def parse_v3(path):
     wd = os.path.dirname(path)
     cfg = {"version": version, "services": [], "networks": {}, "volumes": parsed.get("volumes") or {},
            "secrets": {}, "configs": {}}
-    for name, spec in (parsed.get("networks") or {}).items():
-        spec = spec or {}
-        ext = spec.get("external")
-        external = bool(ext) if not isinstance(ext, dict) else True
-        net_name = spec.get("name") or ""
-        if external and isinstance(ext, dict) and ext.get("name"):
-            net_name = ext["name"]
-        elif external and not net_name:
-            net_name = name
-        cfg["networks"][name] = {"name": net_name, "external": external}
-    for kind in ("secrets", "configs"):
-        for name, spec in (parsed.get(kind) or {}).items():
-            spec = spec or {}
-            ext = spec.get("external")
-            external = bool(ext) if not isinstance(ext, dict) else True
-            f = spec.get("file") or ""
-            if f and not external:
-                f = cu.resolve_bind_source(f, wd)
-            cfg[kind][name] = {"file": f, "external": external, "name": spec.get("name") or ""}
+    # loadSections: services, networks, volumes, secrets, configs; the first error ends the load
     for sname in services:
         try:
             cfg["services"].append(_load_service(sname, services[sname] or {}, wd, env))
-        except EnvFileError as e:   # resolveEnvironment's error comes back as it is
+        except (ValueError, TypeError) as e:  # Transform / resolveEnvironment / resolveVolumePaths
             raise ComposeError(str(e)) from None
-        except (ValueError, TypeError) as e:  # bad port spec, duration, size, ...
-            raise ComposeError("Failed to load service %s in %s: %s" % (sname, path, e))
+    for name, spec in (parsed.get("networks") or {}).items():
+        cfg["networks"][name] = _external_name("network", name, spec or {}, version, "3.5")
+    for name, spec in (parsed.get("volumes") or {}).items():
+        spec = spec or {}
+        if _external(spec):
+            for key, present in (("driver", spec.get("driver")), ("driver_opts", spec.get("driver_opts")),
+                                 ("labels", spec.get("labels"))):
+                if present:
+                    raise ComposeError('conflicting parameters "external" and %s specified for volume %s'
+                                       % (go_quote(key), go_quote(name)))
+        _external_name("volume", name, spec, version, "3.4")
+    for kind in ("secrets", "configs"):
+        for name, spec in (parsed.get(kind) or {}).items():
+            spec = spec or {}
+            obj = _external_name(kind[:-1], name, spec, version, "3.5")
+            f = _scalar_str(spec.get("file") or "")
+            cfg[kind][name] = {"file": f if obj["external"] else cu.go_abs_path(wd, f), "external": obj["external"],
+                               "name": obj["name"]}
     cfg["services"].sort(key=lambda s: s["name"])
     return cfg
 
 
+def _go_type_name(v):
+    """``%T`` of a value go-yaml v2 decoded into interface{}."""
+    if isinstance(v, bool):
+        return "bool"
+    return {int: "int", float: "float64", str: "string", list: "[]interface {}"}.get(
+        type(v), "map[string]interface {}" if isinstance(v, dict) else "<nil>")
+
+
+def _transform_ports(entries):
+    """``transformServicePort`` over the list: the first bad entry's error."""
+    out = []
+    for p in entries:
+        if isinstance(p, dict):
+            out.append({"target": int(p.get("target") or 0), "published": int(p.get("published") or 0),
+                        "protocol": _scalar_str(p.get("protocol") or ""), "mode": _scalar_str(p.get("mode") or "")})
+        elif isinstance(p, (int, str)) and not isinstance(p, bool):
+            for tgt, pub, proto, mode in cu.to_service_port_configs(str(p)):
+                out.append({"target": tgt, "published": pub, "protocol": proto, "mode": mode})
+        else:
+            raise ValueError("invalid type %s for port" % _go_type_name(p))
+    return out
+
+
+def _transform(name, d):
+    """The values docker/cli's ``Transform`` (mapstructure with the loader's
+    transform hooks) can fail on, each under its field path; every failure is
+    collected and the lot is one ``mapstructure.Error`` (``N error(s)
+    decoding:`` and the sorted ``* error decoding '<path>': <cause>``
+    lines)."""
+    errs = []
+    out = {"ports": [], "memory": {}, "volumes": []}
+    if d.get("ports") is not None:
+        try:
+            out["ports"] = _transform_ports(d["ports"])
+        except ValueError as e:
+            errs.append("error decoding 'Ports': %s" % e)
+    res = (d.get("deploy") or {}).get("resources") or {}
+    for key in ("limits", "reservations"):
+        r = res.get(key)
+        if isinstance(r, dict) and r.get("memory") is not None:
+            try:
+                out["memory"][key] = cu.ram_in_bytes(r["memory"])
+            except ValueError as e:
+                errs.append("error decoding 'Deploy.Resources.%s.memory': %s" % (key.capitalize(), e))
+    for i, v in enumerate(d.get("volumes") or []):
+        if isinstance(v, dict):
+            out["volumes"].append({"type": _scalar_str(v.get("type") or "volume"),
+                                   "source": _scalar_str(v.get("source") or ""),
+                                   "target": _scalar_str(v.get("target") or ""), "read_only": bool(v.get("read_only"))})
+            continue
+        try:
+            if not isinstance(v, str):
+                raise ValueError("invalid type %s for service volume" % _go_type_name(v))
+            out["volumes"].append(cu.parse_volume_v3(v))
+        except ValueError as e:
+            errs.append("error decoding 'Volumes[%d]': %s" % (i, e))
+    if errs:
+        raise ComposeError("%d error(s) decoding:\n\n%s" % (len(errs), "\n".join(sorted("* " + e for e in errs))))
+    return out
+
+
+def _is_windows_abs(p):
+    """docker/cli loader ``isAbs`` (windows_path.go): ``C:\\x`` / ``C:/x``, or a UNC path."""
+    if len(p) >= 3 and p[0].isascii() and p[0].isalpha() and p[1] == ":" and p[2] in "\\/":
+        return True
+    return p.startswith("\\\\") or p.startswith("//")
+
+
+def _resolve_volume_paths(vols, wd, env):
+    """``resolveVolumePaths``: a bind mount needs a source; ``~`` is the
+    environment's HOME (a warning when it has none); a relative source is
+    joined to the compose file's directory."""
+    for vol in vols:
+        if vol["type"] != "bind":
+            continue
+        src = vol["source"]
+        if src == "":
+            raise ComposeError('invalid mount config for type "bind": field Source must not be empty')
+        if src.startswith("~"):
+            if "HOME" in env:
+                src = src.replace("~", env["HOME"], 1)
+            else:
+                log.warning("cannot expand '~', because the environment lacks HOME")
+        if not src.startswith("/") and not _is_windows_abs(src):
+            src = cu.go_abs_path(wd, src)
+        vol["source"] = src
+
+
 def _load_service(name, d, wd, env):
+    t = _transform(name, d)
     s = {"name": name}
     b = d.get("build")
     if isinstance(b, str):
@@ -307,15 +437,7 @@ def _load_service(name, d, wd, env):
     s["tmpfs"] = _as_list_of_str(d.get("tmpfs"))
     s["expose"] = _as_list_of_str(d.get("expose"))
     # ports
-    ports = []
-    for p in d.get("ports") or []:
-        if isinstance(p, dict):
-            ports.append({"target": int(p.get("target") or 0), "published": int(p.get("published") or 0),
-                          "protocol": _scalar_str(p.get("protocol") or ""), "mode": _scalar_str(p.get("mode") or "")})
-        else:
-            for host_ip, pub, tgt, proto in cu.parse_port_spec(_scalar_str(p)):
-                ports.append({"target": tgt, "published": pub, "protocol": proto, "mode": "ingress"})
-    s["ports"] = ports
+    s["ports"] = t["ports"]
     # environment: env_file contents first, then environment entries; bare keys from env
     environment = {}
     for ef in _as_list_of_str(d.get(cu.ENV_FILE)):
@@ -339,9 +461,8 @@ def _load_service(name, d, wd, env):
     for key in ("limits", "reservations"):
         r = res.get(key)
         if isinstance(r, dict):
-            mem = r.get("memory")
             deploy[key] = {"cpus": _scalar_str(r.get("cpus")) if r.get("cpus") is not None else "",
-                           "memory": cu.ram_in_bytes(mem) if mem is not None else 0}
+                           "memory": t["memory"].get(key, 0)}
     rp = dep.get("restart_policy")
     if isinstance(rp, dict):
         deploy["restart_condition"] = _scalar_str(rp.get("condition") or "")
@@ -369,17 +490,8 @@ def _load_service(name, d, wd, env):
                 items.append({"source": _scalar_str(it), "target": "", "mode": None})
         s[key] = items
     # volumes
-    vols = []
-    for v in d.get("volumes") or []:
-        if isinstance(v, dict):
-            vol = {"type": _scalar_str(v.get("type") or "volume"), "source": _scalar_str(v.get("source") or ""),
-                   "target": _scalar_str(v.get("target") or ""), "read_only": bool(v.get("read_only"))}
-        else:
-            vol = cu.parse_volume_v3(v)
-        if vol["type"] == "bind" and vol["source"]:
-            vol["source"] = cu.resolve_bind_source(vol["source"], wd)
-        vols.append(vol)
-    s["volumes"] = vols
+    _resolve_volume_paths(t["volumes"], wd, env)
+    s["volumes"] = t["volumes"]
     return s
 
 

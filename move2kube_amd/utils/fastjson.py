@@ -187,6 +187,35 @@ def _go_value(v, out):
         raise TypeError("json: unsupported type: %s" % type(v).__name__)
 
 
+def _go_value_indent(v, out, indent, depth):
+    if isinstance(v, dict) and v:
+        inner = "\n" + indent * (depth + 1)
+        out.append("{")
+        for i, (k, x) in enumerate(v.items()):
+            out.append(("," if i else "") + inner + _go_string(str(k)) + ": ")
+            _go_value_indent(x, out, indent, depth + 1)
+        out.append("\n" + indent * depth + "}")
+    elif isinstance(v, (list, tuple)) and v:
+        inner = "\n" + indent * (depth + 1)
+        out.append("[")
+        for i, x in enumerate(v):
+            out.append(("," if i else "") + inner)
+            _go_value_indent(x, out, indent, depth + 1)
+        out.append("\n" + indent * depth + "]")
+    else:
+        _go_value(v, out)
+
+
+def go_marshal_indent(v, indent):
+    """``json.MarshalIndent(v, "", indent)``: Go's escaping, ``": "`` after a
+    key, an empty object or array kept as ``{}`` / ``[]``, no trailing
+    newline; UTF-8 bytes.  Dicts are written in their own order (a Go map's
+    keys sorted, a struct's fields in declaration order: the caller's job)."""
+    out = []
+    _go_value_indent(v, out, indent, 0)
+    return "".join(out).encode("utf-8")
+
+
 def go_encode(v):
     """``json.NewEncoder(w).Encode(v)`` of a value whose dicts hold the Go
     struct's fields in declaration order: compact, HTML-escaped, one trailing

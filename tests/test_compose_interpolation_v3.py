@@ -140,3 +140,32 @@ def test_substitute_never_crashes():
         out, err = substitute_v3(value, ENV.get)
         assert isinstance(out, str) and (err is None or isinstance(err.template, str))
     check()
+
+
+@pytest.mark.parametrize("body,err", [
+    ("    healthcheck:\n      interval: 5x\n", "services.web.healthcheck.interval Does not match format 'duration'"),
+    ("    healthcheck:\n      start_period: 1\n", "services.web.healthcheck.start_period must be a string"),
+    ("    stop_grace_period: 1d\n", "services.web.stop_grace_period Does not match format 'duration'"),
+    ("    deploy:\n      restart_policy:\n        window: 10\n",
+     "services.web.deploy.restart_policy.window must be a string"),
+    ("    deploy:\n      update_config:\n        monitor: 1h1\n",
+     "services.web.deploy.update_config.monitor Does not match format 'duration'"),
+])
+def test_duration_format_fails_the_load(tmp_path, body, err):
+    """docker/cli's schema.go checks the "duration" format with
+    time.ParseDuration, so a bad duration refuses the whole file (v3.go:93-121)
+    instead of only its health check."""
+    p = tmp_path / "docker-compose.yaml"
+    p.write_text('version: "3.7"\nservices:\n  web:\n    image: nginx\n' + body)
+    with pytest.raises(v3.ComposeError) as ei:
+        v3.parse_v3(str(p))
+    assert str(ei.value) == 'Unable to load Compose file at path %s Error: "%s"' % (p, err)
+
+
+def test_durations_from_the_environment(tmp_path, monkeypatch):
+    monkeypatch.setenv("HC", "1m30s")
+    p = tmp_path / "docker-compose.yaml"
+    p.write_text('version: "3.7"\nservices:\n  web:\n    image: nginx\n    stop_grace_period: 2h45m.5s\n'
+                 '    healthcheck:\n      interval: ${HC}\n      timeout: "-1.5us"\n')
+    (svc,) = v3.parse_v3(str(p))["services"]
+    assert svc["healthcheck"]["interval"] == "1m30s"

@@ -8,6 +8,8 @@ import os
 
 import pytest
 
+import logparse
+
 from move2kube_amd.source.compose import utils as cu
 
 S, MS, US, M, H = 10 ** 9, 10 ** 6, 10 ** 3, 60 * 10 ** 9, 3600 * 10 ** 9
@@ -50,16 +52,23 @@ def test_parse_duration_errors_like_go(text, err):
 @pytest.mark.parametrize("v,want", [
     (512, 512), (1.5, 1), ("512", 512), ("32k", 32 * 1024), ("32kb", 32 * 1024), ("32Ki", 32 * 1024),
     ("32KiB", 32 * 1024), ("1.5m", int(1.5 * 1024 ** 2)), ("2g", 2 * 1024 ** 3), ("1 t", 1024 ** 4),
-    ("1p", 1024 ** 5), (" 7b ", 7),
+    ("1p", 1024 ** 5), ("7b", 7), ("0012.50M", int(12.5 * 1024 ** 2)),
 ])
 def test_ram_in_bytes(v, want):
     assert cu.ram_in_bytes(v) == want
 
 
-@pytest.mark.parametrize("v", [True, "", "abc", "1x", "-1m"])
-def test_ram_in_bytes_errors(v):
-    with pytest.raises(ValueError):
+@pytest.mark.parametrize("v,err", [
+    (True, "invalid size"), ("", "invalid size: ''"), ("abc", "invalid size: 'abc'"), ("1x", "invalid size: '1x'"),
+    ("-1m", "invalid size: '-1m'"), (" 7b ", "invalid size: ' 7b '"), ("5m\n", "invalid size: '5m\n'"),
+    ("\u0661m", "invalid size: '\u0661m'"), ("1.2.3k", 'strconv.ParseFloat: parsing "1.2.3": invalid syntax'),
+])
+def test_ram_in_bytes_errors(v, err):
+    """go-units v0.4.0 parseSize: RE2 semantics (ASCII digits, ``$`` at the
+    very end, no trimming), then ParseFloat of the number part."""
+    with pytest.raises(ValueError) as ei:
         cu.ram_in_bytes(v)
+    assert str(ei.value) == err
 
 
 @pytest.mark.parametrize("milli,want", [
@@ -82,22 +91,55 @@ def test_shell_split():
 
 
 @pytest.mark.parametrize("spec,want", [
-    ("80", [("", 0, 80, "tcp")]),
-    ("8080:80/UDP", [("", 8080, 80, "udp")]),
-    ("127.0.0.1:8080:80", [("127.0.0.1", 8080, 80, "tcp")]),
-    ("3000-3001:4000-4001", [("", 3000, 4000, "tcp"), ("", 3001, 4001, "tcp")]),
-    ("9000:4000-4001", [("", 9000, 4000, "tcp"), ("", 9000, 4001, "tcp")]),
-    ("[::1]:8080:80", [("::1", 8080, 80, "tcp")]),
-    ("80/", [("", 0, 80, "tcp")]),
+    ("80", [(80, 0, "tcp", "ingress")]),
+    (80, [(80, 0, "tcp", "ingress")]),
+    ("8080:80/UDP", [(80, 8080, "udp", "ingress")]),
+    ("127.0.0.1:8080:80", [(80, 8080, "tcp", "ingress")]),
+    ("3000-3001:4000-4001", [(4000, 3000, "tcp", "ingress"), (4001, 3001, "tcp", "ingress")]),
+    ("8000-8002:80", [(80, 8000, "tcp", "ingress"), (80, 8001, "tcp", "ingress"), (80, 8002, "tcp", "ingress")]),
+    ("9-10:9-10", [(10, 10, "tcp", "ingress"), (9, 9, "tcp", "ingress")]),     # "10/tcp" sorts first
+    ("[::1]:8080:80", [(80, 8080, "tcp", "ingress")]),
+    ("80/", [(80, 0, "tcp", "ingress")]),
+    ("80/sctp/x", [(80, 0, "sctp", "ingress")]),
+    (":80", [(80, 0, "tcp", "ingress")]),
+    ("1.2.3.4::80", [(80, 0, "tcp", "ingress")]),
+    ("010.1.1.1:1:1", [(1, 1, "tcp", "ingress")]),
 ])
-def test_parse_port_spec(spec, want):
-    assert cu.parse_port_spec(spec) == want
+def test_to_service_port_configs(spec, want):
+    """docker/cli toServicePortConfigs over go-connections nat (v0.4.0)."""
+    assert cu.to_service_port_configs(str(spec)) == want
 
 
-@pytest.mark.parametrize("spec", ["8080:", "[::1:8080:80", "5-3", "1-3:4-5", "a:b:c:d"])
-def test_parse_port_spec_errors(spec):
-    with pytest.raises(ValueError):
-        cu.parse_port_spec(spec)
+@pytest.mark.parametrize("spec,err", [
+    ("8080:", "No port specified: 8080:<empty>"),
+    ("", "No port specified: <empty>"),
+    ("[::1:8080:80", "Invalid ip address [::1: address [::1:: missing ']' in address"),
+    ("::1:8080:80", "Invalid ip address ::1: address ::1:: too many colons in address"),
+    ("1.2.3:80:80", "Invalid ip address: 1.2.3"),
+    ("fe80::1%eth0:80:80", "Invalid ip address fe80::1%eth0: address fe80::1%eth0:: too many colons in address"),
+    ("5-3", "Invalid containerPort: 5-3"),
+    ("70000", "Invalid containerPort: 70000"),
+    ("+80", "Invalid containerPort: +80"),
+    ("abc:80", "Invalid hostPort: abc"),
+    ("1-3:4-5", "Invalid ranges specified for container and host Ports: 4-5 and 1-3"),
+    ("9000:4000-4001", "Invalid ranges specified for container and host Ports: 4000-4001 and 9000"),
+    ("80/xyz", "Invalid proto: xyz"),
+    ("a:b:c:d", "Invalid ip address a:b: address a:b:: too many colons in address"),
+])
+def test_port_spec_errors(spec, err):
+    with pytest.raises(ValueError) as ei:
+        cu.to_service_port_configs(spec)
+    assert str(ei.value) == err
+
+
+def test_host_ip_warning(capsys):
+    """opts.ConvertPortToPortConfig warns for a host IP other than 0.0.0.0."""
+    cu.to_service_port_configs("0.0.0.0:80:80")
+    cu.to_service_port_configs("127.0.0.1:8000-8001:80/udp")
+    err = capsys.readouterr().err
+    assert err.count("level=warning") == 1
+    assert logparse.logged(err, "ignoring IP-address (127.0.0.1:8000-8001:80/udp) service will listen on "
+                                "'0.0.0.0'", "warning")
 
 
 @pytest.mark.parametrize("spec,want", [
@@ -106,14 +148,29 @@ def test_parse_port_spec_errors(spec):
     ("./src:/app:ro", {"type": "bind", "source": "./src", "target": "/app", "read_only": True}),
     ("~/x:/app:ro,rw", {"type": "bind", "source": "~/x", "target": "/app", "read_only": False}),
     ("/abs:/app:z", {"type": "bind", "source": "/abs", "target": "/app", "read_only": False}),
+    ("v:/data", {"type": "volume", "source": "", "target": "v:/data", "read_only": False}),   # a drive letter
+    ("c:/d:/data", {"type": "bind", "source": "c:/d", "target": "/data", "read_only": False}),
+    ("a:", {"type": "volume", "source": "", "target": "a:", "read_only": False}),           # two characters
+    ("data:/x:nocopy,ro", {"type": "volume", "source": "data", "target": "/x", "read_only": True}),
 ])
 def test_parse_volume(spec, want):
+    """docker/cli loader.ParseVolume (cli/compose/loader/volume.go)."""
     assert cu.parse_volume_v3(spec) == want
 
 
-def test_resolve_bind_source(monkeypatch, tmp_path):
-    monkeypatch.setenv("HOME", str(tmp_path / "home"))
-    assert cu.resolve_bind_source("~/data", "/w") == str(tmp_path / "home" / "data")
-    assert cu.resolve_bind_source("./a/../b", "/w") == "/w/b"
-    assert cu.resolve_bind_source("/abs", "/w") == "/abs"
-    assert os.path.isabs(cu.resolve_bind_source("rel", str(tmp_path)))
+@pytest.mark.parametrize("spec,err", [
+    ("", "invalid empty volume spec"),
+    ("vol::/x", "invalid spec: vol::/x: empty section between colons"),
+    ("vol:/x:ro:z", "invalid spec: vol:/x:ro:z: too many colons"),
+])
+def test_parse_volume_errors(spec, err):
+    with pytest.raises(ValueError) as ei:
+        cu.parse_volume_v3(spec)
+    assert str(ei.value) == err
+
+
+def test_abs_path():
+    assert cu.go_abs_path("/w", "./a/../b") == "/w/b"
+    assert cu.go_abs_path("/w", "/abs") == "/abs"
+    assert cu.go_abs_path("/w", "") == "/w"
+    assert cu.go_abs_path("/w", "~/x") == "/w/~/x"

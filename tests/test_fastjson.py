@@ -98,3 +98,14 @@ def test_errors_inside_containers_without_the_json_package():
     assert out.splitlines() == ["unexpected end of JSON input", "invalid character '2' after array element",
                                 "invalid character ']' looking for beginning of value",
                                 "invalid character '1' after object key"]
+
+
+def test_go_marshal_indent():
+    """json.MarshalIndent(v, "", "\\t") as docker/cli's SaveToWriter writes a
+    config file (configfile/file.go): Go's escapes, no trailing newline,
+    empty containers kept compact."""
+    from move2kube_amd.utils import fastjson
+    got = fastjson.go_marshal_indent({"auths": {"r<é>&": {}, "b": {"auth": "x"}}, "l": [], "n": [1, None]}, "\t")
+    assert got == ('{\n\t"auths": {\n\t\t"r\\u003cé\\u003e\\u0026": {},\n\t\t"b": {\n\t\t\t"auth": "x"\n\t\t}\n\t},'
+                   '\n\t"l": [],\n\t"n": [\n\t\t1,\n\t\tnull\n\t]\n}').encode()
+    assert fastjson.go_marshal_indent({}, "  ") == b"{}"

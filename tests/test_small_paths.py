@@ -85,3 +85,40 @@ def test_dockerfile_translate_debug_lines(tmp_path, capsys):
     assert logparse.logged(err, "The service x has translation type %s . Expected %s . Skipping."
                            % (plantypes.ANY2KUBE, plantypes.DOCKERFILE2KUBE), "debug")
     assert logparse.logged(err, "Translating %s" % svc.service_name, "debug")
+
+
+def test_plugin_type_names_in_log_lines(monkeypatch, capsys):
+    """``[%T] Begin ...`` / ``[%T] Failed : %s`` name the Go types of the
+    reference's plugin lists: optimizer.go:31-33 (package ``optimize``),
+    customizer.go:30-32, parameterizer.go:30-32 (package ``parameterize``)."""
+    from move2kube_amd import customizer, optimizer, parameterizer
+    assert [optimizer._go_type(o) for o in optimizer.get_optimizers()] == [
+        "*optimize.normalizeCharacterOptimizer", "*optimize.ingressOptimizer", "*optimize.replicaOptimizer",
+        "*optimize.imagePullPolicyOptimizer", "*optimize.portMergeOptimizer"]
+    assert [customizer._go_type(c) for c in customizer.get_customizers()] == [
+        "*customizer.registryCustomizer", "*customizer.storageCustomizer", "*customizer.ingressCustomizer"]
+    assert [parameterizer._go_type(p) for p in parameterizer.get_parameterizers()] == [
+        "*parameterize.imageNameParameterizer", "*parameterize.storageClassParameterizer",
+        "*parameterize.ingressParameterizer"]
+
+    class StorageCustomizer:
+        def customize(self, ir):
+            raise ValueError("No storage classes available in the cluster")
+
+    class ReplicaOptimizer:
+        def optimize(self, ir):
+            raise ValueError("x")
+
+    monkeypatch.setattr(customizer, "get_customizers", lambda: [StorageCustomizer()])
+    monkeypatch.setattr(optimizer, "get_optimizers", lambda: [ReplicaOptimizer()])
+    log.set_verbose(True)
+    try:
+        customizer.customize(object())
+        optimizer.optimize(object())
+    finally:
+        log.set_verbose(False)
+    err = capsys.readouterr().err
+    assert logparse.logged(err, "[*customizer.storageCustomizer] Begin Customization", "debug")
+    assert logparse.logged(err, "[*customizer.storageCustomizer] Failed : No storage classes available in the "
+                                "cluster", "warning")
+    assert logparse.logged(err, "[*optimize.replicaOptimizer] Failed : x", "warning")
