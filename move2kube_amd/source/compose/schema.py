@@ -103,7 +103,7 @@ _TOP_NETWORK = _or(NULL, _obj(name=STR, driver=STR, driver_opts=_map(STR_OR_NUM)
                               ipam=_obj(driver=STR, config=_list(_map(_or(STR, NUM, NULL))))))
 _TOP_FILE = _or(NULL, _obj(name=STR, file=STR, external=EXTERNAL, labels=LIST_OR_DICT, template_driver=STR))
 
-V3_TOP = _obj(version=_or(STR, NUM), services=_or(NULL, _map(_or(NULL, V3_SERVICE))),
+V3_TOP = _obj(version=_or(STR, NUM), services=_or(NULL, _map(V3_SERVICE)),
               volumes=_or(NULL, _map(_TOP_VOLUME)), networks=_or(NULL, _map(_TOP_NETWORK)),
               secrets=_or(NULL, _map(_TOP_FILE)), configs=_or(NULL, _map(_TOP_FILE)))
 

@@ -15,6 +15,7 @@ from ...containerizer.reusedockerfile import ReuseDockerfileContainerizer
 from ...models import ir as irtypes
 from ...utils import common, log, yamlio
 from ...utils.constants import VOLUME_PREFIX
+from ...utils.lazyre import lazy as _lazy_re
 from ...utils.log import go_quote
 from . import schema as cschema
 from . import utils as cu
@@ -148,6 +149,9 @@ def _labels(v):
     return {k: (x if x is not None else "") for k, x in m.items()}
 
 
+_SERVICE_NAME_RE = _lazy_re(r"^[a-zA-Z0-9._-]+\Z")
+
+
 def _validate(d):
     if not isinstance(d, dict):
         raise ComposeError("Top-level object must be a mapping")
@@ -155,7 +159,8 @@ def _validate(d):
         if not isinstance(k, str):
             raise ComposeError("Non-string key at top level: %r" % (k,))
         if k not in TOP_KEYS and not k.startswith("x-"):
-            raise ComposeError("Additional property %s is not allowed" % k)
+            # gojsonschema names the root context "(root)"
+            raise ComposeError("(root) Additional property %s is not allowed" % k)
     services = d.get("services")
     if not isinstance(services, dict):
         if "services" in d and services is None:
@@ -165,8 +170,10 @@ def _validate(d):
         else:
             services = {}
     for sname, svc in services.items():
-        if svc is None:
-            continue
+        # "services": patternProperties ^[a-zA-Z0-9._-]+$, additionalProperties false;
+        # a service is "type": "object" (null included: LoadServices would not survive it)
+        if not _SERVICE_NAME_RE.match(str(sname)):
+            raise ComposeError("services Additional property %s is not allowed" % sname)
         if not isinstance(svc, dict):
             raise ComposeError("services.%s must be a mapping" % sname)
         for k in svc:
@@ -446,8 +453,10 @@ def _load_service(name, d, wd, env):
             environment[k] = v
     for k, v in _mapping_with_equals(d.get("environment")).items():
         environment[k] = v
+    # updateEnvironment: a key with no value or an empty one takes the loader's environment
+    # ("lookupEnv is prioritized over the file content")
     for k, v in list(environment.items()):
-        if v is None and k in env:
+        if (v is None or v == "") and k in env:
             environment[k] = env[k]
     s["environment"] = environment
     # networks

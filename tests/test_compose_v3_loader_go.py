@@ -119,3 +119,31 @@ def test_v2_memory_errors(tmp_path, mem, err):
     with pytest.raises(v1v2.ComposeError) as ei:
         v1v2.parse_v2(str(p))
     assert str(ei.value) == 'Failed to load docker compose file at path %s Error: "%s"' % (p, err)
+
+
+def test_empty_environment_values_take_the_loader_environment(tmp_path, monkeypatch):
+    """resolveEnvironment / updateEnvironment: ``K``, ``K=`` and ``K: ""``
+    (from the service or an env file) take the value the loader's
+    environment has for K; a value that is set stays."""
+    monkeypatch.setenv("A", "os-a")
+    monkeypatch.setenv("B", "os-b")
+    monkeypatch.setenv("C", "os-c")
+    monkeypatch.delenv("D", raising=False)
+    (tmp_path / "e.env").write_text("A=\nE=\n")
+    p = _load(tmp_path, "services:\n  web:\n    image: x\n    env_file: e.env\n"
+                        "    environment:\n      - B=\n      - C\n      - D=\n      - F=set\n")
+    (svc,) = v3.parse_v3(str(p))["services"]
+    assert svc["environment"] == {"A": "os-a", "E": "", "B": "os-b", "C": "os-c", "D": "", "F": "set"}
+
+
+@pytest.mark.parametrize("body,err", [
+    ("services:\n  web:\n", "services.web must be a mapping"),
+    ('services:\n  "my web":\n    image: x\n', "services Additional property my web is not allowed"),
+    ("services:\n  w\u00e9b:\n    image: x\n", "services Additional property w\u00e9b is not allowed"),
+    ("services:\n  web:\n    image: x\nhelicopters: {}\n", "(root) Additional property helicopters is not allowed"),
+])
+def test_schema_service_map(tmp_path, body, err):
+    """config_schema_v3.x.json: a service is an object, its name matches
+    ``^[a-zA-Z0-9._-]+$`` (additionalProperties false); gojsonschema's root
+    context is ``(root)``."""
+    assert _err(tmp_path, body) == '"%s"' % err
