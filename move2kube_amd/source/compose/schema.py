@@ -123,8 +123,6 @@ def _human(t):
 
 
 def _type_name(spec):
-    if spec == DURATION:
-        return STR
     if isinstance(spec, str):
         return spec
     if spec[0] == "or":
@@ -154,9 +152,8 @@ def _matches_scalar(v, t):
 
 
 def _shape_ok(v, spec):
-    """Does ``v`` have the outer shape of ``spec`` (used to pick an alternative)."""
-    if spec == DURATION:
-        return isinstance(v, str)
+    """Does ``v`` have the outer shape of ``spec`` (used to pick an alternative;
+    DURATION is never one)."""
     if isinstance(spec, str):
         return _matches_scalar(v, spec)
     kind = spec[0]
@@ -220,3 +217,12 @@ def validate_v3(doc):
 
 def validate_v2_service(name, svc):
     check(svc, V2_SERVICE, name)
+    # libcompose registers a "ports" format checker that runs nat.ParsePortSpecs on
+    # each string entry (numbers are not format-checked)
+    from .utils import parse_port_spec
+    for i, p in enumerate(svc.get("ports") or []):
+        if isinstance(p, str):
+            try:
+                parse_port_spec(p)
+            except ValueError:
+                raise SchemaError("%s.ports.%d Does not match format 'ports'" % (name, i)) from None

@@ -64,6 +64,10 @@ class _GoQ(str):
 
 
 def _format(msg, args):
+    if any(type(a) in (list, dict) for a in args):
+        # a slice or map argument prints as Go's %v / %s does ([a b], map[k:v])
+        from .gofmt import sprint_one
+        args = tuple(sprint_one(a) if type(a) in (list, dict) else a for a in args)
     if "%r" in msg:
         args = tuple(_GoQ(a) if type(a) is str else a for a in args)
     return msg % args

@@ -174,3 +174,33 @@ def test_abs_path():
     assert cu.go_abs_path("/w", "/abs") == "/abs"
     assert cu.go_abs_path("/w", "") == "/w"
     assert cu.go_abs_path("/w", "~/x") == "/w/~/x"
+
+
+@pytest.mark.parametrize("hostport,want", [
+    ("a:", ("a", "")), ("[::1]:80", ("::1", "80")), (":", ("", "")),
+    ("x", "address x: missing port in address"),
+    ("[::1]", "address [::1]: missing port in address"),
+    ("[::1", "address [::1: missing ']' in address"),
+    ("[a]b:", "address [a]b:: missing port in address"),
+    ("[::1]:x:", "address [::1]:x:: too many colons in address"),
+    ("a:b:", "address a:b:: too many colons in address"),
+    ("a[b:", "address a[b:: unexpected '[' in address"),
+    ("a]b:", "address a]b:: unexpected ']' in address"),
+])
+def test_split_host_port(hostport, want):
+    """net.SplitHostPort (Go 1.15) and its *net.AddrError texts."""
+    if isinstance(want, tuple):
+        assert cu._split_host_port(hostport) == want
+    else:
+        with pytest.raises(ValueError) as ei:
+            cu._split_host_port(hostport)
+        assert str(ei.value) == want
+
+
+@pytest.mark.parametrize("ip,ok", [
+    ("1.2.3.4", True), ("001.02.3.255", True), ("1.2.3.4.5", False), ("1..2.3", False), ("256.1.1.1", False),
+    ("1.2.3", False), ("::1", True), ("::ffff:1.2.3.4", True), ("fe80::1%eth0", False), ("::zz", False),
+    ("abc", False), ("", False),
+])
+def test_go_parse_ip(ip, ok):
+    assert cu.go_parse_ip_ok(ip) is ok

@@ -147,3 +147,25 @@ def test_schema_service_map(tmp_path, body, err):
     ``^[a-zA-Z0-9._-]+$`` (additionalProperties false); gojsonschema's root
     context is ``(root)``."""
     assert _err(tmp_path, body) == '"%s"' % err
+
+
+def test_v2_ports_format(tmp_path):
+    """libcompose's "ports" format checker (nat.ParsePortSpecs on string
+    entries) refuses the file; a number is not format-checked."""
+    p = _load(tmp_path, 'services:\n  web:\n    image: x\n    ports:\n      - 80\n      - "abc:80"\n', "2")
+    with pytest.raises(v1v2.ComposeError, match=r"web\.ports\.1 Does not match format 'ports'"):
+        v1v2.parse_v2(str(p))
+    p = _load(tmp_path, 'services:\n  web:\n    image: x\n    ports:\n      - 80\n      - "8000-8001:80"\n', "2")
+    assert v1v2.parse_v2(str(p))["services"][0]["ports"] == ["80", "8000-8001:80"]
+
+
+def test_probe_without_command_warning(capsys):
+    """getHealthCheck's warning prints the HealthCheckTest slice as Go does."""
+    from move2kube_amd.source.compose.v3 import V3Loader
+    V3Loader.get_health_check({"test": ["NONE"], "timeout": None, "interval": None, "retries": None,
+                               "start_period": None})
+    V3Loader.get_health_check({"test": [], "timeout": None, "interval": None, "retries": None,
+                               "start_period": None})
+    err = capsys.readouterr().err
+    assert logparse.logged(err, "Could not find command to execute in probe : [NONE]", "warning")
+    assert logparse.logged(err, "Could not find command to execute in probe : []", "warning")
