@@ -81,7 +81,9 @@ _FUZZ_INNER = ["target", "published", "source", "type", "mode", "resources", "li
                "size", "protocol", "x-a"]
 _FUZZ_SCALARS = [None, True, False, 0, 1, -5, 80, 1.5, "", "x", "80:80", "1g", "a=b", "/tmp:/x:ro",
                  "8080-8081:80-81", "udp", "10s", "${X}", "$$", "CMD-SHELL", "127.0.0.1:5000:5000/udp",
-                 "${N:-3}", "${B:-yes}", "${F:-0.5}", "$", "${X:?needed}", "${X-a}b", "$1"]
+                 "${N:-3}", "${B:-yes}", "${F:-0.5}", "$", "${X:?needed}", "${X-a}b", "$1",
+                 "v:/x", "a::b", "8000-8002:80", "80/xyz", "5zz", "1.2.3m", "~/x:/y", "1m30s", "5x",
+                 "[::1]:80:80", "::1:80:80", "0.0.0.0:1-2:3-4/sctp", "my web"]
 
 
 def _fuzz_value(rng, depth=0):
