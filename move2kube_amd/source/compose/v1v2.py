@@ -18,6 +18,7 @@ from ...containerizer.reusedockerfile import ReuseDockerfileContainerizer
 from ...models import ir as irtypes
 from ...utils import common, log, yamlio
 from ...utils.constants import VOLUME_PREFIX, settings
+from ...utils.lazyre import lazy as _lazy_re
 from . import schema as cschema
 from . import utils as cu
 from .interpolate import EnvFileError, InterpolationError, interpolate_v1v2, parse_env_file
@@ -149,11 +150,18 @@ def _prune_env_files(raw_services, compose_path):
             svc[cu.ENV_FILE] = kept
 
 
+_SERVICE_NAME_RE = _lazy_re(r"^[a-zA-Z0-9._-]+\Z")
+
+
 def _validate(raw_services, version):
     allowed = V2_SERVICE_KEYS if version else V1_SERVICE_KEYS
     for name, svc in raw_services.items():
         if not isinstance(name, str):
             raise ComposeError("Non-string service name %r" % (name,))
+        # the services schema: patternProperties ^[a-zA-Z0-9._-]+$, additionalProperties
+        # false; libcompose words it as an unsupported option of the "(root)" service
+        if not _SERVICE_NAME_RE.match(name):
+            raise ComposeError("Unsupported config option for (root) service: '%s'" % name)
         if not isinstance(svc, dict):
             raise ComposeError("Service %s has neither an image nor a build context specified" % name
                                if svc is None else "Invalid type for service %s" % name)

@@ -169,3 +169,17 @@ def test_probe_without_command_warning(capsys):
     err = capsys.readouterr().err
     assert logparse.logged(err, "Could not find command to execute in probe : [NONE]", "warning")
     assert logparse.logged(err, "Could not find command to execute in probe : []", "warning")
+
+
+@pytest.mark.parametrize("version", ["2", None])
+def test_v1v2_service_names(tmp_path, version):
+    """libcompose validates the services map against a schema whose service
+    names match ^[a-zA-Z0-9._-]+$ (additionalProperties false)."""
+    p = tmp_path / "docker-compose.yaml"
+    body = '"my web":\n  image: x\n'
+    if version:
+        p.write_text('version: "2"\nservices:\n' + "".join("  " + ln + "\n" for ln in body.splitlines()))
+    else:
+        p.write_text(body)
+    with pytest.raises(v1v2.ComposeError, match=r"Unsupported config option for \(root\) service: 'my web'"):
+        v1v2.parse_v2(str(p))
