@@ -63,11 +63,30 @@ class _GoQ(str):
         return go_quote(self)
 
 
+class _GoVal:
+    """A slice or map argument: ``%s`` prints Go's ``%v`` (``[a b]``,
+    ``map[k:v]``), ``%r`` Go's ``%q`` (``["a" "b"]``)."""
+
+    __slots__ = ("v", "q")
+
+    def __init__(self, a):
+        from .gofmt import sprint_one
+        self.v = sprint_one(a)
+        if type(a) is list:
+            self.q = "[" + " ".join(go_quote(x) if type(x) is str else sprint_one(x) for x in a) + "]"
+        else:
+            self.q = self.v
+
+    def __str__(self):
+        return self.v
+
+    def __repr__(self):
+        return self.q
+
+
 def _format(msg, args):
     if any(type(a) in (list, dict) for a in args):
-        # a slice or map argument prints as Go's %v / %s does ([a b], map[k:v])
-        from .gofmt import sprint_one
-        args = tuple(sprint_one(a) if type(a) in (list, dict) else a for a in args)
+        args = tuple(_GoVal(a) if type(a) in (list, dict) else a for a in args)
     if "%r" in msg:
         args = tuple(_GoQ(a) if type(a) is str else a for a in args)
     return msg % args

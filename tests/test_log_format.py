@@ -8,6 +8,8 @@ import subprocess
 import sys
 import time
 
+import logparse
+
 from move2kube_amd.utils import log
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -121,3 +123,12 @@ def test_failed_object_and_container_writes_print_go_path_errors(tmp_path, capsy
     assert ("error", 'Failed to write "Service" Error: "open %s/web-service.yaml: is a directory"' % tmp_path) in msgs
     assert ("warning", "Error writing file at %s/containers/svc/Dockerfile.svc : open %s/containers/svc/Dockerfile.svc: "
             "is a directory" % (tmp_path, tmp_path)) in msgs
+
+
+def test_slice_and_map_arguments_print_as_go(capsys):
+    """A []string argument prints as fmt's %v ([a b]) under %s and as %q
+    (["a b" "c"]) under %r; a map as map[k:v] with sorted keys."""
+    from move2kube_amd.utils import log
+    log.warning("a %s b %r c %s d %r", ["x y", "z"], ["x y", "z"], {"b": 1, "a": [2]}, "q")
+    err = capsys.readouterr().err
+    assert logparse.logged(err, 'a [x y z] b ["x y" "z"] c map[a:[2] b:1] d "q"', "warning")
