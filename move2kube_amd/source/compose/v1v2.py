@@ -150,6 +150,11 @@ def _prune_env_files(raw_services, compose_path):
             svc[cu.ENV_FILE] = kept
 
 
+# libcompose's dockerConfigHints (config/validation.go), after docker-compose's
+_CONFIG_HINTS = {"cpu_share": "cpu_shares", "add_host": "extra_hosts", "hosts": "extra_hosts",
+                 "extra_host": "extra_hosts", "device": "devices", "link": "links", "memory_swap": "memswap_limit",
+                 "port": "ports", "privilege": "privileged", "priviliged": "privileged", "privilige": "privileged",
+                 "volume": "volumes", "workdir": "working_dir"}
 _SERVICE_NAME_RE = _lazy_re(r"^[a-zA-Z0-9._-]+\Z")
 
 
@@ -167,7 +172,9 @@ def _validate(raw_services, version):
                                if svc is None else "Invalid type for service %s" % name)
         for k in svc:
             if k not in allowed:
-                raise ComposeError("Unsupported config option for %s service: '%s'" % (name, k))
+                hint = _CONFIG_HINTS.get(k)
+                raise ComposeError("Unsupported config option for %s service: '%s'" % (name, k)
+                                   + (" (did you mean '%s'?)" % hint if hint else ""))
         try:
             cschema.validate_v2_service(name, svc)
         except cschema.SchemaError as e:

@@ -183,3 +183,16 @@ def test_v1v2_service_names(tmp_path, version):
         p.write_text(body)
     with pytest.raises(v1v2.ComposeError, match=r"Unsupported config option for \(root\) service: 'my web'"):
         v1v2.parse_v2(str(p))
+
+
+@pytest.mark.parametrize("key,msg", [
+    ("workdir", "Unsupported config option for web service: 'workdir' (did you mean 'working_dir'?)"),
+    ("port", "Unsupported config option for web service: 'port' (did you mean 'ports'?)"),
+    ("colour", "Unsupported config option for web service: 'colour'"),
+])
+def test_v2_unsupported_option_hints(tmp_path, key, msg):
+    """libcompose's unsupportedConfigMessage adds dockerConfigHints' guess."""
+    p = _load(tmp_path, "services:\n  web:\n    image: x\n    %s: y\n" % key, "2")
+    with pytest.raises(v1v2.ComposeError) as ei:
+        v1v2.parse_v2(str(p))
+    assert msg in str(ei.value)
